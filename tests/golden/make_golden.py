@@ -1,0 +1,276 @@
+"""Generate golden vectors by running the reference's own Python code.
+
+Run in the build container (needs /root/reference, read-only):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+The reference is imported from /root/reference with three shims for modules
+absent from this environment:
+  * cv2          -> oracle.cv_resize (the OpenCV INTER_CUBIC restatement; so the
+                    resize arithmetic is a shared input, "parity unpinned")
+  * torchvision  -> empty stub (body.py imports `transforms` but never uses it)
+  * skimage      -> skimage.measure.label = scipy.ndimage.label with a 3x3
+                    structure (8-connectivity, raster-order numbering)
+Reference networks get synthetic weights (islpose.synth) through the
+reference's own util.transfer + load_state_dict; Body / Hand instances are
+built with __new__ and a stub model that replays designed low-resolution
+maps, so post-processing runs on controlled inputs.
+
+Outputs (compressed .npz, data only) go next to this script.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "isl-signlanguage-translation_amd"))
+
+from oracle import cv_resize  # noqa: E402
+from islpose import synth  # noqa: E402
+
+
+def install_shims():
+    cv2 = types.ModuleType("cv2")
+    cv2.INTER_CUBIC = 2
+
+    def resize(img, dsize, fx=None, fy=None, interpolation=None):
+        assert interpolation == 2
+        return cv_resize.resize(img, tuple(dsize), fx=fx, fy=fy)
+    cv2.resize = resize
+    sys.modules["cv2"] = cv2
+    tv = types.ModuleType("torchvision")
+    tvt = types.ModuleType("torchvision.transforms")
+    tv.transforms = tvt
+    sys.modules["torchvision"] = tv
+    sys.modules["torchvision.transforms"] = tvt
+    from scipy import ndimage
+    sk = types.ModuleType("skimage")
+    skm = types.ModuleType("skimage.measure")
+
+    def label(binary, return_num=False, connectivity=None):
+        assert connectivity == binary.ndim
+        lab, n = ndimage.label(binary, structure=np.ones((3,) * binary.ndim, np.int32))
+        lab = lab.astype(np.int64)
+        return (lab, n) if return_num else lab
+    skm.label = label
+    sk.measure = skm
+    sys.modules["skimage"] = sk
+    sys.modules["skimage.measure"] = skm
+    sys.path.insert(0, REF)
+
+
+def load_ref_model(cls, kind):
+    from src import util
+    m = cls()
+    w = {k: torch.from_numpy(v) for k, v in synth.synth_weights(kind, seed=0).items()}
+    m.load_state_dict(util.transfer(m, w))
+    m.eval()
+    return m
+
+
+def frame_input(h, w, seed):
+    f = synth.synth_frames(1, h, w, seed=seed)[0]
+    return np.ascontiguousarray(np.transpose(np.float32(f[:, :, :, None]), (3, 2, 0, 1)) / 256 - 0.5)
+
+
+def g1_networks():
+    from src.model import bodypose_25_model, bodypose_model, handpose_model
+    from PIL import Image
+    out = {}
+    torch.set_num_threads(8)
+    body = load_ref_model(bodypose_25_model, 0)
+    for (h, w, seed) in ((184, 328, 1), (50, 70, 2)):
+        x = frame_input(h, w, seed)
+        with torch.no_grad():
+            paf, heat = body(torch.from_numpy(x))
+        out["body25_%dx%d_paf" % (h, w)] = paf.numpy()
+        out["body25_%dx%d_heat" % (h, w)] = heat.numpy()
+        out["body25_%dx%d_seed" % (h, w)] = np.int64(seed)
+    # COCO on images/ski.jpg (config 1): decode with PIL, BGR order like cv2.imread
+    ski = np.asarray(Image.open(os.path.join(REF, "images/ski.jpg")).convert("RGB"))[:, :, ::-1].copy()
+    np.savez_compressed(os.path.join(HERE, "ski_bgr.npz"), img=ski)
+    coco = load_ref_model(bodypose_model, 1)
+    from src import util
+    scale = 0.5 * 368 / ski.shape[0]
+    small = cv_resize.resize(ski, (0, 0), fx=scale, fy=scale)
+    padded, pad = util.padRightDownCorner(small, 8, 128)
+    x = np.ascontiguousarray(np.transpose(np.float32(padded[:, :, :, None]), (3, 2, 0, 1)) / 256 - 0.5)
+    with torch.no_grad():
+        p1, p2 = coco(torch.from_numpy(x))
+    out["coco_ski_paf"] = p1.numpy()
+    out["coco_ski_heat"] = p2.numpy()
+    hand = load_ref_model(handpose_model, 2)
+    for (s, seed) in ((184, 3), (368, 4)):
+        x = frame_input(s, s, seed)
+        with torch.no_grad():
+            o = hand(torch.from_numpy(x))
+        out["hand_%d" % s] = o.numpy()
+        out["hand_%d_seed" % s] = np.int64(seed)
+    np.savez_compressed(os.path.join(HERE, "g1_networks.npz"), **out)
+
+
+class ReplayNet:
+    """Stub for Body.model / Hand.model: returns the next designed map(s) per call."""
+
+    def __init__(self, outputs):
+        self.outputs = list(outputs)
+        self.calls = []
+
+    def __call__(self, data):
+        self.calls.append(tuple(data.shape))
+        o = self.outputs.pop(0)
+        if isinstance(o, tuple):
+            return tuple(torch.from_numpy(a[None]) for a in o)
+        return torch.from_numpy(o[None])
+
+
+def patched_body_class(scales):
+    """src.body.Body with the literal `scale_search = [0.5]` replaced at run time."""
+    import src.body as body_mod
+    text = open(body_mod.__file__).read()
+    assert "scale_search = [0.5]" in text
+    text = text.replace("scale_search = [0.5]", "scale_search = %r" % (list(scales),), 1)
+    ns = dict(body_mod.__dict__)
+    exec(compile(text, body_mod.__file__, "exec"), ns)
+    return ns["Body"]
+
+
+def run_body(model_type, frame_hw, scales, maps_fn):
+    import src.body as body_mod
+    cls = body_mod.Body if tuple(scales) == (0.5,) else patched_body_class(scales)
+    b = cls.__new__(cls)
+    b.model_type = model_type
+    b.njoint, b.npaf = (26, 52) if model_type == "body25" else (19, 38)
+    H, W = frame_hw
+    outs = []
+    for s in scales:
+        mult = s * 368 / H
+        h = int(np.rint(H * mult))
+        w = int(np.rint(W * mult))
+        h8, w8 = -(-h // 8), -(-w // 8)
+        outs.append(maps_fn(h8, w8))
+    b.model = ReplayNet(outs)
+    frame = np.zeros((H, W, 3), np.uint8)
+    try:
+        cand, subset = b(frame)
+        err = ""
+    except IndexError as e:
+        cand, subset, err = np.zeros((0,)), np.zeros((0, b.njoint + 1)), "IndexError: %s" % e
+    return outs, cand, subset, err
+
+
+def g2_body_post():
+    cases = []
+    # (name, model_type, frame_hw, scales, persons, seed)
+    spec = [
+        ("b25_R_p1", "body25", (368, 656), (0.5,), 1, 11),
+        ("b25_R_p3", "body25", (368, 656), (0.5,), 3, 12),
+        ("b25_R_p6", "body25", (368, 656), (0.5,), 6, 13),
+        ("b25_N_p3", "body25", (368, 656), (1.0,), 3, 14),
+        ("b25_N_p2_odd", "body25", (300, 500), (1.0,), 2, 15),
+        ("b25_pyr_p2", "body25", (368, 656), (0.5, 1.0, 1.5, 2.0), 2, 16),
+        ("b25_R_p0", "body25", (368, 656), (0.5,), 0, 17),
+        ("coco_R_p3", "coco", (368, 656), (0.5,), 3, 18),
+        ("coco_ski_p2", "coco", (674, 712), (0.5,), 2, 19),
+    ]
+    for name, mt, hw, scales, persons, seed in spec:
+        def maps(h8, w8, persons=persons, seed=seed, mt=mt):
+            return synth.designed_pose_maps(h8, w8, persons, seed, mt)
+        outs, cand, subset, err = run_body(mt, hw, scales, maps)
+        cases.append((name, mt, hw, scales, outs, cand, subset, err))
+    # The 3-way-match IndexError of body.py:193-196 is unreachable with these limb
+    # tables (each joint is the B end of exactly one body_25 limb; COCO's two
+    # redundant limbs come last); the device assembly still flags it.
+    out = {}
+    for name, mt, hw, scales, outs, cand, subset, err in cases:
+        out[name + "/model_type"] = np.array(mt)
+        out[name + "/frame_hw"] = np.array(hw)
+        out[name + "/scales"] = np.array(scales, np.float64)
+        for i, (paf, heat) in enumerate(outs):
+            out[name + "/paf%d" % i] = paf
+            out[name + "/heat%d" % i] = heat
+        out[name + "/candidate"] = cand
+        out[name + "/subset"] = subset
+        out[name + "/error"] = np.array(err)
+        print(name, "candidate", cand.shape, "subset", subset.shape, err)
+    np.savez_compressed(os.path.join(HERE, "g2_body_post.npz"), **out)
+    return cases
+
+
+def g4_hand_post():
+    import src.hand as hand_mod
+    out = {}
+    for ci, (crop, seed) in enumerate(((64, 21), (120, 22), (96, 24))):
+        h = hand_mod.Hand.__new__(hand_mod.Hand)
+        maps = []
+        for s in (0.5, 1.0, 1.5, 2.0):
+            side = int(np.rint(crop * (s * 368 / crop)))
+            h8 = -(-side // 8)
+            maps.append(synth.designed_hand_maps(h8, h8, seed * 10 + int(s * 2)))
+        if ci == 2:
+            maps = [np.zeros_like(m) for m in maps]          # no part above threshold -> [0, 0]
+        h.model = ReplayNet(maps)
+        peaks = h(np.zeros((crop, crop, 3), np.uint8))
+        out["h%d/crop" % ci] = np.int64(crop)
+        for i, m in enumerate(maps):
+            out["h%d/heat%d" % (ci, i)] = m
+        out["h%d/peaks" % ci] = peaks
+        print("hand", ci, peaks.tolist()[:4])
+    np.savez_compressed(os.path.join(HERE, "g4_hand_post.npz"), **out)
+
+
+def g5_hand_detect(cases):
+    from src import util
+    out = {}
+    n = 0
+    for name, mt, hw, scales, outs, cand, subset, err in cases:
+        if mt != "body25" or cand.ndim != 2 or len(subset) == 0:
+            continue
+        for shape in (hw, (hw[0] // 2, hw[1] // 2)):
+            res = util.handDetect(cand, subset, np.zeros(tuple(shape) + (3,), np.uint8))
+            out["d%d/candidate" % n] = cand
+            out["d%d/subset" % n] = subset
+            out["d%d/img_hw" % n] = np.array(shape)
+            out["d%d/result" % n] = np.array(res, dtype=np.int64).reshape(-1, 4)
+            n += 1
+    # a hand-made person with arms near the image border (clamping branches)
+    cand = np.array([[10.0, 10.0, 0.9, 0], [30.0, 12.0, 0.9, 1], [5.0, 40.0, 0.8, 2],
+                     [2.0, 80.0, 0.8, 3], [60.0, 12.0, 0.9, 4], [95.0, 30.0, 0.7, 5],
+                     [99.0, 60.0, 0.6, 6]])
+    row = -np.ones(27)
+    row[[2, 3, 4, 5, 6, 7]] = [1, 2, 3, 4, 5, 6]
+    row[-2:] = [5.0, 6]
+    subset = row[None]
+    for shape in ((100, 100), (70, 120)):
+        res = util.handDetect(cand, subset, np.zeros(shape + (3,), np.uint8))
+        out["d%d/candidate" % n] = cand
+        out["d%d/subset" % n] = subset
+        out["d%d/img_hw" % n] = np.array(shape)
+        out["d%d/result" % n] = np.array(res, dtype=np.int64).reshape(-1, 4)
+        n += 1
+    np.savez_compressed(os.path.join(HERE, "g5_hand_detect.npz"), **out)
+    print("handDetect cases", n)
+
+
+def main():
+    install_shims()
+    shutil.copy(os.path.join(REF, "src/hand_model_output_size.json"),
+                os.path.join(HERE, "hand_model_output_size.json"))
+    g1_networks()
+    cases = g2_body_post()
+    g4_hand_post()
+    g5_hand_detect(cases)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,202 @@
+"""Benchmark: frames/s of body_25 forward + NMS + PAF grouping (BASELINE.json metric).
+
+One step = the whole hot path over one batch of synthetic 368x656 uint8 frames
+resident in HBM:
+    isl_net_preprocess   (cubic resize / pad / normalise -> padded NHWC)
+    isl_net_run          (body_25: 114 FP32-MFMA convolutions + 3 pools)
+    isl_body_post        (x8 cubic resize, fp64 blur + NMS, peak lists, PAF line
+                          integrals, greedy matching, person assembly)
+    + async D2H of the per-frame result records.
+The post stage is fed designed pose maps (3 persons per frame) so that its cost
+is that of real footage (raw outputs of random weights produce ~4k peaks, see
+SURVEY.md §8d); the network still runs in full every step.
+
+Multi-GPU: one process per GPU (torch.distributed.run), frames sharded across
+ranks with no collective on the data path (weak scaling); a barrier + sync
+brackets the timed region and rank 0 reports the max-over-ranks time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "isl-signlanguage-translation_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "frames/sec body_25 368×656 fwd+NMS+PAF at 1/8 MI355X; conv MFMA util %"
+PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix peak (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=32, help="frames per GPU per step")
+    p.add_argument("--height", type=int, default=368)
+    p.add_argument("--width", type=int, default=656)
+    p.add_argument("--scale", type=float, default=1.0,
+                   help="scale_search entry: 1.0 = net at 368x656 (metric shape); 0.5 = reference default")
+    p.add_argument("--persons", type=int, default=3)
+    p.add_argument("--cpu-frames", type=int, default=6, help="frames for the CPU baseline sample (0 = skip)")
+    p.add_argument("--no-cpu", action="store_true")
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from islpose import synth, netspec
+    from islpose.body import BodyEstimator, scale_geometry
+
+    B, H, W = args.batch, args.height, args.width
+    est = BodyEstimator(synth.synth_weights(0), "body25", device=local, scale_search=(args.scale,))
+    # frames of this rank (frame index = rank * B + i: disjoint shards)
+    frames = torch.from_numpy(synth.synth_frames(B, H, W, seed=1000 + rank)).to(dev)
+    (mult, nh, nw, vh, vw), = scale_geometry(H, W, (args.scale,))
+    geoms = [(nh, nw, vh, vw)]
+    maps = [synth.designed_pose_maps(nh // 8, nw // 8, args.persons, seed=rank * B + i) for i in range(B)]
+    d_paf = torch.from_numpy(np.stack([m[0] for m in maps])).to(dev)
+    d_heat = torch.from_numpy(np.stack([m[1] for m in maps])).to(dev)
+    net = est.net
+    import ctypes
+    from islpose import runtime as rt
+    caps = rt.IslCaps(**est.caps)
+    lay = rt.body_layout(est.kind, caps)
+    d_res = torch.empty(B * lay.record_bytes, dtype=torch.uint8, device=dev)
+    h_res = torch.empty(B * lay.record_bytes, dtype=torch.uint8, pin_memory=True)
+    g = (rt.IslScaleGeom * 1)(rt.IslScaleGeom(*geoms[0]))
+    pp = (ctypes.c_void_p * 1)(d_paf.data_ptr())
+    hp = (ctypes.c_void_p * 1)(d_heat.data_ptr())
+    stream = torch.cuda.current_stream(dev)
+    sh = rt.stream_handle(stream)
+    L = rt.lib()
+    ev = []
+
+    def step(timed):
+        net.preprocess(frames, mult, stream=stream)
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        net.run(stream=stream)
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        rt.check(L.isl_body_post(net.h, B, H, W, 1, g, pp, hp, ctypes.byref(caps), rt.ptr(d_res), sh), "post")
+        h_res.copy_(d_res, non_blocking=True)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize(dev)
+    # validate one step's records (no overflow / errors) outside the timed region
+    host = h_res.numpy()
+    for f in range(B):
+        st = int(host[f * lay.record_bytes + lay.status:f * lay.record_bytes + lay.status + 4].view(np.int32)[0])
+        assert st == 0, "post status %d on frame %d" % (st, f)
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    if dist:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    net_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if dist:
+        t = torch.tensor([elapsed, net_ms], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed, net_ms = float(t[0]), float(t[1])
+    if rank != 0:
+        if dist:
+            torch.distributed.destroy_process_group()
+        return
+    total_frames = B * world * args.steps
+    fps = total_frames / elapsed
+    conv_flop = netspec.conv_flops(0, nh, nw) * B
+    achieved = conv_flop / (net_ms * 1e-3) / 1e12
+    traffic = None
+    prof = os.path.join(REPO, "profiles", "conv_traffic.json")
+    if os.path.exists(prof):
+        traffic = json.load(open(prof)).get("hbm_bytes_per_net_run")
+    out = {
+        "metric": METRIC,
+        "value": round(fps, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded uint8 frames, counter-hash weights; post fed designed %d-person maps)"
+                % args.persons,
+        "config": {"workload": "configs[1]: body_25 single-scale %dx%d frames, batch %d per GPU, net input %dx%d"
+                               % (H, W, B, nh, nw),
+                   "batch_per_gpu": B, "frame_hw": [H, W], "scale_search": [args.scale], "net_hw": [nh, nw],
+                   "parallelism": "frame-sharded x%d (no collective)" % world},
+        "roofline": {"bound": "mfma", "kernel": "conv_mfma_f32 (body_25 net run, 114 convs + 3 pools)",
+                     "achieved": round(achieved, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
+                     "net_ms_per_step": round(net_ms, 3), "conv_gflop_per_step": round(conv_flop / 1e9, 1)},
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu and args.cpu_frames > 0:
+        out["cpu_baseline"] = cpu_baseline(args, mult, nh, nw)
+    print(json.dumps(out))
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+def cpu_baseline(args, mult, nh, nw):
+    """The oracle (torch-CPU conv graph + numpy post, parity-pinned against the
+    reference) timed per frame on this host's cores: forward + post, designed maps
+    for the post exactly as on the GPU."""
+    from oracle import cpu_ref
+    from islpose import synth
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, 16)
+    torch.set_num_threads(cores)
+    w = synth.synth_weights(0)
+    fwd = cpu_ref.make_net_fn("body25", w)
+    frames = synth.synth_frames(args.cpu_frames, args.height, args.width, seed=1000)
+    t_fwd, t_post = [], []
+    for i in range(args.cpu_frames):
+        t0 = time.perf_counter()
+        im, _, _ = cpu_ref.net_input(frames[i], mult)
+        fwd(im)
+        t1 = time.perf_counter()
+        pl, hl = synth.designed_pose_maps(nh // 8, nw // 8, args.persons, seed=i)
+        cpu_ref.body_call(frames[i], lambda x: (pl[None], hl[None]), "body25", (args.scale,))
+        t2 = time.perf_counter()
+        t_fwd.append(t1 - t0)
+        t_post.append(t2 - t1)
+    per = float(np.median(t_fwd[1:] if len(t_fwd) > 2 else t_fwd)) + float(np.median(t_post[1:] if len(t_post) > 2 else t_post))
+    return {"value": round(1.0 / per, 4), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": "%d frames %dx%d (scale %.2f, net %dx%d), median of frames 2..N: fwd %.3f s + post %.3f s per frame"
+                      % (args.cpu_frames, args.height, args.width, args.scale, nh, nw,
+                         float(np.median(t_fwd[1:])), float(np.median(t_post[1:])))}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+/*
+ * islpose.h — C ABI of libislpose.so, the MI355X (gfx950) OpenPose keypoint engine.
+ *
+ * Drop-in boundary for the reference's hot path
+ * (sunilsarolkarcds/ISL-SignLanguage-Translation):
+ *
+ *   module seam  : bodypose_25_model / bodypose_model / handpose_model .forward
+ *                  (src/model.py:179-207, 302-329, 394-407), weights loaded through
+ *                  util.transfer (src/util.py:35-44)          -> isl_net_create,
+ *                  isl_net_set_param, isl_net_forward
+ *   frame seam   : Body.__call__ (src/body.py:39-235)         -> isl_body_preprocess +
+ *                  isl_net_run + isl_body_post (isl_body_estimate chains them)
+ *                  Hand.__call__ (src/hand.py:24-74)          -> isl_hand_post
+ *
+ * Conventions
+ *   - every function returns 0 (ISL_OK) or a negative ISL_E_* code and records a
+ *     message retrievable with isl_last_error() (thread-local);
+ *   - device pointers are plain HIP device addresses; the caller owns every I/O
+ *     buffer, the library owns the weights and an activation arena per net;
+ *   - `stream` is a hipStream_t (NULL = default stream); work is stream-ordered,
+ *     no function synchronises the device except where noted;
+ *   - one isl_net per device; not thread-safe without external locking.
+ */
+#ifndef ISLPOSE_H
+#define ISLPOSE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ISL_ABI_VERSION 1
+
+enum isl_kind { ISL_BODY25 = 0, ISL_COCO = 1, ISL_HAND = 2 };
+
+enum isl_status {
+  ISL_OK = 0,
+  ISL_E_ARG = -1,       /* bad argument / shape                                  */
+  ISL_E_PARAM = -2,     /* unknown or missing parameter name (Python: KeyError)  */
+  ISL_E_HIP = -3,       /* HIP runtime error                                     */
+  ISL_E_CAPACITY = -4,  /* a fixed-capacity result buffer overflowed             */
+  ISL_E_STATE = -5,     /* call sequence error (e.g. forward before all params)  */
+  ISL_E_INDEX = -6      /* reference IndexError (3-way subset match, body.py:196)*/
+};
+
+typedef struct isl_net isl_net;
+
+int isl_abi_version(void);
+const char* isl_last_error(void);
+
+/* ---- module seam --------------------------------------------------------- */
+
+/* Replaces `bodypose_25_model()` / `bodypose_model()` / `handpose_model()`
+ * construction (src/model.py:66,210,331) on `device`. */
+int isl_net_create(int kind, int device, isl_net** out);
+int isl_net_destroy(isl_net* net);
+
+/* Parameter table in caffe naming (the keys of the flat weight dict that
+ * util.transfer maps onto state_dict, src/util.py:35-44). */
+int isl_net_param_count(const isl_net* net);
+int isl_net_param_info(const isl_net* net, int index, const char** name, int64_t* numel);
+
+/* Copy one parameter from host memory (float32, the caffe/torch layout:
+ * OIHW for conv weights).  Unknown name or wrong numel -> ISL_E_PARAM.
+ * Weights are repacked for the MFMA kernels once all are present. */
+int isl_net_set_param(isl_net* net, const char* caffe_name, const float* host, int64_t numel);
+
+/* Replaces `model.forward(x)`: x is float32 NCHW [n,3,h,w] on the device.
+ * body25/coco: out0 = PAF [n,npaf,h/8,w/8], out1 = heat [n,njoint,h/8,w/8];
+ * hand: out0 = heat [n,22,h/8,w/8], out1 must be NULL.  (floor-mode pooling.) */
+int isl_net_forward(isl_net* net, const float* d_x_nchw, int n, int h, int w,
+                    float* d_out0, float* d_out1, void* stream);
+
+/* ---- frame seam ---------------------------------------------------------- */
+
+/* Pre-processing of Body/Hand.__call__ for one scale (body.py:53-56):
+ * frames uint8 [n,H,W,3] (BGR, device) -> cv2.resize(INTER_CUBIC, fx=fy=scale)
+ * -> padRightDownCorner(stride 8, 128) -> float32/256 - 0.5, written straight
+ * into the net's input buffer.  Returns the padded net size in *net_h, *net_w. */
+int isl_net_preprocess(isl_net* net, const uint8_t* d_frames, int n, int H, int W,
+                       double scale, int* net_h, int* net_w, void* stream);
+
+/* Run the network on the input buffer filled by isl_net_preprocess; outputs stay
+ * in the arena (low-res NHWC) for the post kernels, and are also copied to
+ * d_out0/d_out1 (NCHW) when those are non-NULL. */
+int isl_net_run(isl_net* net, float* d_out0, float* d_out1, void* stream);
+
+/* Diagnostic: copy the net input buffer (filled by isl_net_preprocess) out as
+ * float32 NCHW [n,3,net_h,net_w]. */
+int isl_net_debug_input(isl_net* net, float* d_x_nchw, void* stream);
+
+/* Capacities of the per-frame result records. */
+typedef struct {
+  int32_t max_peaks;   /* per part                                            */
+  int32_t max_pairs;   /* candidate (i,j) pairs scored per limb (>= nA*nB)    */
+  int32_t max_conns;   /* accepted connections per limb                       */
+  int32_t max_rows;    /* subset rows during assembly                         */
+} isl_caps;
+
+/* Byte offsets inside one frame's result record (device memory, 8-byte aligned):
+ *   int32  status                       ISL_OK / ISL_E_CAPACITY / ISL_E_INDEX
+ *   int32  n_peaks[32]                  per part (body: njoint-1 parts)
+ *   int32  n_conns[32]                  per limb, -1 = limb skipped (special_k)
+ *   int32  n_rows                       subset rows after pruning
+ *   double peaks[parts][max_peaks][3]   (x, y, score); id = running count
+ *   double conns[limbs][max_conns][5]   (idA, idB, score, i, j)   body.py:171
+ *   double subset[max_rows][njoint+1]                             body.py:182-231
+ */
+typedef struct {
+  int64_t status, n_peaks, n_conns, n_rows, peaks, conns, subset, record_bytes;
+} isl_layout;
+
+int isl_body_layout(int model_kind, const isl_caps* caps, isl_layout* out);
+
+/* Geometry of one scale of the pyramid (body.py:51-78): the net ran on a padded
+ * input of net_h x net_w whose valid (un-padded) part is valid_h x valid_w. */
+typedef struct {
+  int32_t net_h, net_w;       /* padded net input size (multiples of 8)         */
+  int32_t valid_h, valid_w;   /* resized image size before padding              */
+} isl_scale_geom;
+
+/* Body post-processing (body.py:64-235) for n frames of size H x W.
+ * For each scale s, low-res maps are read from d_paf[s] / d_heat[s] (float32
+ * NCHW [n,C,net_h/8,net_w/8]); NULL entries mean "use the net's own arena
+ * output" (valid only for nscales == 1, right after isl_net_run).
+ * Results: n records of isl_body_layout(...).record_bytes at d_result. */
+int isl_body_post(isl_net* net, int n, int H, int W, int nscales, const isl_scale_geom* geom,
+                  const float* const* d_paf, const float* const* d_heat,
+                  const isl_caps* caps, void* d_result, void* stream);
+
+/* Hand post-processing (hand.py:35-74) for n crops of size w x w: 4 scales of
+ * low-res hand maps (NCHW [n,22,g.net_h/8,g.net_w/8]) -> int64 peaks [n][21][2]. */
+int isl_hand_post(isl_net* net, int n, int w, int nscales, const isl_scale_geom* geom,
+                  const float* const* d_heat, int64_t* d_peaks, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ISLPOSE_H */

@@ -1,0 +1,261 @@
+// Direct convolution (3x3 / 1x1 / 7x7, stride 1, "same" padding) as an
+// implicit GEMM on the gfx950 FP32 matrix cores (v_mfma_f32_32x32x2_f32).
+//
+// Replaces every nn.Conv2d (+ReLU / PReLU) of src/model.py:25-64 (make_layers,
+// make_layers_Mconv).  FP32 in, FP32 accumulate: each MFMA is an exact fmaf
+// chain, so results differ from torch-CPU only by summation order.
+//
+// GEMM view:  D[co][px] = sum_k Wt[co][k] * X[k][px],  k = (ky, kx, ci).
+//   A operand (32 rows)  = 32 output channels      (lane: co = l&31, k = l>>5)
+//   B operand (32 cols)  = 32 output pixels        (lane: px = l&31, k = l>>5)
+//   D                    = lane holds pixel l&31, channels (r&3)+8(r>>2)+4(l>>5)
+//
+// Pixel tiles: BPX consecutive output pixels of one frame in raster order
+// (flattened M; a frame's last tile is partial, nothing else is wasted).  The
+// input buffer is stored with a zero ring (Act.pad >= k/2), so in its padded
+// linear pixel index L = (y+p)*(W+2p) + (x+p) the input row dy of a whole tile
+// is ONE contiguous segment [La + dy*Wp - P, Lb + dy*Wp + P]: no bounds checks,
+// no im2col, no halo logic beyond a per-lane offset.
+//
+// K loop: one step = (8-channel chunk, kernel row ky): stage that row's input
+// segment (8 ch) and the KS x 8 x BCO weight slab into LDS (register-staged,
+// double-buffered, one barrier per step), then KS taps x 4 MFMA k-steps.
+// The 8 channels of a chunk are split in two planes of 4 (ci 0-3 | 4-7); lane
+// half h reads plane h with one ds_read_b128 and feeds its 4 floats to 4
+// successive MFMAs, so MFMA k-step e covers channels {e, 4+e}.
+#include "internal.h"
+
+namespace isl {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct ConvArgs {
+  const float* in;
+  float* out;
+  const float* wpk;
+  const float* bias;
+  const float* slope;
+  int in_pad, in_cs, in_coff;
+  int out_pad, out_cs, out_coff;
+  int H, W, cin_chunks, cout, co_tiles, px_tiles, act, nblocks;
+};
+
+template <int KS, int WAVES_M, int WAVES_N, int WM, int WN>
+__global__ void __launch_bounds__(WAVES_M * WAVES_N * 64)
+conv_mfma_f32(ConvArgs a) {
+  constexpr int NPL = 2;                        // planes of 4 channels per 8-channel chunk
+  constexpr int NT = WAVES_M * WAVES_N * 64;
+  constexpr int BCO = WAVES_M * WM * 32;
+  constexpr int BPX = WAVES_N * WN * 32;
+  constexpr int P = KS / 2;
+  constexpr int SEGMAX = 2 * BPX;               // input segment capacity (host-checked)
+  constexpr int WTILE = KS * NPL * BCO;         // float4 per weight slab (one kernel row)
+  constexpr int ACT_IT = (SEGMAX + NT - 1) / NT;
+  constexpr int W_IT = (WTILE + NT - 1) / NT;
+  constexpr int BUF = NPL * SEGMAX + WTILE;     // float4 per LDS stage
+  __shared__ f32x4 smem[2 * BUF];
+
+  // XCD-aware tile order: consecutive logical tiles (the co-tiles of one pixel
+  // tile, then neighbouring pixel tiles) land on the same XCD / L2.
+  int bid = blockIdx.x;
+  {
+    const int nb = a.nblocks, q = nb >> 3, r = nb & 7, xcd = bid & 7, k = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int co_t = bid % a.co_tiles;
+  const int rest = bid / a.co_tiles;
+  const int pt = rest % a.px_tiles;
+  const int n = rest / a.px_tiles;
+
+  const int HW = a.H * a.W;
+  const int m0 = pt * BPX;
+  const int mlast = min(m0 + BPX, HW) - 1;
+  const int Wi = a.W + 2 * a.in_pad;
+  const int ya = m0 / a.W, xa = m0 - ya * a.W;
+  const int yb = mlast / a.W, xb = mlast - yb * a.W;
+  const int La = (ya + a.in_pad) * Wi + xa + a.in_pad;
+  const int Lb = (yb + a.in_pad) * Wi + xb + a.in_pad;
+  const int seg = Lb - La + 2 * P + 1;
+  const float* in_f = a.in + (size_t)n * (a.H + 2 * a.in_pad) * Wi * a.in_cs + a.in_coff;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wave_m = wave % WAVES_M, wave_n = wave / WAVES_M;
+  const int h = lane >> 5, l32 = lane & 31;
+
+  int rel[WN];
+#pragma unroll
+  for (int wn = 0; wn < WN; ++wn) {
+    const int j = (wave_n * WN + wn) * 32 + l32;
+    const int m = min(m0 + j, mlast);
+    const int y = m / a.W, x = m - y * a.W;
+    rel[wn] = (y + a.in_pad) * Wi + x + a.in_pad - La;
+  }
+
+  const int T = a.cin_chunks * KS;
+  f32x4 ra[NPL][ACT_IT];
+  f32x4 rw[W_IT];
+
+  auto gload = [&](int t) {
+    const int c = t / KS, ky = t - c * KS;
+    const float* src = in_f + (size_t)(La + (ky - P) * Wi - P) * a.in_cs + c * 8;
+#pragma unroll
+    for (int pl = 0; pl < NPL; ++pl)
+#pragma unroll
+      for (int i = 0; i < ACT_IT; ++i) {
+        const int px = tid + i * NT;
+        ra[pl][i] = (px < seg) ? *(const f32x4*)(src + (size_t)px * a.in_cs + 4 * pl) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    const f32x4* wsrc = (const f32x4*)a.wpk + ((size_t)(co_t * a.cin_chunks + c) * KS + ky) * WTILE;
+#pragma unroll
+    for (int i = 0; i < W_IT; ++i) {
+      const int idx = tid + i * NT;
+      if (WTILE % NT == 0 || idx < WTILE) rw[i] = wsrc[idx];
+    }
+  };
+  auto lstore = [&](int buf) {
+    f32x4* s = smem + buf * BUF;
+#pragma unroll
+    for (int pl = 0; pl < NPL; ++pl)
+#pragma unroll
+      for (int i = 0; i < ACT_IT; ++i) {
+        const int px = tid + i * NT;
+        if (SEGMAX % NT == 0 || px < SEGMAX) s[pl * SEGMAX + px] = ra[pl][i];
+      }
+#pragma unroll
+    for (int i = 0; i < W_IT; ++i) {
+      const int idx = tid + i * NT;
+      if (WTILE % NT == 0 || idx < WTILE) s[NPL * SEGMAX + idx] = rw[i];
+    }
+  };
+
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+    for (int wn = 0; wn < WN; ++wn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[wm][wn][r] = 0.f;
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < T) gload(t + 1);
+    const f32x4* sa = smem + buf * BUF + h * SEGMAX;
+    const f32x4* sw = smem + buf * BUF + NPL * SEGMAX + h * BCO + wave_m * WM * 32 + l32;
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx) {
+      f32x4 A[WM], B[WN];
+#pragma unroll
+      for (int wm = 0; wm < WM; ++wm) A[wm] = sw[kx * NPL * BCO + wm * 32];
+#pragma unroll
+      for (int wn = 0; wn < WN; ++wn) B[wn] = sa[rel[wn] + kx];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+          for (int wn = 0; wn < WN; ++wn)
+            acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[wm][e], B[wn][e], acc[wm][wn], 0, 0, 0);
+    }
+    if (t + 1 < T) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: bias + activation, masked float4 stores into the output slice
+  const int Wo = a.W + 2 * a.out_pad;
+  float* out_f = a.out + (size_t)n * (a.H + 2 * a.out_pad) * Wo * a.out_cs + a.out_coff;
+#pragma unroll
+  for (int wn = 0; wn < WN; ++wn) {
+    const int m = m0 + (wave_n * WN + wn) * 32 + l32;
+    if (m > mlast) continue;
+    const int y = m / a.W, x = m - y * a.W;
+    float* op = out_f + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * a.out_cs;
+#pragma unroll
+    for (int wm = 0; wm < WM; ++wm) {
+      const int cob = co_t * BCO + (wave_m * WM + wm) * 32 + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = cob + 8 * q;
+        const f32x4 b = *(const f32x4*)(a.bias + co);
+        f32x4 v = {acc[wm][wn][4 * q] + b[0], acc[wm][wn][4 * q + 1] + b[1],
+                   acc[wm][wn][4 * q + 2] + b[2], acc[wm][wn][4 * q + 3] + b[3]};
+        if (a.act == ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        } else if (a.act == ACT_PRELU) {
+          const f32x4 sl = *(const f32x4*)(a.slope + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
+        }
+        if (co + 3 < a.cout) {
+          *(f32x4*)(op + co) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (co + e < a.cout) op[co + e] = v[e];
+        }
+      }
+    }
+  }
+}
+
+int conv_bco_for(int cout) {
+  if (cout % 128 == 0) return 128;
+  if (cout == 96) return 96;
+  if (cout > 96) return 128;
+  if (cout > 32) return 64;
+  return 32;
+}
+
+template <int KS, int WAVES_M, int WAVES_N, int WM, int WN>
+static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
+  constexpr int BCO = WAVES_M * WM * 32;
+  constexpr int BPX = WAVES_N * WN * 32;
+  constexpr int P = KS / 2;
+  if (c.in_pad < P) { set_error("conv: input ring narrower than kernel radius"); return hipErrorInvalidValue; }
+  const int max_rows = (c.W + BPX - 2) / c.W;
+  const int max_seg = BPX - 1 + 2 * c.in_pad * max_rows + 2 * P + 1;
+  if (max_seg > 2 * BPX) { set_error("conv: image too narrow for the pixel tile"); return hipErrorInvalidValue; }
+  if (c.bco != BCO) { set_error("conv: tile mismatch"); return hipErrorInvalidValue; }
+  ConvArgs a;
+  a.in = c.in; a.out = c.out; a.wpk = c.wpk; a.bias = c.bias; a.slope = c.slope;
+  a.in_pad = c.in_pad; a.in_cs = c.in_cs; a.in_coff = c.in_coff;
+  a.out_pad = c.out_pad; a.out_cs = c.out_cs; a.out_coff = c.out_coff;
+  a.H = c.H; a.W = c.W; a.cin_chunks = c.cin_chunks; a.cout = c.cout;
+  a.co_tiles = (c.cout + BCO - 1) / BCO;
+  a.px_tiles = (c.H * c.W + BPX - 1) / BPX;
+  a.act = c.act;
+  const long long nb = (long long)c.n * a.px_tiles * a.co_tiles;
+  if (nb <= 0 || nb > 0x7fffffff) { set_error("conv: bad grid"); return hipErrorInvalidValue; }
+  a.nblocks = (int)nb;
+  hipLaunchKernelGGL((conv_mfma_f32<KS, WAVES_M, WAVES_N, WM, WN>), dim3(a.nblocks),
+                     dim3(WAVES_M * WAVES_N * 64), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int KS>
+static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
+  switch (c.bco) {
+    case 128: return launch_t<KS, 2, 2, 2, 2>(c, s);
+    case 96: return launch_t<KS, 1, 4, 3, 1>(c, s);
+    case 64: return launch_t<KS, 1, 4, 2, 1>(c, s);
+    case 32: return launch_t<KS, 1, 4, 1, 1>(c, s);
+  }
+  set_error("conv: unsupported tile");
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_conv(const ConvLaunch& c, hipStream_t s) {
+  switch (c.ks) {
+    case 1: return launch_ks<1>(c, s);
+    case 3: return launch_ks<3>(c, s);
+    case 7: return launch_ks<7>(c, s);
+  }
+  set_error("conv: unsupported kernel size");
+  return hipErrorInvalidValue;
+}
+
+}  // namespace isl

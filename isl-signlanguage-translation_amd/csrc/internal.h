@@ -1,0 +1,72 @@
+// Internal declarations shared by the libislpose translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+namespace isl {
+
+// Activation buffer: NHWC float32 with a zero ring of `pad` pixels around every
+// frame, i.e. element (n, y, x, c) lives at
+//   base + ((n*(H+2p) + y+p) * (W+2p) + x+p) * cs + c.
+// Convolutions read/write channel slices [coff, coff+C) of such buffers, which
+// is how every torch.cat of the reference becomes zero-copy.
+struct Act {
+  float* base = nullptr;
+  int n = 0, H = 0, W = 0, pad = 0, cs = 0;
+  size_t frame_elems() const { return (size_t)(H + 2 * pad) * (W + 2 * pad) * cs; }
+  size_t bytes() const { return frame_elems() * n * sizeof(float); }
+};
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_PRELU = 2 };
+
+// One convolution launch.
+struct ConvLaunch {
+  const float* in;  int in_pad, in_cs, in_coff;
+  float* out;       int out_pad, out_cs, out_coff;
+  const float* wpk;            // packed weights  [co_tile][chunk][ky][kx][plane][BCO][4]
+  const float* bias;           // [co_tiles*BCO]
+  const float* slope;          // [co_tiles*BCO] or null
+  int n, H, W;
+  int ks;                      // 1, 3, 7
+  int cin_chunks;              // physical input channels / 8
+  int cout;                    // real output channels
+  int bco;                     // output channels per block tile (32, 64, 96, 128)
+  int act;
+};
+
+// Returns the block tile width (output channels) the conv kernels use for cout.
+int conv_bco_for(int cout);
+hipError_t launch_conv(const ConvLaunch& c, hipStream_t s);
+
+hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s);
+hipError_t launch_pack_nchw(const float* x, int n, int C, int h, int w, const Act& out, hipStream_t s);
+hipError_t launch_unpack_nchw(const Act& in, int coff, int C, float* y, hipStream_t s);
+hipError_t launch_preprocess(const uint8_t* frames, int n, int H, int W, double scale,
+                             int rh, int rw, const Act& out, hipStream_t s);
+
+struct MapSrc {            // one single-stage cubic resize, sampled per output element
+  const float* base;       // element (f, c, y, x) at base + f*fs + c*cstr + y*ys + x*xs
+  long long fs, cstr, ys, xs;
+  int sh, sw;              // source size (tap clamping)
+  int dh, dw;              // destination size of this resize
+  double scy, scx;         // source pixels per destination pixel (1/inv_scale)
+  int cn;                  // channels of the image OpenCV resized (SIMD body / tail split)
+  int identity;            // dsize == ssize: plain copy
+};
+
+void set_error(const std::string& msg);
+
+
+}  // namespace isl
+
+struct isl_net;
+namespace isl {
+int net_kind(const isl_net* net);
+int net_device(const isl_net* net);
+// low-resolution output `which` (0 = out0 / PAF, 1 = out1 / heat) of the last run, as a MapSrc
+int net_low_res(isl_net* net, int which, MapSrc* m);
+// grow-only device scratch owned by the net (nullptr + error on failure)
+void* net_scratch(isl_net* net, size_t bytes);
+}  // namespace isl

@@ -1,0 +1,180 @@
+// Byte-moving kernels around the convolutions: 2x2 max-pool, NCHW <-> padded
+// NHWC packing, and the frame pre-processing of Body/Hand.__call__.
+#include "internal.h"
+
+namespace isl {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// nn.MaxPool2d(2, 2, 0) (model.py:30-31): floor mode, NHWC, 4 channels per thread.
+__global__ void maxpool2_kernel(const float* __restrict__ in, int ip, int ics, int iH, int iW,
+                                float* __restrict__ out, int op, int ocs, int oH, int oW, int C4, int n) {
+  const long long total = (long long)n * oH * oW * C4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    long long r = i / C4;
+    const int x = (int)(r % oW); r /= oW;
+    const int y = (int)(r % oH);
+    const int f = (int)(r / oH);
+    const int iWp = iW + 2 * ip, oWp = oW + 2 * op;
+    const float* p = in + ((size_t)f * (iH + 2 * ip) * iWp + (size_t)(2 * y + ip) * iWp + 2 * x + ip) * ics + 4 * c4;
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + ics);
+    const f32x4 c = *(const f32x4*)(p + (size_t)iWp * ics), d = *(const f32x4*)(p + (size_t)iWp * ics + ics);
+    f32x4 m;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = fmaxf(fmaxf(a[e], b[e]), fmaxf(c[e], d[e]));
+    *(f32x4*)(out + ((size_t)f * (oH + 2 * op) * oWp + (size_t)(y + op) * oWp + x + op) * ocs + 4 * c4) = m;
+  }
+}
+
+hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s) {
+  const int C4 = (C + 3) / 4;
+  const long long total = (long long)out.n * out.H * out.W * C4;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(maxpool2_kernel, dim3(grid), dim3(256), 0, s, in.base, in.pad, in.cs, in.H, in.W,
+                     out.base, out.pad, out.cs, out.H, out.W, C4, in.n);
+  return hipGetLastError();
+}
+
+// NCHW float (module seam input) -> padded NHWC, channels >= C zero-filled.
+__global__ void pack_nchw_kernel(const float* __restrict__ x, int n, int C, int h, int w,
+                                 float* __restrict__ out, int op, int ocs) {
+  const long long total = (long long)n * h * w;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int xx = (int)(i % w);
+    const int yy = (int)((i / w) % h);
+    const int f = (int)(i / ((long long)w * h));
+    float* o = out + ((size_t)f * (h + 2 * op) * (w + 2 * op) + (size_t)(yy + op) * (w + 2 * op) + xx + op) * ocs;
+    for (int c = 0; c < ocs; ++c)
+      o[c] = c < C ? x[(((size_t)f * C + c) * h + yy) * w + xx] : 0.f;
+  }
+}
+
+hipError_t launch_pack_nchw(const float* x, int n, int C, int h, int w, const Act& out, hipStream_t s) {
+  const long long total = (long long)n * h * w;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(pack_nchw_kernel, dim3(grid), dim3(256), 0, s, x, n, C, h, w, out.base, out.pad, out.cs);
+  return hipGetLastError();
+}
+
+// padded NHWC slice [coff, coff+C) -> NCHW float (module seam output).
+__global__ void unpack_nchw_kernel(const float* __restrict__ in, int ip, int ics, int coff, int n, int C,
+                                   int h, int w, float* __restrict__ y) {
+  const long long total = (long long)n * C * h * w;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int xx = (int)(i % w);
+    long long r = i / w;
+    const int yy = (int)(r % h); r /= h;
+    const int c = (int)(r % C);
+    const int f = (int)(r / C);
+    y[i] = in[((size_t)f * (h + 2 * ip) * (w + 2 * ip) + (size_t)(yy + ip) * (w + 2 * ip) + xx + ip) * ics + coff + c];
+  }
+}
+
+hipError_t launch_unpack_nchw(const Act& in, int coff, int C, float* y, hipStream_t s) {
+  const long long total = (long long)in.n * C * in.H * in.W;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(unpack_nchw_kernel, dim3(grid), dim3(256), 0, s, in.base, in.pad, in.cs, coff, in.n, C,
+                     in.H, in.W, y);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Frame pre-processing (body.py:53-56, hand.py:37-40):
+//   cv2.resize(uint8 BGR, fx=fy=scale, INTER_CUBIC) -> padRightDownCorner(8, 128)
+//   -> float32(img)/256 - 0.5, written as padded NHWC (3 real + 5 zero channels).
+// The uint8 cubic follows OpenCV's generic path (see oracle/cv_resize.py):
+// 11-bit fixed-point coefficients, int horizontal sums, and a vertical pass that
+// is float (beta/2^22, round-half-even) for the SIMD body of each output row and
+// fixed point ((sum + 2^21) >> 22) for its scalar tail.
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ void cubic_coeffs(float t, float c[4]) {
+  const float A = -0.75f;
+  const float tp1 = t + 1.f;
+  c[0] = ((A * tp1 - 5.f * A) * tp1 + 8.f * A) * tp1 - 4.f * A;
+  c[1] = ((A + 2.f) * t - (A + 3.f)) * t * t + 1.f;
+  const float u = 1.f - t;
+  c[2] = ((A + 2.f) * u - (A + 3.f)) * u * u + 1.f;
+  c[3] = 1.f - c[0] - c[1] - c[2];
+}
+
+__device__ __forceinline__ void axis_tap(int d, double scale, int n, int idx[4], float c[4]) {
+  float f = (float)((d + 0.5) * scale - 0.5);
+  const int s = (int)floorf(f);
+  f -= (float)s;
+  cubic_coeffs(f, c);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) idx[k] = min(max(s + k - 1, 0), n - 1);
+}
+
+__global__ void preprocess_kernel(const uint8_t* __restrict__ frames, int n, int H, int W, double scale_y,
+                                  double scale_x, int rh, int rw, int identity, float* __restrict__ out,
+                                  int op, int ocs, int ph, int pw) {
+  const long long total = (long long)n * ph * pw;
+  const int rowlen = rw * 3;
+  const int body = rowlen - rowlen % 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int x = (int)(i % pw);
+    const int y = (int)((i / pw) % ph);
+    const int f = (int)(i / ((long long)pw * ph));
+    float v[3];
+    if (y >= rh || x >= rw) {
+      v[0] = v[1] = v[2] = 128.f / 256.f - 0.5f;
+    } else if (identity) {
+      const uint8_t* p = frames + (((size_t)f * H + y) * W + x) * 3;
+      for (int c = 0; c < 3; ++c) v[c] = (float)p[c] / 256.f - 0.5f;
+    } else {
+      int xi[4], yi[4];
+      float xc[4], yc[4];
+      axis_tap(x, scale_x, W, xi, xc);
+      axis_tap(y, scale_y, H, yi, yc);
+      int ia[4], ib[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        ia[k] = (int)rintf(xc[k] * 2048.f);
+        ib[k] = (int)rintf(yc[k] * 2048.f);
+      }
+      for (int c = 0; c < 3; ++c) {
+        int hz[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint8_t* row = frames + ((size_t)f * H + yi[k]) * W * 3 + c;
+          hz[k] = row[xi[0] * 3] * ia[0] + row[xi[1] * 3] * ia[1] + row[xi[2] * 3] * ia[2] + row[xi[3] * 3] * ia[3];
+        }
+        int r;
+        if (x * 3 + c < body) {
+          const float sc = 1.f / (2048.f * 2048.f);
+          const float b0 = (float)ib[0] * sc, b1 = (float)ib[1] * sc, b2 = (float)ib[2] * sc, b3 = (float)ib[3] * sc;
+          const float s = (float)hz[0] * b0 + ((float)hz[1] * b1 + ((float)hz[2] * b2 + (float)hz[3] * b3));
+          r = (int)rintf(s);
+        } else {
+          const long long acc = (long long)hz[0] * ib[0] + (long long)hz[1] * ib[1] + (long long)hz[2] * ib[2] +
+                                (long long)hz[3] * ib[3];
+          r = (int)((acc + (1 << 21)) >> 22);
+        }
+        r = min(max(r, 0), 255);
+        v[c] = (float)r / 256.f - 0.5f;
+      }
+    }
+    float* o = out + ((size_t)f * (ph + 2 * op) * (pw + 2 * op) + (size_t)(y + op) * (pw + 2 * op) + x + op) * ocs;
+    *(f32x4*)o = f32x4{v[0], v[1], v[2], 0.f};
+    *(f32x4*)(o + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+hipError_t launch_preprocess(const uint8_t* frames, int n, int H, int W, double scale, int rh, int rw,
+                             const Act& out, hipStream_t s) {
+  const int identity = (rh == H && rw == W);
+  const long long total = (long long)n * out.H * out.W;
+  const int grid = (int)std::min<long long>((total + 255) / 256, 256 * 32);
+  hipLaunchKernelGGL(preprocess_kernel, dim3(grid), dim3(256), 0, s, frames, n, H, W, 1.0 / scale, 1.0 / scale,
+                     rh, rw, identity, out.base, out.pad, out.cs, out.H, out.W);
+  return hipGetLastError();
+}
+
+}  // namespace isl

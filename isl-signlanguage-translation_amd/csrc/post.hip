@@ -1,0 +1,661 @@
+// Post-network kernels of Body.__call__ (src/body.py:64-235) and
+// Hand.__call__ (src/hand.py:51-74):
+//
+//   resize_kernel      cv2.resize INTER_CUBIC of the low-res maps (x8, crop,
+//                      to frame size), fp32, OpenCV operation order
+//   blur_nms_kernel    gaussian_filter(sigma=3) in fp64 (scipy order) fused
+//                      with the 4-neighbour NMS -> one 64-bit mask word per
+//                      (row, 64 columns), written by a wave ballot
+//   compact_kernel     raster-order peak lists (np.nonzero order) + scores
+//   group_kernel       PAF line integral for every (A,B) pair (PAF sampled on
+//                      demand from the low-res / intermediate maps), stable
+//                      score sort, greedy matching, person assembly and
+//                      pruning -- one workgroup per frame
+//
+// Every floating-point expression follows the reference's evaluation order;
+// the file is built with -ffp-contract=off so no FMA is formed.
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "islpose.h"
+
+namespace isl {
+
+// scipy _gaussian_kernel1d(3, 0, 12), taps 0..12 (symmetric), from numpy
+__constant__ double kGauss[13] = {
+    0x1.105a329f98197p-3, 0x1.01a25f86eb137p-3, 0x1.b42a57d56c0bep-4, 0x1.4a614d1afd337p-4,
+    0x1.bfde9c12bec92p-5, 0x1.0fa58939b528fp-5, 0x1.26defcaeb0202p-6, 0x1.1e6bccad344bap-7,
+    0x1.f1e9915139406p-9, 0x1.8345966f69518p-10, 0x1.0d8a5ad43c165p-11, 0x1.4fbe39149e277p-13,
+    0x1.763a210dfb306p-15};
+
+// limb tables, body.py:111-126
+__constant__ int kLimbs25[24][2] = {{1, 0}, {1, 2}, {2, 3}, {3, 4}, {1, 5}, {5, 6}, {6, 7}, {1, 8},
+                                    {8, 9}, {9, 10}, {10, 11}, {8, 12}, {12, 13}, {13, 14}, {0, 15}, {0, 16},
+                                    {15, 17}, {16, 18}, {11, 24}, {11, 22}, {14, 21}, {14, 19}, {22, 23}, {19, 20}};
+__constant__ int kMap25[24][2] = {{30, 31}, {14, 15}, {16, 17}, {18, 19}, {22, 23}, {24, 25}, {26, 27}, {0, 1},
+                                  {6, 7}, {2, 3}, {4, 5}, {8, 9}, {10, 11}, {12, 13}, {32, 33}, {34, 35},
+                                  {36, 37}, {38, 39}, {50, 51}, {46, 47}, {44, 45}, {40, 41}, {48, 49}, {42, 43}};
+__constant__ int kLimbsCoco[19][2] = {{1, 2}, {1, 5}, {2, 3}, {3, 4}, {5, 6}, {6, 7}, {1, 8}, {8, 9}, {9, 10}, {1, 11},
+                                      {11, 12}, {12, 13}, {1, 0}, {0, 14}, {14, 16}, {0, 15}, {15, 17}, {2, 16}, {5, 17}};
+__constant__ int kMapCoco[19][2] = {{12, 13}, {20, 21}, {14, 15}, {16, 17}, {22, 23}, {24, 25}, {0, 1},
+                                    {2, 3},   {4, 5},   {6, 7},   {8, 9},   {10, 11}, {28, 29}, {30, 31},
+                                    {34, 35}, {32, 33}, {36, 37}, {18, 19}, {26, 27}};
+
+// ---------------------------------------------------------------------------
+// cubic resize (OpenCV generic path; see oracle/cv_resize.py for the contract)
+// ---------------------------------------------------------------------------
+
+
+
+__device__ __forceinline__ void cubic_coeffs_f(float t, float c[4]) {
+  const float A = -0.75f;
+  const float tp1 = t + 1.f;
+  c[0] = ((A * tp1 - 5.f * A) * tp1 + 8.f * A) * tp1 - 4.f * A;
+  c[1] = ((A + 2.f) * t - (A + 3.f)) * t * t + 1.f;
+  const float u = 1.f - t;
+  c[2] = ((A + 2.f) * u - (A + 3.f)) * u * u + 1.f;
+  c[3] = 1.f - c[0] - c[1] - c[2];
+}
+
+__device__ __forceinline__ void taps(int d, double scale, int n, int idx[4], float c[4]) {
+  float f = (float)((d + 0.5) * scale - 0.5);
+  const int s = (int)floorf(f);
+  f -= (float)s;
+  cubic_coeffs_f(f, c);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) idx[k] = min(max(s + k - 1, 0), n - 1);
+}
+
+__device__ __forceinline__ float sample(const MapSrc& m, int f, int c, int y, int x) {
+  const float* b = m.base + f * m.fs + c * m.cstr;
+  if (m.identity) return b[y * m.ys + x * m.xs];
+  int xi[4], yi[4];
+  float a[4], be[4];
+  taps(x, m.scx, m.sw, xi, a);
+  taps(y, m.scy, m.sh, yi, be);
+  float hz[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float* r = b + yi[k] * m.ys;
+    hz[k] = ((r[xi[0] * m.xs] * a[0] + r[xi[1] * m.xs] * a[1]) + r[xi[2] * m.xs] * a[2]) + r[xi[3] * m.xs] * a[3];
+  }
+  const int rowlen = m.dw * m.cn;
+  if (x * m.cn + c < rowlen - rowlen % 4)   // VResizeCubicVec_32f body (mul + add, SSE baseline)
+    return hz[0] * be[0] + (hz[1] * be[1] + (hz[2] * be[2] + hz[3] * be[3]));
+  return ((hz[0] * be[0] + hz[1] * be[1]) + hz[2] * be[2]) + hz[3] * be[3];   // scalar tail
+}
+
+// out(f, c, y, x) for c < nch, y < oh, x < ow of resize `m`.
+// mode 0: dense NHWC f32 [n][oh][ow][nch]; 1: planar f32 [n][nch][oh][ow];
+// mode 2: planar f64 accumulate avg = avg + (avg + v/L)  (body.py:80, the doubling quirk)
+// mode 3: planar f64 accumulate avg += v/L                (hand.py:56)
+__global__ void resize_kernel(MapSrc m, int n, int nch, int oh, int ow, int mode, float inv_div_f, void* out) {
+  const long long total = (long long)n * nch * oh * ow;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int c, x, y, f;
+    long long r = i;
+    if (mode == 0) {
+      c = (int)(r % nch); r /= nch; x = (int)(r % ow); r /= ow; y = (int)(r % oh); f = (int)(r / oh);
+    } else {
+      x = (int)(r % ow); r /= ow; y = (int)(r % oh); r /= oh; c = (int)(r % nch); f = (int)(r / nch);
+    }
+    const float v = sample(m, f, c, y, x);
+    if (mode <= 1) {
+      ((float*)out)[i] = v;
+    } else {
+      double* o = (double*)out + i;
+      const float q = v / inv_div_f;   // heatmap / len(multiplier), float32
+      if (mode == 2) *o = *o + (*o + (double)q);
+      else *o = *o + (double)q;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp64 blur + NMS
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  // scipy 'reflect' (d c b a | a b c d | d c b a), periodic for short lines
+  const int p = 2 * n;
+  i %= p;
+  if (i < 0) i += p;
+  return i < n ? i : p - 1 - i;
+}
+
+constexpr int NMS_TY = 16, NMS_TX = 64, NMS_R = 12;
+
+// planes: [n*nparts][H][W] (T = float or double); mask: [n*nparts][H][words]
+template <typename T>
+__global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ planes, int H, int W, int words,
+                                                        unsigned long long* __restrict__ mask, double thre,
+                                                        int mode_hand) {
+  constexpr int IR = NMS_TY + 2 + 2 * NMS_R, IC = NMS_TX + 2 + 2 * NMS_R;  // 42 x 90
+  constexpr int VR = NMS_TY + 2, GC = NMS_TX + 2;                         // 18 rows, 66 cols
+  __shared__ double s_in[IR][IC];
+  __shared__ double s_v[VR][IC];
+  __shared__ double s_g[VR][GC];
+  const int plane = blockIdx.z;
+  const int y0 = blockIdx.y * NMS_TY, x0 = blockIdx.x * NMS_TX;
+  const T* src = planes + (size_t)plane * H * W;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < IR * IC; i += 256) {
+    const int r = i / IC, c = i - r * IC;
+    const int yy = reflect_idx(y0 - 1 - NMS_R + r, H), xx = reflect_idx(x0 - 1 - NMS_R + c, W);
+    s_in[r][c] = (double)src[(size_t)yy * W + xx];
+  }
+  __syncthreads();
+  // axis 0 (NI_Correlate1D, symmetric): o = c*w0; for j = 12..1: o += (a[-j] + a[+j]) * w[j]
+  for (int i = tid; i < VR * IC; i += 256) {
+    const int r = i / IC, c = i - r * IC;
+    double o = s_in[r + NMS_R][c] * kGauss[0];
+#pragma unroll
+    for (int j = NMS_R; j >= 1; --j) o = o + (s_in[r + NMS_R - j][c] + s_in[r + NMS_R + j][c]) * kGauss[j];
+    s_v[r][c] = o;
+  }
+  __syncthreads();
+  for (int i = tid; i < VR * GC; i += 256) {
+    const int r = i / GC, c = i - r * GC;
+    double o = s_v[r][c + NMS_R] * kGauss[0];
+#pragma unroll
+    for (int j = NMS_R; j >= 1; --j) o = o + (s_v[r][c + NMS_R - j] + s_v[r][c + NMS_R + j]) * kGauss[j];
+    s_g[r][c] = o;
+  }
+  __syncthreads();
+  // one wave per output row, lane = column -> one 64-bit mask word per (row, tile)
+  const int lane = tid & 63, wave = tid >> 6;
+  for (int ty = wave; ty < NMS_TY; ty += 4) {
+    const int y = y0 + ty, x = x0 + lane;
+    bool pk = false;
+    if (y < H && x < W) {
+      const double g = s_g[ty + 1][lane + 1];
+      if (mode_hand) {
+        pk = g > thre;                                  // hand.py:62 binary map
+      } else {
+        const double up = y > 0 ? s_g[ty][lane + 1] : 0.0;
+        const double dn = y + 1 < H ? s_g[ty + 2][lane + 1] : 0.0;
+        const double lf = x > 0 ? s_g[ty + 1][lane] : 0.0;
+        const double rt = x + 1 < W ? s_g[ty + 1][lane + 2] : 0.0;
+        pk = g >= up && g >= dn && g >= lf && g >= rt && g > thre;   // body.py:99-100
+      }
+    }
+    const unsigned long long word = __ballot(pk);
+    if (lane == 0 && y < H) mask[((size_t)plane * H + y) * words + blockIdx.x] = word;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// peak compaction: np.nonzero (row-major) order, one block per (frame, part)
+// ---------------------------------------------------------------------------
+
+template <typename T>
+__global__ void __launch_bounds__(256) compact_kernel(const unsigned long long* __restrict__ mask,
+                                                       const T* __restrict__ planes, int nparts, int H, int W,
+                                                       int words, char* __restrict__ result, isl_layout lay,
+                                                       int max_peaks) {
+  const int f = blockIdx.y, part = blockIdx.x;
+  const int plane = f * nparts + part;
+  const unsigned long long* mk = mask + (size_t)plane * H * words;
+  const T* src = planes + (size_t)plane * H * W;
+  char* rec = result + (size_t)f * lay.record_bytes;
+  double* peaks = (double*)(rec + lay.peaks) + (size_t)part * max_peaks * 3;
+  __shared__ int s_scan[256];
+  __shared__ int s_base;
+  const int tid = threadIdx.x;
+  const int nw = H * words;
+  if (tid == 0) s_base = 0;
+  __syncthreads();
+  for (int w0 = 0; w0 < nw; w0 += 256 * 4) {
+    // each thread owns 4 consecutive words
+    unsigned long long wv[4];
+    int cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int wi = w0 + tid * 4 + k;
+      wv[k] = wi < nw ? mk[wi] : 0ull;
+      cnt += __popcll(wv[k]);
+    }
+    s_scan[tid] = cnt;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {   // inclusive Hillis-Steele scan
+      const int v = tid >= off ? s_scan[tid - off] : 0;
+      __syncthreads();
+      s_scan[tid] += v;
+      __syncthreads();
+    }
+    int pos = s_base + s_scan[tid] - cnt;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int wi = w0 + tid * 4 + k;
+      unsigned long long w = wv[k];
+      while (w) {
+        const int b = __ffsll((long long)w) - 1;
+        w &= w - 1;
+        const int y = wi / words, x = (wi - y * words) * 64 + b;
+        if (pos < max_peaks) {
+          double* p = peaks + (size_t)pos * 3;
+          p[0] = (double)x;
+          p[1] = (double)y;
+          p[2] = (double)src[(size_t)y * W + x];
+        }
+        ++pos;
+      }
+    }
+    __syncthreads();
+    if (tid == 255) s_base += s_scan[255];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    ((int*)(rec + lay.n_peaks))[part] = s_base;
+    if (s_base > max_peaks) atomicExch((int*)(rec + lay.status), ISL_E_CAPACITY);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// PAF scoring + greedy matching + assembly (body.py:128-235), one block per frame
+// ---------------------------------------------------------------------------
+
+constexpr int MAX_SCALES = 8;
+
+struct GroupArgs {
+  MapSrc paf[MAX_SCALES];   // final-resolution PAF of each scale (sampled on demand)
+  int nscales;
+  float div_f;              // len(multiplier), as float32
+  int H, W;                 // frame size
+  int model;                // ISL_BODY25 / ISL_COCO
+  int njoint, nlimbs;
+  int max_peaks, max_pairs, max_conns, max_rows;
+  isl_layout lay;
+  char* result;
+  double* pair_score;       // [n][max_pairs]
+  int* pair_keep;           // [n][max_pairs]  (-1 rejected, else rank key)
+  int* order;               // [n][max_pairs]
+  unsigned char* used;      // [n][2][max_peaks]
+};
+
+__device__ __forceinline__ double paf_value(const GroupArgs& a, int f, int c, int y, int x) {
+  double acc = 0.0;
+  for (int s = 0; s < a.nscales; ++s) {
+    const float v = sample(a.paf[s], f, c, y, x);
+    acc = acc + (double)(v / a.div_f);   // paf_avg += + paf / len(multiplier)
+  }
+  return acc;
+}
+
+__global__ void __launch_bounds__(256) group_kernel(GroupArgs a) {
+  const int f = blockIdx.x, tid = threadIdx.x;
+  char* rec = a.result + (size_t)f * a.lay.record_bytes;
+  int* status = (int*)(rec + a.lay.status);
+  const int* n_peaks = (const int*)(rec + a.lay.n_peaks);
+  int* n_conns = (int*)(rec + a.lay.n_conns);
+  int* n_rows = (int*)(rec + a.lay.n_rows);
+  const double* peaks = (const double*)(rec + a.lay.peaks);
+  double* conns = (double*)(rec + a.lay.conns);
+  double* subset = (double*)(rec + a.lay.subset);
+  double* pscore = a.pair_score + (size_t)f * a.max_pairs;
+  int* pkeep = a.pair_keep + (size_t)f * a.max_pairs;
+  int* order = a.order + (size_t)f * a.max_pairs;
+  unsigned char* usedA = a.used + (size_t)f * 2 * a.max_peaks;
+  unsigned char* usedB = usedA + a.max_peaks;
+  const int RW = a.njoint + 1;   // subset row width
+
+  __shared__ int s_off[32];
+  __shared__ int s_nkeep;
+  __shared__ int s_rows;
+  __shared__ int s_abort;
+  if (tid == 0) {
+    int acc = 0;
+    for (int p = 0; p < a.njoint - 1; ++p) { s_off[p] = acc; acc += n_peaks[p]; }
+    s_rows = 0;
+    s_abort = *status != ISL_OK;
+  }
+  __syncthreads();
+  if (s_abort) return;
+
+  for (int k = 0; k < a.nlimbs; ++k) {
+    const int A = a.model == ISL_BODY25 ? kLimbs25[k][0] : kLimbsCoco[k][0];
+    const int B = a.model == ISL_BODY25 ? kLimbs25[k][1] : kLimbsCoco[k][1];
+    const int mx = a.model == ISL_BODY25 ? kMap25[k][0] : kMapCoco[k][0];
+    const int my = a.model == ISL_BODY25 ? kMap25[k][1] : kMapCoco[k][1];
+    const int nA = n_peaks[A], nB = n_peaks[B];
+    if (nA == 0 || nB == 0) {            // special_k
+      if (tid == 0) n_conns[k] = -1;
+      continue;
+    }
+    const int np = nA * nB;
+    if (np > a.max_pairs) {
+      if (tid == 0) { *status = ISL_E_CAPACITY; n_conns[k] = -2; }
+      return;
+    }
+    const double* pA = peaks + (size_t)A * a.max_peaks * 3;
+    const double* pB = peaks + (size_t)B * a.max_peaks * 3;
+    // --- score every (i, j) pair (body.py:142-164) ---
+    for (int p = tid; p < np; p += 256) {
+      const int i = p / nB, j = p - i * nB;
+      const long long ax = (long long)pA[i * 3], ay = (long long)pA[i * 3 + 1];
+      const long long bx = (long long)pB[j * 3], by = (long long)pB[j * 3 + 1];
+      const long long vx = bx - ax, vy = by - ay;
+      double norm = sqrt((double)(vx * vx + vy * vy));
+      norm = 0.001 < norm ? norm : 0.001;              // max(0.001, norm)
+      const double ux = (double)vx / norm, uy = (double)vy / norm;
+      const double stx = ((double)bx - (double)ax) / 9.0, sty = ((double)by - (double)ay) / 9.0;
+      double sum = 0.0;
+      int cnt = 0;
+      for (int I = 0; I < 10; ++I) {
+        const double sx = I == 9 ? (double)bx : (double)I * stx + (double)ax;   // np.linspace
+        const double sy = I == 9 ? (double)by : (double)I * sty + (double)ay;
+        const int xi = (int)rint(sx), yi = (int)rint(sy);                      // round half to even
+        const double s = paf_value(a, f, mx, yi, xi) * ux + paf_value(a, f, my, yi, xi) * uy;
+        sum = sum + s;
+        cnt += s > 0.05;
+      }
+      const double prior = 0.5 * (double)a.H / norm - 1.0;
+      const double score = sum / 10.0 + (0.0 < prior ? 0.0 : prior);
+      pscore[p] = score;
+      pkeep[p] = (cnt > 8 && score > 0.0) ? 1 : 0;
+    }
+    __syncthreads();
+    // --- stable descending sort of kept pairs: rank = #(better) ---
+    if (tid == 0) s_nkeep = 0;
+    __syncthreads();
+    for (int p = tid; p < np; p += 256) {
+      if (!pkeep[p]) continue;
+      const double sp = pscore[p];
+      int rank = 0;
+      for (int q = 0; q < np; ++q)
+        if (pkeep[q] && (pscore[q] > sp || (pscore[q] == sp && q < p))) ++rank;
+      order[rank] = p;
+      atomicAdd(&s_nkeep, 1);
+    }
+    for (int i = tid; i < nA; i += 256) usedA[i] = 0;
+    for (int j = tid; j < nB; j += 256) usedB[j] = 0;
+    __syncthreads();
+    if (tid == 0) {
+      // --- greedy matching (body.py:166-175) ---
+      double* cw = conns + (size_t)k * a.max_conns * 5;
+      const int lim = nA < nB ? nA : nB;
+      int m = 0;
+      for (int r = 0; r < s_nkeep && m < lim; ++r) {
+        const int p = order[r];
+        const int i = p / nB, j = p - i * nB;
+        if (usedA[i] || usedB[j]) continue;
+        usedA[i] = usedB[j] = 1;
+        if (m >= a.max_conns) { *status = ISL_E_CAPACITY; break; }
+        double* c = cw + (size_t)m * 5;
+        c[0] = (double)(s_off[A] + i);
+        c[1] = (double)(s_off[B] + j);
+        c[2] = pscore[p];
+        c[3] = (double)i;
+        c[4] = (double)j;
+        ++m;
+      }
+      n_conns[k] = m;
+      // --- assembly for limb k (body.py:185-225) ---
+      int rows = s_rows;
+      for (int ci = 0; ci < m && *status == ISL_OK; ++ci) {
+        const double* c = cw + (size_t)ci * 5;
+        const double idA = c[0], idB = c[1], sc = c[2];
+        int hit[2] = {-1, -1}, found = 0;
+        for (int r = 0; r < rows; ++r) {
+          const double* row = subset + (size_t)r * RW;
+          if (row[A] == idA || row[B] == idB) {
+            if (found == 2) { found = 3; break; }
+            hit[found++] = r;
+          }
+        }
+        if (found == 3) { *status = ISL_E_INDEX; break; }   // body.py:196 IndexError
+        if (found == 1) {
+          double* row = subset + (size_t)hit[0] * RW;
+          if (row[B] != idB) {
+            row[B] = idB;
+            row[RW - 1] += 1.0;
+            row[RW - 2] += peaks[((size_t)B * a.max_peaks + (int)(idB - s_off[B])) * 3 + 2] + sc;
+          }
+        } else if (found == 2) {
+          double* r1 = subset + (size_t)hit[0] * RW;
+          double* r2 = subset + (size_t)hit[1] * RW;
+          bool overlap = false;
+          for (int q = 0; q < RW - 2; ++q) overlap |= (r1[q] >= 0.0) && (r2[q] >= 0.0);
+          if (!overlap) {
+            for (int q = 0; q < RW - 2; ++q) r1[q] += r2[q] + 1.0;
+            r1[RW - 2] += r2[RW - 2];
+            r1[RW - 1] += r2[RW - 1];
+            r1[RW - 2] += sc;
+            for (int r = hit[1]; r + 1 < rows; ++r)     // np.delete(subset, j2, 0)
+              for (int q = 0; q < RW; ++q) subset[(size_t)r * RW + q] = subset[(size_t)(r + 1) * RW + q];
+            --rows;
+          } else {
+            r1[B] = idB;
+            r1[RW - 1] += 1.0;
+            r1[RW - 2] += peaks[((size_t)B * a.max_peaks + (int)(idB - s_off[B])) * 3 + 2] + sc;
+          }
+        } else if (k < a.njoint - 2) {
+          if (rows >= a.max_rows) { *status = ISL_E_CAPACITY; break; }
+          double* row = subset + (size_t)rows * RW;
+          for (int q = 0; q < RW; ++q) row[q] = -1.0;
+          row[A] = idA;
+          row[B] = idB;
+          row[RW - 1] = 2.0;
+          const double sa = peaks[((size_t)A * a.max_peaks + (int)(idA - s_off[A])) * 3 + 2];
+          const double sb = peaks[((size_t)B * a.max_peaks + (int)(idB - s_off[B])) * 3 + 2];
+          row[RW - 2] = (sa + sb) + sc;
+          ++rows;
+        }
+      }
+      s_rows = rows;
+      s_abort = *status != ISL_OK;
+    }
+    __syncthreads();
+    if (s_abort) return;
+  }
+  if (tid == 0) {
+    // prune (body.py:227-231)
+    int w = 0;
+    for (int r = 0; r < s_rows; ++r) {
+      const double* row = subset + (size_t)r * RW;
+      if (row[RW - 1] < 4.0 || row[RW - 2] / row[RW - 1] < 0.4) continue;
+      if (w != r)
+        for (int q = 0; q < RW; ++q) subset[(size_t)w * RW + q] = row[q];
+      ++w;
+    }
+    *n_rows = w;
+  }
+}
+
+__global__ void init_records_kernel(char* result, isl_layout lay, int n, int nlimbs) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n) return;
+  char* rec = result + (size_t)f * lay.record_bytes;
+  *(int*)(rec + lay.status) = ISL_OK;
+  for (int k = 0; k < 32; ++k) ((int*)(rec + lay.n_conns))[k] = k < nlimbs ? 0 : -1;
+  *(int*)(rec + lay.n_rows) = 0;
+}
+
+// ---------------------------------------------------------------------------
+// host orchestration
+// ---------------------------------------------------------------------------
+
+static inline long long al8(long long x) { return (x + 7) / 8 * 8; }
+
+}  // namespace isl
+
+using namespace isl;
+
+extern "C" int isl_body_layout(int model_kind, const isl_caps* caps, isl_layout* out) {
+  if (!caps || !out || (model_kind != ISL_BODY25 && model_kind != ISL_COCO)) {
+    set_error("isl_body_layout: bad argument");
+    return ISL_E_ARG;
+  }
+  const int njoint = model_kind == ISL_BODY25 ? 26 : 19;
+  const int nlimbs = model_kind == ISL_BODY25 ? 24 : 19;
+  long long o = 0;
+  out->status = o; o += 8;
+  out->n_peaks = o; o += 32 * 4;
+  out->n_conns = o; o += 32 * 4;
+  out->n_rows = o; o += 8;
+  out->peaks = o = al8(o); o += (long long)(njoint - 1) * caps->max_peaks * 3 * 8;
+  out->conns = o; o += (long long)nlimbs * caps->max_conns * 5 * 8;
+  out->subset = o; o += (long long)caps->max_rows * (njoint + 1) * 8;
+  out->record_bytes = al8(o);
+  return ISL_OK;
+}
+
+
+static int post_fail(int code, const char* msg) {
+  set_error(msg);
+  return code;
+}
+
+#define PHIP(expr)                                          \
+  do {                                                      \
+    hipError_t e_ = (expr);                                 \
+    if (e_ != hipSuccess) {                                 \
+      set_error(std::string(#expr) + ": " + hipGetErrorString(e_)); \
+      return ISL_E_HIP;                                     \
+    }                                                       \
+  } while (0)
+
+static int grid_for(long long total) { return (int)std::min<long long>((total + 255) / 256, 256 * 32); }
+
+// Low-res map of scale s: caller NCHW array or the net's arena output.
+static int low_src(isl_net* net, const float* p, int which, int n, int C, int h8, int w8, MapSrc* m) {
+  if (p) {
+    m->base = p;
+    m->xs = 1; m->ys = w8; m->cstr = (long long)h8 * w8; m->fs = (long long)C * h8 * w8;
+    m->sh = h8; m->sw = w8;
+    return ISL_OK;
+  }
+  const int rc = net_low_res(net, which, m);
+  if (rc) return rc;
+  if (m->sh != h8 || m->sw != w8) return post_fail(ISL_E_STATE, "arena output does not match the scale geometry");
+  return ISL_OK;
+}
+
+extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, const isl_scale_geom* geom,
+                             const float* const* d_paf, const float* const* d_heat, const isl_caps* caps,
+                             void* d_result, void* stream) {
+  if (!net || n <= 0 || H <= 0 || W <= 0 || nscales <= 0 || nscales > MAX_SCALES || !geom || !caps || !d_result)
+    return post_fail(ISL_E_ARG, "isl_body_post: bad argument");
+  const int kind = net_kind(net);
+  if (kind != ISL_BODY25 && kind != ISL_COCO) return post_fail(ISL_E_ARG, "isl_body_post needs a body net");
+  PHIP(hipSetDevice(net_device(net)));
+  hipStream_t s = (hipStream_t)stream;
+  const int njoint = kind == ISL_BODY25 ? 26 : 19, npaf = kind == ISL_BODY25 ? 52 : 38;
+  const int nparts = njoint - 1, nlimbs = kind == ISL_BODY25 ? 24 : 19;
+  isl_layout lay;
+  int rc = isl_body_layout(kind, caps, &lay);
+  if (rc) return rc;
+  // ---- scratch plan ----
+  const bool multi = nscales > 1;
+  const size_t heat_bytes = (size_t)n * nparts * H * W * (multi ? 8 : 4);
+  size_t mid_bytes = 0;
+  for (int si = 0; si < nscales; ++si) {
+    const isl_scale_geom& g = geom[si];
+    if (!(g.valid_h == H && g.valid_w == W)) mid_bytes += (size_t)n * g.valid_h * g.valid_w * (nparts + npaf) * 4;
+  }
+  const int words = (W + 63) / 64;
+  const size_t mask_bytes = (size_t)n * nparts * H * words * 8;
+  const size_t pair_bytes = (size_t)n * caps->max_pairs * (8 + 4 + 4);
+  const size_t used_bytes = (size_t)n * 2 * caps->max_peaks;
+  auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t total = up(heat_bytes) + up(mid_bytes) + up(mask_bytes) + up(pair_bytes) + up(used_bytes);
+  char* base = (char*)net_scratch(net, total);
+  if (!base) return ISL_E_HIP;
+  char* heat = base;
+  char* mid = heat + up(heat_bytes);
+  unsigned long long* mask = (unsigned long long*)(mid + up(mid_bytes));
+  char* pairs = (char*)mask + up(mask_bytes);
+  unsigned char* used = (unsigned char*)(pairs + up(pair_bytes));
+
+  hipLaunchKernelGGL(init_records_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (char*)d_result, lay, n, nlimbs);
+  PHIP(hipGetLastError());
+  if (multi) PHIP(hipMemsetAsync(heat, 0, heat_bytes, s));
+
+  GroupArgs ga;
+  memset(&ga, 0, sizeof(ga));
+  char* midp = mid;
+  const float div_f = (float)nscales;
+  for (int si = 0; si < nscales; ++si) {
+    const isl_scale_geom& g = geom[si];
+    const int h8 = g.net_h / 8, w8 = g.net_w / 8;
+    MapSrc lh, lp;
+    if ((rc = low_src(net, d_heat ? d_heat[si] : nullptr, 1, n, njoint, h8, w8, &lh))) return rc;
+    if ((rc = low_src(net, d_paf ? d_paf[si] : nullptr, 0, n, npaf, h8, w8, &lp))) return rc;
+    // stage 1: cv2.resize(fx=fy=8) -> (h8*8, w8*8); crop to (valid_h, valid_w)
+    lh.dh = lp.dh = h8 * 8; lh.dw = lp.dw = w8 * 8;
+    lh.scy = lh.scx = lp.scy = lp.scx = 1.0 / 8.0;
+    lh.cn = njoint; lp.cn = npaf;
+    lh.identity = lp.identity = 0;
+    const bool two_stage = !(g.valid_h == H && g.valid_w == W);
+    MapSrc fh, fp;   // final-resolution sources
+    if (two_stage) {
+      float* mh = (float*)midp;
+      float* mp = mh + (size_t)n * g.valid_h * g.valid_w * nparts;
+      midp += (size_t)n * g.valid_h * g.valid_w * (nparts + npaf) * 4;
+      const long long th = (long long)n * g.valid_h * g.valid_w * nparts;
+      hipLaunchKernelGGL(resize_kernel, dim3(grid_for(th)), dim3(256), 0, s, lh, n, nparts, g.valid_h, g.valid_w, 0,
+                         1.f, (void*)mh);
+      PHIP(hipGetLastError());
+      const long long tp = (long long)n * g.valid_h * g.valid_w * npaf;
+      hipLaunchKernelGGL(resize_kernel, dim3(grid_for(tp)), dim3(256), 0, s, lp, n, npaf, g.valid_h, g.valid_w, 0,
+                         1.f, (void*)mp);
+      PHIP(hipGetLastError());
+      // stage 2: cv2.resize(crop, (W, H)): inv_scale = W / valid_w, scale = 1 / inv_scale
+      auto stage2 = [&](MapSrc& m, const float* p, int C, int cn) {
+        m.base = p; m.xs = C; m.ys = (long long)g.valid_w * C; m.cstr = 1; m.fs = (long long)g.valid_h * g.valid_w * C;
+        m.sh = g.valid_h; m.sw = g.valid_w; m.dh = H; m.dw = W;
+        m.scy = 1.0 / ((double)H / g.valid_h); m.scx = 1.0 / ((double)W / g.valid_w);
+        m.cn = cn; m.identity = 0;
+      };
+      stage2(fh, mh, nparts, njoint);
+      stage2(fp, mp, npaf, npaf);
+    } else {
+      fh = lh;
+      fp = lp;
+    }
+    const long long tf = (long long)n * nparts * H * W;
+    hipLaunchKernelGGL(resize_kernel, dim3(grid_for(tf)), dim3(256), 0, s, fh, n, nparts, H, W, multi ? 2 : 1, div_f,
+                       (void*)heat);
+    PHIP(hipGetLastError());
+    ga.paf[si] = fp;
+  }
+  // blur + NMS (body.py:86-100)
+  dim3 gb(words, (H + NMS_TY - 1) / NMS_TY, n * nparts);
+  if (multi)
+    hipLaunchKernelGGL(blur_nms_kernel<double>, gb, dim3(256), 0, s, (const double*)heat, H, W, words, mask, 0.1, 0);
+  else
+    hipLaunchKernelGGL(blur_nms_kernel<float>, gb, dim3(256), 0, s, (const float*)heat, H, W, words, mask, 0.1, 0);
+  PHIP(hipGetLastError());
+  if (multi)
+    hipLaunchKernelGGL(compact_kernel<double>, dim3(nparts, n), dim3(256), 0, s, mask, (const double*)heat, nparts, H,
+                       W, words, (char*)d_result, lay, caps->max_peaks);
+  else
+    hipLaunchKernelGGL(compact_kernel<float>, dim3(nparts, n), dim3(256), 0, s, mask, (const float*)heat, nparts, H,
+                       W, words, (char*)d_result, lay, caps->max_peaks);
+  PHIP(hipGetLastError());
+  ga.nscales = nscales;
+  ga.div_f = div_f;
+  ga.H = H; ga.W = W;
+  ga.model = kind; ga.njoint = njoint; ga.nlimbs = nlimbs;
+  ga.max_peaks = caps->max_peaks; ga.max_pairs = caps->max_pairs; ga.max_conns = caps->max_conns;
+  ga.max_rows = caps->max_rows;
+  ga.lay = lay;
+  ga.result = (char*)d_result;
+  ga.pair_score = (double*)pairs;
+  ga.pair_keep = (int*)(pairs + (size_t)n * caps->max_pairs * 8);
+  ga.order = ga.pair_keep + (size_t)n * caps->max_pairs;
+  ga.used = used;
+  hipLaunchKernelGGL(group_kernel, dim3(n), dim3(256), 0, s, ga);
+  PHIP(hipGetLastError());
+  return ISL_OK;
+}
+
+extern "C" int isl_hand_post(isl_net* net, int n, int w, int nscales, const isl_scale_geom* geom,
+                             const float* const* d_heat, int64_t* d_peaks, void* stream) {
+  (void)net; (void)n; (void)w; (void)nscales; (void)geom; (void)d_heat; (void)d_peaks; (void)stream;
+  return post_fail(ISL_E_STATE, "isl_hand_post: not built yet");
+}

@@ -1,0 +1,607 @@
+// libislpose runtime: network graphs, weight packing, activation arena and the
+// C ABI of include/islpose.h.
+//
+// The three networks of src/model.py are rebuilt here as static graphs over
+// padded-NHWC buffers.  Every torch.cat of the reference (model.py:177, 190,
+// 199, 308-324, 397-405) becomes a channel-slice layout decision: producers
+// write their slice of a shared buffer, consumers read the whole span, and the
+// conv weights are repacked so that logical input channel order (the concat
+// order of the reference) maps onto the physical slices.
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "islpose.h"
+
+namespace isl {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+static int fail(int code, const std::string& msg) {
+  set_error(msg);
+  return code;
+}
+
+#define HIP_OK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess) {                                                           \
+      std::string m_ = g_err.empty() ? "" : (" (" + g_err + ")");                     \
+      return fail(ISL_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_) + m_); \
+    }                                                                                 \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// layer tables (model.py)
+// ---------------------------------------------------------------------------
+
+struct Seg {
+  int logical, phys, len;  // logical input channels [logical, logical+len) live at physical offset phys
+};
+
+struct ConvLayer {
+  std::string name, prelu;
+  int cin = 0, cout = 0, k = 0, act = ACT_RELU;
+  std::vector<float> w, b, s;
+  bool has_w = false, has_b = false, has_s = false;
+  std::vector<Seg> cmap;
+  int cin_phys = 0, bco = 0;
+  float *d_w = nullptr, *d_b = nullptr, *d_s = nullptr;
+};
+
+static ConvLayer mk(const std::string& name, int cin, int cout, int k, int act, const std::string& prelu = "") {
+  ConvLayer c;
+  c.name = name; c.cin = cin; c.cout = cout; c.k = k; c.act = act; c.prelu = prelu;
+  return c;
+}
+
+static void vgg_front(std::vector<ConvLayer>& L, bool hand, const std::vector<std::string>& prelu) {
+  struct { const char* n; int ci, co; } t[] = {
+      {"conv1_1", 3, 64},    {"conv1_2", 64, 64},   {"conv2_1", 64, 128},  {"conv2_2", 128, 128},
+      {"conv3_1", 128, 256}, {"conv3_2", 256, 256}, {"conv3_3", 256, 256}, {"conv3_4", 256, 256},
+      {"conv4_1", 256, 512}, {"conv4_2", 512, 512}};
+  for (auto& e : t) {
+    const bool p = std::find(prelu.begin(), prelu.end(), e.n) != prelu.end();
+    // make_layers: PReLU named 'prelu' + name[4:] (model.py:43)
+    L.push_back(mk(e.n, e.ci, e.co, 3, p ? ACT_PRELU : ACT_RELU, p ? "prelu" + std::string(e.n + 4) : ""));
+  }
+  if (hand) {
+    L.push_back(mk("conv4_3", 512, 512, 3, ACT_RELU));
+    L.push_back(mk("conv4_4", 512, 512, 3, ACT_RELU));
+    L.push_back(mk("conv5_1", 512, 512, 3, ACT_RELU));
+    L.push_back(mk("conv5_2", 512, 512, 3, ACT_RELU));
+    L.push_back(mk("conv5_3_CPM", 512, 128, 3, ACT_RELU));
+  } else {
+    for (auto n : {"conv4_3_CPM", "conv4_4_CPM"}) {
+      const bool p = std::find(prelu.begin(), prelu.end(), n) != prelu.end();
+      const int ci = std::string(n) == "conv4_3_CPM" ? 512 : 256, co = ci == 512 ? 256 : 128;
+      L.push_back(mk(n, ci, co, 3, p ? ACT_PRELU : ACT_RELU, p ? "prelu" + std::string(n + 4) : ""));
+    }
+  }
+}
+
+static std::vector<ConvLayer> body25_layers() {  // model.py:66-165
+  std::vector<ConvLayer> L;
+  vgg_front(L, false, {"conv4_2", "conv4_3_CPM", "conv4_4_CPM"});
+  const std::vector<std::string> no_act = {"Mconv7_stage0_L1", "Mconv7_stage0_L2", "Mconv7_stage1_L1",
+                                           "Mconv7_stage1_L2", "Mconv7_stage2_L2", "Mconv7_stage3_L2"};
+  auto mc = [&](const std::string& n, int ci, int co, int k) {
+    const bool none = std::find(no_act.begin(), no_act.end(), n) != no_act.end();
+    // make_layers_Mconv: PReLU 'Mprelu' + name[5:] (model.py:61-62)
+    L.push_back(mk(n, ci, co, k, none ? ACT_NONE : ACT_PRELU, none ? "" : "Mprelu" + n.substr(5)));
+  };
+  auto stage = [&](const std::string& tag, int cin, int w, int c6, int cout) {
+    for (int b = 1; b <= 5; ++b)
+      for (int j = 0; j < 3; ++j)
+        mc("Mconv" + std::to_string(b) + "_" + tag + "_" + std::to_string(j), j ? w : (b == 1 ? cin : 3 * w), w, 3);
+    mc("Mconv6_" + tag, 3 * w, c6, 1);
+    mc("Mconv7_" + tag, c6, cout, 1);
+  };
+  stage("stage0_L2", 128, 96, 256, 52);
+  for (int s = 1; s < 4; ++s) stage("stage" + std::to_string(s) + "_L2", 180, 128, 512, 52);
+  stage("stage0_L1", 180, 96, 256, 26);
+  stage("stage1_L1", 206, 128, 512, 26);
+  return L;
+}
+
+static std::vector<ConvLayer> coco_layers() {  // model.py:210-299
+  std::vector<ConvLayer> L;
+  vgg_front(L, false, {});
+  // model.py:215-218: 'Mconv7_stage6_L1' listed twice, 'Mconv7_stage6_L2' never -> keeps its ReLU
+  auto none = [](const std::string& n) {
+    if (n == "conv5_5_CPM_L1" || n == "conv5_5_CPM_L2" || n == "Mconv7_stage6_L1") return true;
+    for (int i = 2; i <= 5; ++i)
+      for (int b = 1; b <= 2; ++b)
+        if (n == "Mconv7_stage" + std::to_string(i) + "_L" + std::to_string(b)) return true;
+    return false;
+  };
+  auto c = [&](const std::string& n, int ci, int co, int k) { L.push_back(mk(n, ci, co, k, none(n) ? ACT_NONE : ACT_RELU)); };
+  for (int br = 1; br <= 2; ++br) {
+    const std::string s = "_L" + std::to_string(br);
+    c("conv5_1_CPM" + s, 128, 128, 3); c("conv5_2_CPM" + s, 128, 128, 3); c("conv5_3_CPM" + s, 128, 128, 3);
+    c("conv5_4_CPM" + s, 128, 512, 1); c("conv5_5_CPM" + s, 512, br == 1 ? 38 : 19, 1);
+  }
+  for (int i = 2; i <= 6; ++i)
+    for (int br = 1; br <= 2; ++br) {
+      const std::string s = "_stage" + std::to_string(i) + "_L" + std::to_string(br);
+      c("Mconv1" + s, 185, 128, 7);
+      for (int j = 2; j <= 5; ++j) c("Mconv" + std::to_string(j) + s, 128, 128, 7);
+      c("Mconv6" + s, 128, 128, 1);
+      c("Mconv7" + s, 128, br == 1 ? 38 : 19, 1);
+    }
+  return L;
+}
+
+static std::vector<ConvLayer> hand_layers() {  // model.py:331-392
+  std::vector<ConvLayer> L;
+  vgg_front(L, true, {});
+  L.push_back(mk("conv6_1_CPM", 128, 512, 1, ACT_RELU));
+  L.push_back(mk("conv6_2_CPM", 512, 22, 1, ACT_NONE));
+  for (int i = 2; i <= 6; ++i) {
+    const std::string s = "_stage" + std::to_string(i);
+    L.push_back(mk("Mconv1" + s, 150, 128, 7, ACT_RELU));
+    for (int j = 2; j <= 5; ++j) L.push_back(mk("Mconv" + std::to_string(j) + s, 128, 128, 7, ACT_RELU));
+    L.push_back(mk("Mconv6" + s, 128, 128, 1, ACT_RELU));
+    L.push_back(mk("Mconv7" + s, 128, 22, 1, ACT_NONE));
+  }
+  return L;
+}
+
+// ---------------------------------------------------------------------------
+// graph
+// ---------------------------------------------------------------------------
+
+struct BufSpec {
+  int level, cs, pad;
+};
+
+struct Op {
+  int type;  // 0 conv, 1 maxpool
+  int layer;
+  int in, in_coff, out, out_coff, C;
+};
+
+struct OutRef {
+  int buf, coff, C;
+};
+
+}  // namespace isl
+
+using namespace isl;
+
+struct isl_net {
+  int kind = 0, device = 0;
+  std::vector<ConvLayer> layers;
+  std::map<std::string, int> layer_index;
+  std::vector<std::pair<std::string, int64_t>> params;  // caffe name, numel
+  std::vector<BufSpec> bufs;
+  std::vector<Op> ops;
+  int in_buf = 0;
+  OutRef out0{}, out1{};
+  int n_out = 2;
+  bool packed = false;
+  // plan
+  int pn = 0, ph = 0, pw = 0;
+  std::vector<Act> act;
+  void* arena = nullptr;
+  size_t arena_bytes = 0;
+  // post scratch
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+};
+
+namespace isl {
+
+static int round8(int c) { return (c + 7) / 8 * 8; }
+
+struct Builder {
+  isl_net* net;
+  int buf(int level, int cs, int pad) {
+    net->bufs.push_back({level, cs, pad});
+    return (int)net->bufs.size() - 1;
+  }
+  int L(const std::string& name) {
+    auto it = net->layer_index.find(name);
+    if (it == net->layer_index.end()) {
+      fprintf(stderr, "islpose: graph references unknown layer %s\n", name.c_str());
+      abort();
+    }
+    return it->second;
+  }
+  // conv reading logical channels through `cmap` (relative to in_coff)
+  void conv(const std::string& name, int in, int in_coff, int out, int out_coff, std::vector<Seg> cmap = {},
+            int cin_phys = 0) {
+    const int li = L(name);
+    ConvLayer& c = net->layers[li];
+    if (cmap.empty()) cmap = {{0, 0, c.cin}};
+    if (!cin_phys) cin_phys = round8(c.cin);
+    c.cmap = cmap;
+    c.cin_phys = cin_phys;
+    c.bco = conv_bco_for(c.cout);
+    net->ops.push_back({0, li, in, in_coff, out, out_coff, 0});
+  }
+  void pool(int in, int out, int C) { net->ops.push_back({1, -1, in, 0, out, 0, C}); }
+
+  // shared VGG front; returns the level-3 buffer written by the last front conv
+  void front(int X, bool hand, int out_buf, int out_coff, int pad3) {
+    int A1 = buf(0, 64, 1), A2 = buf(0, 64, 1), B1 = buf(1, 64, 1), B2 = buf(1, 128, 1), B3 = buf(1, 128, 1);
+    int C1 = buf(2, 128, 1), C2 = buf(2, 256, 1), C3 = buf(2, 256, 1);
+    int D1 = buf(3, 256, 1), D2 = buf(3, 512, 1), D3 = buf(3, 512, 1);
+    (void)pad3;
+    conv("conv1_1", X, 0, A1, 0);
+    conv("conv1_2", A1, 0, A2, 0);
+    pool(A2, B1, 64);
+    conv("conv2_1", B1, 0, B2, 0);
+    conv("conv2_2", B2, 0, B3, 0);
+    pool(B3, C1, 128);
+    conv("conv3_1", C1, 0, C2, 0);
+    conv("conv3_2", C2, 0, C3, 0);
+    conv("conv3_3", C3, 0, C2, 0);
+    conv("conv3_4", C2, 0, C3, 0);
+    pool(C3, D1, 256);
+    conv("conv4_1", D1, 0, D2, 0);
+    conv("conv4_2", D2, 0, D3, 0);
+    if (hand) {
+      conv("conv4_3", D3, 0, D2, 0);
+      conv("conv4_4", D2, 0, D3, 0);
+      conv("conv5_1", D3, 0, D2, 0);
+      conv("conv5_2", D2, 0, D3, 0);
+      conv("conv5_3_CPM", D3, 0, out_buf, out_coff);
+    } else {
+      conv("conv4_3_CPM", D3, 0, D2, 0);
+      conv("conv4_4_CPM", D2, 0, out_buf, out_coff);
+    }
+  }
+};
+
+static void build_body25(isl_net* net) {
+  Builder b{net};
+  const int X = b.buf(0, 8, 1);
+  net->in_buf = X;
+  // stage input: [out0 0:128 | paf 128:180 (gap to 184) | heat0 184:210 (gap to 216)]
+  const int SIN = b.buf(3, 216, 1), CA = b.buf(3, 384, 1), CB = b.buf(3, 384, 1), T6 = b.buf(3, 512, 1);
+  const int HOUT = b.buf(3, 32, 1);
+  b.front(X, false, SIN, 0, 1);
+  auto stage = [&](const std::string& tag, int w, std::vector<Seg> cmap, int cin_phys, int out, int out_coff) {
+    int cur = CA, oth = CB;
+    for (int j = 0; j < 3; ++j)
+      b.conv("Mconv1_" + tag + "_" + std::to_string(j), j ? cur : SIN, j ? (j - 1) * w : 0, cur, j * w,
+             j ? std::vector<Seg>{} : cmap, j ? 0 : cin_phys);
+    for (int blk = 2; blk <= 5; ++blk) {
+      for (int j = 0; j < 3; ++j)
+        b.conv("Mconv" + std::to_string(blk) + "_" + tag + "_" + std::to_string(j), j ? oth : cur,
+               j ? (j - 1) * w : 0, oth, j * w);
+      std::swap(cur, oth);
+    }
+    b.conv("Mconv6_" + tag, cur, 0, T6, 0);
+    b.conv("Mconv7_" + tag, T6, 0, out, out_coff);
+  };
+  // model.py:183-190: L2 stages; stage 0 sees out0, stages 1-3 cat(out0, paf)
+  stage("stage0_L2", 96, {{0, 0, 128}}, 128, SIN, 128);
+  for (int s = 1; s < 4; ++s) stage("stage" + std::to_string(s) + "_L2", 128, {{0, 0, 180}}, 184, SIN, 128);
+  // model.py:193-198: L1 stage 0 on cat(out0, paf)
+  stage("stage0_L1", 96, {{0, 0, 180}}, 184, SIN, 184);
+  // model.py:199-205: L1 stage 1 on cat(out0, heat0, paf) — logical order mapped onto physical slices
+  stage("stage1_L1", 128, {{0, 0, 128}, {128, 184, 26}, {154, 128, 52}}, 216, HOUT, 0);
+  net->out0 = {SIN, 128, 52};
+  net->out1 = {HOUT, 0, 26};
+  net->n_out = 2;
+}
+
+static void build_coco(isl_net* net) {
+  Builder b{net};
+  const int X = b.buf(0, 8, 1);
+  net->in_buf = X;
+  // stage input: [L1 0:38 (gap 40) | L2 40:59 (gap 64) | out1 64:192]; 7x7 consumers -> ring 3
+  const int SIN = b.buf(3, 192, 3), T1 = b.buf(3, 128, 3), T2 = b.buf(3, 128, 3);
+  const int T5a = b.buf(3, 512, 1), T5b = b.buf(3, 512, 1), T6a = b.buf(3, 128, 1), T6b = b.buf(3, 128, 1);
+  b.front(X, false, SIN, 64, 3);
+  // stage 1 (model.py:306-308): both branches read out1, write their slices last
+  for (int br = 1; br <= 2; ++br) {
+    const std::string s = "_L" + std::to_string(br);
+    b.conv("conv5_1_CPM" + s, SIN, 64, T1, 0);
+    b.conv("conv5_2_CPM" + s, T1, 0, T2, 0);
+    b.conv("conv5_3_CPM" + s, T2, 0, T1, 0);
+    b.conv("conv5_4_CPM" + s, T1, 0, br == 1 ? T5a : T5b, 0);
+  }
+  b.conv("conv5_5_CPM_L1", T5a, 0, SIN, 0);
+  b.conv("conv5_5_CPM_L2", T5b, 0, SIN, 40);
+  const std::vector<Seg> cmap = {{0, 0, 38}, {38, 40, 19}, {57, 64, 128}};  // cat(L1, L2, out1)
+  for (int i = 2; i <= 6; ++i) {
+    for (int br = 1; br <= 2; ++br) {
+      const std::string s = "_stage" + std::to_string(i) + "_L" + std::to_string(br);
+      b.conv("Mconv1" + s, SIN, 0, T1, 0, cmap, 192);
+      b.conv("Mconv2" + s, T1, 0, T2, 0);
+      b.conv("Mconv3" + s, T2, 0, T1, 0);
+      b.conv("Mconv4" + s, T1, 0, T2, 0);
+      b.conv("Mconv5" + s, T2, 0, T1, 0);
+      b.conv("Mconv6" + s, T1, 0, br == 1 ? T6a : T6b, 0);
+    }
+    // both branches have consumed SIN; now overwrite its L1/L2 slices
+    b.conv("Mconv7_stage" + std::to_string(i) + "_L1", T6a, 0, SIN, 0);
+    b.conv("Mconv7_stage" + std::to_string(i) + "_L2", T6b, 0, SIN, 40);
+  }
+  net->out0 = {SIN, 0, 38};
+  net->out1 = {SIN, 40, 19};
+  net->n_out = 2;
+}
+
+static void build_hand(isl_net* net) {
+  Builder b{net};
+  const int X = b.buf(0, 8, 1);
+  net->in_buf = X;
+  // stage input: [stage output 0:22 (gap 24) | out1_0 24:152]
+  const int SIN = b.buf(3, 152, 3), T1 = b.buf(3, 128, 3), T2 = b.buf(3, 128, 3);
+  const int T5 = b.buf(3, 512, 1), T6 = b.buf(3, 128, 1);
+  b.front(X, true, SIN, 24, 3);
+  b.conv("conv6_1_CPM", SIN, 24, T5, 0);
+  b.conv("conv6_2_CPM", T5, 0, SIN, 0);
+  const std::vector<Seg> cmap = {{0, 0, 22}, {22, 24, 128}};  // cat(prev, out1_0), model.py:397-405
+  for (int i = 2; i <= 6; ++i) {
+    const std::string s = "_stage" + std::to_string(i);
+    b.conv("Mconv1" + s, SIN, 0, T1, 0, cmap, 152);
+    b.conv("Mconv2" + s, T1, 0, T2, 0);
+    b.conv("Mconv3" + s, T2, 0, T1, 0);
+    b.conv("Mconv4" + s, T1, 0, T2, 0);
+    b.conv("Mconv5" + s, T2, 0, T1, 0);
+    b.conv("Mconv6" + s, T1, 0, T6, 0);
+    b.conv("Mconv7" + s, T6, 0, SIN, 0);
+  }
+  net->out0 = {SIN, 0, 22};
+  net->n_out = 1;
+}
+
+// Repack OIHW weights into [co_tile][chunk][ky][kx][plane(2)][BCO][4] (see conv.hip).
+static std::vector<float> pack_weights(const ConvLayer& c) {
+  const int ks = c.k, bco = c.bco, chunks = c.cin_phys / 8;
+  const int co_tiles = (c.cout + bco - 1) / bco;
+  std::vector<int> p2l(c.cin_phys, -1);
+  for (const Seg& s : c.cmap)
+    for (int i = 0; i < s.len; ++i) p2l[s.phys + i] = s.logical + i;
+  std::vector<float> out((size_t)co_tiles * chunks * ks * ks * 2 * bco * 4, 0.f);
+  size_t idx = 0;
+  for (int ct = 0; ct < co_tiles; ++ct)
+    for (int ch = 0; ch < chunks; ++ch)
+      for (int ky = 0; ky < ks; ++ky)
+        for (int kx = 0; kx < ks; ++kx)
+          for (int pl = 0; pl < 2; ++pl)
+            for (int i = 0; i < bco; ++i)
+              for (int e = 0; e < 4; ++e, ++idx) {
+                const int co = ct * bco + i, lci = p2l[ch * 8 + pl * 4 + e];
+                if (co < c.cout && lci >= 0) out[idx] = c.w[(((size_t)co * c.cin + lci) * ks + ky) * ks + kx];
+              }
+  return out;
+}
+
+static int upload_params(isl_net* net) {
+  for (ConvLayer& c : net->layers) {
+    if (!c.has_w || !c.has_b || (c.act == ACT_PRELU && !c.has_s))
+      return fail(ISL_E_STATE, "parameter missing for layer " + c.name);
+    std::vector<float> wp = pack_weights(c);
+    const int co_tiles = (c.cout + c.bco - 1) / c.bco;
+    std::vector<float> bp((size_t)co_tiles * c.bco, 0.f), sp((size_t)co_tiles * c.bco, 0.f);
+    std::copy(c.b.begin(), c.b.end(), bp.begin());
+    if (c.act == ACT_PRELU) std::copy(c.s.begin(), c.s.end(), sp.begin());
+    if (!c.d_w) HIP_OK(hipMalloc(&c.d_w, wp.size() * sizeof(float)));
+    if (!c.d_b) HIP_OK(hipMalloc(&c.d_b, bp.size() * sizeof(float)));
+    if (!c.d_s) HIP_OK(hipMalloc(&c.d_s, sp.size() * sizeof(float)));
+    HIP_OK(hipMemcpy(c.d_w, wp.data(), wp.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c.d_b, bp.data(), bp.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(c.d_s, sp.data(), sp.size() * sizeof(float), hipMemcpyHostToDevice));
+  }
+  net->packed = true;
+  return ISL_OK;
+}
+
+static int plan(isl_net* net, int n, int h, int w) {
+  if (net->pn == n && net->ph == h && net->pw == w && net->arena) return ISL_OK;
+  if (n <= 0 || h < 8 || w < 8) return fail(ISL_E_ARG, "net input must be at least 8x8 with n >= 1");
+  int lh[4] = {h, h / 2, h / 4, h / 8}, lw[4] = {w, w / 2, w / 4, w / 8};
+  if (net->arena) { (void)hipFree(net->arena); net->arena = nullptr; }
+  net->act.assign(net->bufs.size(), Act{});
+  size_t total = 0;
+  std::vector<size_t> offs;
+  for (size_t i = 0; i < net->bufs.size(); ++i) {
+    const BufSpec& b = net->bufs[i];
+    Act& a = net->act[i];
+    a.n = n; a.H = lh[b.level]; a.W = lw[b.level]; a.pad = b.pad; a.cs = b.cs;
+    offs.push_back(total);
+    total += (a.bytes() + 255) / 256 * 256;
+  }
+  HIP_OK(hipMalloc(&net->arena, total));
+  HIP_OK(hipMemset(net->arena, 0, total));  // zero rings and gap channels, once
+  for (size_t i = 0; i < net->bufs.size(); ++i) net->act[i].base = (float*)((char*)net->arena + offs[i]);
+  net->arena_bytes = total;
+  net->pn = n; net->ph = h; net->pw = w;
+  return ISL_OK;
+}
+
+static int run_ops(isl_net* net, hipStream_t s) {
+  for (const Op& op : net->ops) {
+    const Act& in = net->act[op.in];
+    const Act& out = net->act[op.out];
+    if (op.type == 1) {
+      HIP_OK(launch_maxpool2(in, out, op.C, s));
+      continue;
+    }
+    const ConvLayer& c = net->layers[op.layer];
+    ConvLaunch L;
+    L.in = in.base; L.in_pad = in.pad; L.in_cs = in.cs; L.in_coff = op.in_coff;
+    L.out = out.base; L.out_pad = out.pad; L.out_cs = out.cs; L.out_coff = op.out_coff;
+    L.wpk = c.d_w; L.bias = c.d_b; L.slope = c.d_s;
+    L.n = in.n; L.H = in.H; L.W = in.W; L.ks = c.k; L.cin_chunks = c.cin_phys / 8;
+    L.cout = c.cout; L.bco = c.bco; L.act = c.act;
+    HIP_OK(launch_conv(L, s));
+  }
+  return ISL_OK;
+}
+
+static int copy_outputs(isl_net* net, float* d_out0, float* d_out1, hipStream_t s) {
+  if (d_out0) HIP_OK(launch_unpack_nchw(net->act[net->out0.buf], net->out0.coff, net->out0.C, d_out0, s));
+  if (d_out1 && net->n_out > 1)
+    HIP_OK(launch_unpack_nchw(net->act[net->out1.buf], net->out1.coff, net->out1.C, d_out1, s));
+  return ISL_OK;
+}
+
+int net_kind(const isl_net* net) { return net->kind; }
+int net_device(const isl_net* net) { return net->device; }
+
+int net_low_res(isl_net* net, int which, MapSrc* m) {
+  if (!net->arena) return fail(ISL_E_STATE, "no network output in the arena (run the net first)");
+  const OutRef& o = which == 0 ? net->out0 : net->out1;
+  const Act& a = net->act[o.buf];
+  const int Wp = a.W + 2 * a.pad;
+  m->base = a.base + ((size_t)a.pad * Wp + a.pad) * a.cs + o.coff;
+  m->xs = a.cs; m->ys = (long long)Wp * a.cs; m->cstr = 1; m->fs = (long long)a.frame_elems();
+  m->sh = a.H; m->sw = a.W;
+  return ISL_OK;
+}
+
+void* net_scratch(isl_net* net, size_t bytes) {
+  if (bytes <= net->scratch_bytes) return net->scratch;
+  if (net->scratch) { (void)hipFree(net->scratch); net->scratch = nullptr; net->scratch_bytes = 0; }
+  hipError_t e = hipMalloc(&net->scratch, bytes);
+  if (e != hipSuccess) { set_error(std::string("scratch hipMalloc: ") + hipGetErrorString(e)); return nullptr; }
+  net->scratch_bytes = bytes;
+  return net->scratch;
+}
+
+}  // namespace isl
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+
+extern "C" {
+
+int isl_abi_version(void) { return ISL_ABI_VERSION; }
+const char* isl_last_error(void) { return isl::g_err.c_str(); }
+
+int isl_net_create(int kind, int device, isl_net** out) {
+  if (!out) return fail(ISL_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (kind < ISL_BODY25 || kind > ISL_HAND) return fail(ISL_E_ARG, "unknown net kind");
+  isl_net* net = new isl_net();
+  net->kind = kind;
+  net->device = device;
+  net->layers = kind == ISL_BODY25 ? body25_layers() : kind == ISL_COCO ? coco_layers() : hand_layers();
+  for (size_t i = 0; i < net->layers.size(); ++i) {
+    const ConvLayer& c = net->layers[i];
+    net->layer_index[c.name] = (int)i;
+    net->params.push_back({c.name + ".weight", (int64_t)c.cout * c.cin * c.k * c.k});
+    net->params.push_back({c.name + ".bias", (int64_t)c.cout});
+    if (c.act == ACT_PRELU) net->params.push_back({c.prelu + ".weight", (int64_t)c.cout});
+  }
+  if (kind == ISL_BODY25) build_body25(net);
+  else if (kind == ISL_COCO) build_coco(net);
+  else build_hand(net);
+  *out = net;
+  return ISL_OK;
+}
+
+int isl_net_destroy(isl_net* net) {
+  if (!net) return ISL_OK;
+  (void)hipSetDevice(net->device);
+  for (ConvLayer& c : net->layers) {
+    if (c.d_w) (void)hipFree(c.d_w);
+    if (c.d_b) (void)hipFree(c.d_b);
+    if (c.d_s) (void)hipFree(c.d_s);
+  }
+  if (net->arena) (void)hipFree(net->arena);
+  if (net->scratch) (void)hipFree(net->scratch);
+  delete net;
+  return ISL_OK;
+}
+
+int isl_net_param_count(const isl_net* net) { return net ? (int)net->params.size() : fail(ISL_E_ARG, "net is NULL"); }
+
+int isl_net_param_info(const isl_net* net, int index, const char** name, int64_t* numel) {
+  if (!net || index < 0 || index >= (int)net->params.size()) return fail(ISL_E_ARG, "bad parameter index");
+  if (name) *name = net->params[index].first.c_str();
+  if (numel) *numel = net->params[index].second;
+  return ISL_OK;
+}
+
+int isl_net_set_param(isl_net* net, const char* caffe_name, const float* host, int64_t numel) {
+  if (!net || !caffe_name || !host) return fail(ISL_E_ARG, "NULL argument");
+  std::string nm(caffe_name);
+  const size_t dot = nm.rfind('.');
+  if (dot == std::string::npos || (nm.substr(dot) != ".weight" && nm.substr(dot) != ".bias"))
+    return fail(ISL_E_PARAM, nm);
+  const std::string base = nm.substr(0, dot), field = nm.substr(dot + 1);
+  for (ConvLayer& c : net->layers) {
+    std::vector<float>* dst = nullptr;
+    bool* flag = nullptr;
+    int64_t want = 0;
+    if (c.name == base && field == "weight") { dst = &c.w; flag = &c.has_w; want = (int64_t)c.cout * c.cin * c.k * c.k; }
+    else if (c.name == base && field == "bias") { dst = &c.b; flag = &c.has_b; want = c.cout; }
+    else if (!c.prelu.empty() && c.prelu == base && field == "weight") { dst = &c.s; flag = &c.has_s; want = c.cout; }
+    if (!dst) continue;
+    if (numel != want)
+      return fail(ISL_E_PARAM, nm + ": expected " + std::to_string(want) + " elements, got " + std::to_string(numel));
+    dst->assign(host, host + numel);
+    *flag = true;
+    net->packed = false;
+    return ISL_OK;
+  }
+  return fail(ISL_E_PARAM, nm);
+}
+
+static int prepare(isl_net* net) {
+  HIP_OK(hipSetDevice(net->device));
+  if (!net->packed) return upload_params(net);
+  return ISL_OK;
+}
+
+int isl_net_forward(isl_net* net, const float* d_x, int n, int h, int w, float* d_out0, float* d_out1, void* stream) {
+  if (!net || !d_x || !d_out0) return fail(ISL_E_ARG, "NULL argument");
+  if (net->n_out == 1 && d_out1) return fail(ISL_E_ARG, "hand net has a single output");
+  if (net->n_out == 2 && !d_out1) return fail(ISL_E_ARG, "body nets have two outputs");
+  int rc = prepare(net);
+  if (rc) return rc;
+  if ((rc = plan(net, n, h, w))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_OK(launch_pack_nchw(d_x, n, 3, h, w, net->act[net->in_buf], s));
+  if ((rc = run_ops(net, s))) return rc;
+  return copy_outputs(net, d_out0, d_out1, s);
+}
+
+int isl_net_preprocess(isl_net* net, const uint8_t* d_frames, int n, int H, int W, double scale, int* net_h,
+                       int* net_w, void* stream) {
+  if (!net || !d_frames || n <= 0 || H <= 0 || W <= 0 || !(scale > 0)) return fail(ISL_E_ARG, "bad argument");
+  // cv::resize dsize from fx/fy: saturate_cast<int>(W*fx) = cvRound (half to even)
+  const int rh = (int)std::nearbyint(H * scale), rw = (int)std::nearbyint(W * scale);
+  const int ph = (rh + 7) / 8 * 8, pw = (rw + 7) / 8 * 8;  // padRightDownCorner (util.py:12-32)
+  int rc = prepare(net);
+  if (rc) return rc;
+  if ((rc = plan(net, n, ph, pw))) return rc;
+  HIP_OK(launch_preprocess(d_frames, n, H, W, scale, rh, rw, net->act[net->in_buf], (hipStream_t)stream));
+  if (net_h) *net_h = ph;
+  if (net_w) *net_w = pw;
+  return ISL_OK;
+}
+
+int isl_net_debug_input(isl_net* net, float* d_x, void* stream) {
+  if (!net || !net->arena || !d_x) return fail(ISL_E_STATE, "no input buffer yet");
+  HIP_OK(hipSetDevice(net->device));
+  HIP_OK(launch_unpack_nchw(net->act[net->in_buf], 0, 3, d_x, (hipStream_t)stream));
+  return ISL_OK;
+}
+
+int isl_net_run(isl_net* net, float* d_out0, float* d_out1, void* stream) {
+  if (!net || !net->arena) return fail(ISL_E_STATE, "isl_net_run before isl_net_preprocess");
+  int rc = prepare(net);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if ((rc = run_ops(net, s))) return rc;
+  return copy_outputs(net, d_out0, d_out1, s);
+}
+
+}  // extern "C"

@@ -1,0 +1,178 @@
+"""Batched body-pose estimation on the HIP path (frame seam of src/body.py).
+
+``BodyEstimator.estimate(frames)`` runs, for every scale of ``scale_search``
+(body.py:41, default ``[0.5]``), the fused pre-processing kernel and the
+body_25 / COCO network, then the post-processing kernels (resize, fp64 blur +
+NMS, PAF scoring, greedy matching, assembly), and decodes the per-frame result
+records into the reference's return values ``(candidate, subset)``
+(body.py:235): ``candidate`` float64 [N,4] (x, y, score, id) or shape (0,),
+``subset`` float64 [P, njoint+1].
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import runtime as rt
+
+BOXSIZE, STRIDE = 368, 8
+NJOINT = {rt.ISL_BODY25: 26, rt.ISL_COCO: 19}
+NPAF = {rt.ISL_BODY25: 52, rt.ISL_COCO: 38}
+NLIMBS = {rt.ISL_BODY25: 24, rt.ISL_COCO: 19}
+KINDS = {"body25": rt.ISL_BODY25, "coco": rt.ISL_COCO}
+DEFAULT_CAPS = dict(max_peaks=128, max_pairs=4096, max_conns=128, max_rows=128)
+
+
+def cv_round(x: float) -> int:
+    return int(np.rint(x))
+
+
+def scale_geometry(H: int, W: int, scale_search):
+    """Per scale: (multiplier, net_h, net_w, valid_h, valid_w) as body.py:47-54 computes them."""
+    out = []
+    for s in scale_search:
+        m = s * BOXSIZE / H
+        vh, vw = cv_round(H * m), cv_round(W * m)
+        out.append((m, -(-vh // STRIDE) * STRIDE, -(-vw // STRIDE) * STRIDE, vh, vw))
+    return out
+
+
+class FrameResult:
+    __slots__ = ("candidate", "subset", "all_peaks", "connection_all", "special_k")
+
+    def __init__(self, candidate, subset, all_peaks, connection_all, special_k):
+        self.candidate, self.subset = candidate, subset
+        self.all_peaks, self.connection_all, self.special_k = all_peaks, connection_all, special_k
+
+
+class BodyEstimator:
+    def __init__(self, weights: dict, model_type: str = "body25", device: int = 0, scale_search=(0.5,), caps=None):
+        self.kind = KINDS[model_type]
+        self.model_type = model_type
+        self.device = device
+        self.scale_search = tuple(scale_search)
+        self.caps = dict(DEFAULT_CAPS, **(caps or {}))
+        self.net = rt.Net(self.kind, device)
+        self.net.load_weights(weights)
+        self.njoint, self.npaf = NJOINT[self.kind], NPAF[self.kind]
+
+    # -- network -----------------------------------------------------------------
+    def run_scales(self, frames, keep_maps=False):
+        """frames: torch uint8 cuda [n,H,W,3]. Returns (geoms, pafs, heats); maps are None
+        (read from the arena by the post kernels) for a single scale unless keep_maps."""
+        import torch
+        n, H, W, _ = frames.shape
+        geoms, pafs, heats = [], [], []
+        multi = len(self.scale_search) > 1 or keep_maps
+        for (m, nh, nw, vh, vw) in scale_geometry(H, W, self.scale_search):
+            gh, gw = self.net.preprocess(frames, m)
+            assert (gh, gw) == (nh, nw)
+            if multi:
+                paf = torch.empty((n, self.npaf, nh // 8, nw // 8), device=frames.device)
+                heat = torch.empty((n, self.njoint, nh // 8, nw // 8), device=frames.device)
+                self.net.run(paf, heat)
+            else:
+                paf = heat = None
+                self.net.run()
+            geoms.append((nh, nw, vh, vw))
+            pafs.append(paf)
+            heats.append(heat)
+        return geoms, pafs, heats
+
+    # -- post-processing ---------------------------------------------------------
+    def post(self, n, H, W, geoms, pafs, heats, caps=None):
+        """Run isl_body_post and return the raw result records (numpy uint8) + layout."""
+        import torch
+        caps = dict(self.caps, **(caps or {}))
+        while True:
+            c = rt.IslCaps(**caps)
+            lay = rt.body_layout(self.kind, c)
+            res = torch.empty(n * lay.record_bytes, dtype=torch.uint8, device="cuda:%d" % self.device)
+            ns = len(geoms)
+            g = (rt.IslScaleGeom * ns)(*[rt.IslScaleGeom(*gg) for gg in geoms])
+            pp = (ctypes.c_void_p * ns)(*[rt.ptr(p).value for p in pafs])
+            hp = (ctypes.c_void_p * ns)(*[rt.ptr(h).value for h in heats])
+            rt.check(rt.lib().isl_body_post(self.net.h, n, H, W, ns, g, pp, hp, ctypes.byref(c), rt.ptr(res),
+                                           rt.stream_handle()), "isl_body_post")
+            host = res.cpu().numpy()
+            grow = self._grow(host, lay, n, caps)
+            if grow is None:
+                return host, lay, caps
+            caps = grow          # capacity overflow: re-run the post kernels with larger buffers (GPU)
+
+    def _grow(self, host, lay, n, caps):
+        need = None
+        for f in range(n):
+            rec = host[f * lay.record_bytes:(f + 1) * lay.record_bytes]
+            st = int(rec[lay.status:lay.status + 4].view(np.int32)[0])
+            if st == rt.ISL_E_INDEX:
+                raise IndexError("list assignment index out of range")
+            if st == rt.ISL_E_CAPACITY:
+                npk = rec[lay.n_peaks:lay.n_peaks + 128].view(np.int32)[:self.njoint - 1]
+                mp = int(npk.max())
+                need = need or dict(caps)
+                need["max_peaks"] = max(need["max_peaks"], 2 * mp, 2 * caps["max_peaks"] if mp <= caps["max_peaks"] else 0)
+                need["max_conns"] = max(need["max_conns"], need["max_peaks"])
+                need["max_pairs"] = max(need["max_pairs"], mp * mp)
+                need["max_rows"] = max(need["max_rows"], 2 * caps["max_rows"], need["max_conns"] * 4)
+            elif st != rt.ISL_OK:
+                raise rt.IslError("body post: frame %d status %d" % (f, st))
+        return need
+
+    def decode(self, host, lay, caps, n):
+        out = []
+        nparts, nl = self.njoint - 1, NLIMBS[self.kind]
+        mpk, mcn, rw = caps["max_peaks"], caps["max_conns"], self.njoint + 1
+        for f in range(n):
+            rec = host[f * lay.record_bytes:(f + 1) * lay.record_bytes]
+            npk = rec[lay.n_peaks:lay.n_peaks + 128].view(np.int32)[:nparts]
+            ncn = rec[lay.n_conns:lay.n_conns + 128].view(np.int32)[:nl]
+            nrows = int(rec[lay.n_rows:lay.n_rows + 4].view(np.int32)[0])
+            pk = rec[lay.peaks:lay.peaks + nparts * mpk * 24].view(np.float64).reshape(nparts, mpk, 3)
+            cn = rec[lay.conns:lay.conns + nl * mcn * 40].view(np.float64).reshape(nl, mcn, 5)
+            sb = rec[lay.subset:lay.subset + caps["max_rows"] * rw * 8].view(np.float64).reshape(-1, rw)
+            all_peaks, rows, pid = [], [], 0
+            for p in range(nparts):
+                lst = []
+                for i in range(int(npk[p])):
+                    x, y, s = pk[p, i]
+                    lst.append((np.int64(x), np.int64(y), np.float64(s), pid))
+                    rows.append((x, y, s, float(pid)))
+                    pid += 1
+                all_peaks.append(lst)
+            candidate = np.array(rows, np.float64) if rows else np.array([])
+            conn_all, special = [], []
+            for k in range(nl):
+                if ncn[k] < 0:
+                    special.append(k)
+                    conn_all.append([])
+                else:
+                    conn_all.append(cn[k, :ncn[k]].copy())
+            subset = sb[:nrows].copy()
+            out.append(FrameResult(candidate, subset, all_peaks, conn_all, special))
+        return out
+
+    def estimate(self, frames, details=False):
+        """frames: uint8 [n,H,W,3] (numpy or torch) or one [H,W,3] frame -> list of (candidate, subset)."""
+        import torch
+        single = frames.ndim == 3
+        t = torch.as_tensor(frames)
+        if single:
+            t = t[None]
+        t = t.to("cuda:%d" % self.device).contiguous()
+        n, H, W, _ = t.shape
+        geoms, pafs, heats = self.run_scales(t)
+        host, lay, caps = self.post(n, H, W, geoms, pafs, heats)
+        res = self.decode(host, lay, caps, n)
+        if details:
+            return res
+        out = [(r.candidate, r.subset) for r in res]
+        return out[0] if single else out
+
+    def post_maps(self, H, W, geoms, pafs, heats, details=True):
+        """Post-processing only, on caller low-res maps (NCHW cuda tensors per scale)."""
+        n = pafs[0].shape[0]
+        host, lay, caps = self.post(n, H, W, geoms, pafs, heats)
+        res = self.decode(host, lay, caps, n)
+        return res if details else [(r.candidate, r.subset) for r in res]

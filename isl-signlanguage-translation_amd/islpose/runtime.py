@@ -1,0 +1,180 @@
+"""ctypes binding of libislpose.so (include/islpose.h).
+
+The HIP library is the only compute path: if it is missing or a call fails,
+this module raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+ISL_OK, ISL_E_ARG, ISL_E_PARAM, ISL_E_HIP, ISL_E_CAPACITY, ISL_E_STATE, ISL_E_INDEX = 0, -1, -2, -3, -4, -5, -6
+ISL_BODY25, ISL_COCO, ISL_HAND = 0, 1, 2
+
+LIB_PATH = os.environ.get("ISLPOSE_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libislpose.so"))
+
+# every symbol include/islpose.h declares
+EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destroy", "isl_net_param_count",
+           "isl_net_param_info", "isl_net_set_param", "isl_net_forward", "isl_net_preprocess", "isl_net_run", "isl_net_debug_input",
+           "isl_body_layout", "isl_body_post", "isl_hand_post"]
+
+
+class IslCaps(ctypes.Structure):
+    _fields_ = [("max_peaks", ctypes.c_int32), ("max_pairs", ctypes.c_int32),
+                ("max_conns", ctypes.c_int32), ("max_rows", ctypes.c_int32)]
+
+
+class IslLayout(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in
+                ("status", "n_peaks", "n_conns", "n_rows", "peaks", "conns", "subset", "record_bytes")]
+
+
+class IslScaleGeom(ctypes.Structure):
+    _fields_ = [("net_h", ctypes.c_int32), ("net_w", ctypes.c_int32),
+                ("valid_h", ctypes.c_int32), ("valid_w", ctypes.c_int32)]
+
+
+class IslError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libislpose.so once; raise loudly if it is absent (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libislpose.so not found at %s -- build it with `make` (or __graft_entry__.build())"
+                          % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+    L.isl_abi_version.restype = i32
+    L.isl_last_error.restype = ctypes.c_char_p
+    L.isl_net_create.argtypes = [i32, i32, ctypes.POINTER(vp)]
+    L.isl_net_destroy.argtypes = [vp]
+    L.isl_net_param_count.argtypes = [vp]
+    L.isl_net_param_info.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(i64)]
+    L.isl_net_set_param.argtypes = [vp, ctypes.c_char_p, vp, i64]
+    L.isl_net_forward.argtypes = [vp, vp, i32, i32, i32, vp, vp, vp]
+    L.isl_net_preprocess.argtypes = [vp, vp, i32, i32, i32, dbl, ctypes.POINTER(i32), ctypes.POINTER(i32), vp]
+    L.isl_net_run.argtypes = [vp, vp, vp, vp]
+    L.isl_net_debug_input.argtypes = [vp, vp, vp]
+    L.isl_body_layout.argtypes = [i32, ctypes.POINTER(IslCaps), ctypes.POINTER(IslLayout)]
+    L.isl_body_post.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp),
+                                ctypes.POINTER(vp), ctypes.POINTER(IslCaps), vp, vp]
+    L.isl_hand_post.argtypes = [vp, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp), vp, vp]
+    for name in EXPORTS[2:]:
+        getattr(L, name).restype = i32
+    if L.isl_abi_version() != 1:
+        raise ImportError("libislpose ABI mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = ""):
+    if rc == ISL_OK:
+        return
+    msg = lib().isl_last_error().decode(errors="replace")
+    if rc == ISL_E_PARAM:
+        raise KeyError(msg)
+    if rc == ISL_E_INDEX:
+        raise IndexError("list assignment index out of range")
+    raise IslError("%s failed (%d): %s" % (what or "libislpose", rc, msg))
+
+
+def body_layout(kind: int, caps: IslCaps) -> IslLayout:
+    lay = IslLayout()
+    check(lib().isl_body_layout(kind, ctypes.byref(caps), ctypes.byref(lay)), "isl_body_layout")
+    return lay
+
+
+def stream_handle(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+class Net:
+    """One network (body25 / coco / hand) on one device, owned by libislpose."""
+
+    def __init__(self, kind: int, device: int = 0):
+        self.kind = kind
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().isl_net_create(kind, device, ctypes.byref(h)), "isl_net_create")
+        self.h = h
+        self.loaded = False
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and _lib is not None:
+            _lib.isl_net_destroy(h)
+            self.h = None
+
+    def param_names(self):
+        out = []
+        n = lib().isl_net_param_count(self.h)
+        for i in range(n):
+            name = ctypes.c_char_p()
+            numel = ctypes.c_int64()
+            check(lib().isl_net_param_info(self.h, i, ctypes.byref(name), ctypes.byref(numel)))
+            out.append((name.value.decode(), numel.value))
+        return out
+
+    def load_weights(self, weights: dict):
+        """weights: flat {caffe_name: array/tensor} (the dict util.transfer reads).
+        A missing name raises KeyError like util.transfer (src/util.py:39-43)."""
+        for name, numel in self.param_names():
+            v = weights[name]
+            if hasattr(v, "detach"):
+                v = v.detach().cpu().numpy()
+            a = np.ascontiguousarray(np.asarray(v, dtype=np.float32))
+            if a.size != numel:
+                raise KeyError("%s: expected %d elements, got %d" % (name, numel, a.size))
+            check(lib().isl_net_set_param(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), a.size),
+                  "isl_net_set_param")
+        self.loaded = True
+
+    def forward(self, x, out0=None, out1=None, stream=None):
+        """Module seam: x float32 NCHW cuda tensor -> (paf, heat) or heat."""
+        import torch
+        assert x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] == 3
+        x = x.contiguous()
+        n, _, h, w = x.shape
+        h8, w8 = h // 8, w // 8
+        if self.kind == ISL_HAND:
+            o0 = out0 if out0 is not None else torch.empty((n, 22, h8, w8), device=x.device)
+            o1 = None
+        else:
+            npaf, nj = (52, 26) if self.kind == ISL_BODY25 else (38, 19)
+            o0 = out0 if out0 is not None else torch.empty((n, npaf, h8, w8), device=x.device)
+            o1 = out1 if out1 is not None else torch.empty((n, nj, h8, w8), device=x.device)
+        check(lib().isl_net_forward(self.h, ptr(x), n, h, w, ptr(o0), ptr(o1), stream_handle(stream)),
+              "isl_net_forward")
+        return o0 if o1 is None else (o0, o1)
+
+    def preprocess(self, frames_u8, scale: float, stream=None):
+        """frames uint8 [n,H,W,3] cuda -> fills the net input; returns (net_h, net_w)."""
+        n, H, W, _ = frames_u8.shape
+        nh, nw = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().isl_net_preprocess(self.h, ptr(frames_u8), n, H, W, float(scale), ctypes.byref(nh),
+                                       ctypes.byref(nw), stream_handle(stream)), "isl_net_preprocess")
+        return nh.value, nw.value
+
+    def debug_input(self, n, h, w, stream=None):
+        import torch
+        x = torch.empty((n, 3, h, w), device="cuda:%d" % self.device)
+        check(lib().isl_net_debug_input(self.h, ptr(x), stream_handle(stream)), "isl_net_debug_input")
+        return x
+
+    def run(self, out0=None, out1=None, stream=None):
+        check(lib().isl_net_run(self.h, ptr(out0), ptr(out1), stream_handle(stream)), "isl_net_run")

@@ -1,0 +1,162 @@
+"""Parity of the HIP path (libislpose.so) against the CPU oracle and the golden
+vectors.  Runs on an MI355X only (-m gpu)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref
+from islpose import synth
+from islpose import runtime as rt
+from islpose.body import BodyEstimator, scale_geometry
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-4   # north_star: heatmap/PAF tensors within 1e-4 relative (max|d| / max|ref|) in fp32
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def w25():
+    return synth.synth_weights(0)
+
+
+@pytest.fixture(scope="module")
+def net25(w25):
+    n = rt.Net(rt.ISL_BODY25)
+    n.load_weights(w25)
+    return n
+
+
+def _inputs(n, h, w, seed):
+    f = synth.synth_frames(n, h, w, seed=seed)
+    return np.ascontiguousarray(np.transpose(f.astype(np.float32), (0, 3, 1, 2)) / 256 - 0.5)
+
+
+@pytest.mark.parametrize("n,h,w", [(1, 50, 70), (2, 184, 328), (1, 368, 656)])
+def test_body25_forward_vs_oracle(net25, w25, n, h, w):
+    x = _inputs(n, h, w, seed=h + w)
+    paf, heat = net25.forward(torch.from_numpy(x).cuda())
+    torch.cuda.synchronize()
+    rp, rh = cpu_ref.make_net_fn("body25", w25)(x)
+    assert paf.shape == rp.shape and heat.shape == rh.shape
+    assert _rel(paf.cpu().numpy(), rp) < TOL
+    assert _rel(heat.cpu().numpy(), rh) < TOL
+
+
+def test_body25_forward_golden(net25):
+    g1 = np.load(os.path.join(GOLDEN, "g1_networks.npz"))
+    x = _inputs(1, 184, 328, int(g1["body25_184x328_seed"]))
+    paf, heat = net25.forward(torch.from_numpy(x).cuda())
+    assert _rel(paf.cpu().numpy(), g1["body25_184x328_paf"]) < TOL
+    assert _rel(heat.cpu().numpy(), g1["body25_184x328_heat"]) < TOL
+
+
+def test_coco_forward_golden():
+    g1 = np.load(os.path.join(GOLDEN, "g1_networks.npz"))
+    net = rt.Net(rt.ISL_COCO)
+    net.load_weights(synth.synth_weights(1))
+    ski = np.load(os.path.join(GOLDEN, "ski_bgr.npz"))["img"]
+    im, _, _ = cpu_ref.net_input(ski, 0.5 * 368 / ski.shape[0])
+    paf, heat = net.forward(torch.from_numpy(im).cuda())
+    assert _rel(paf.cpu().numpy(), g1["coco_ski_paf"]) < TOL
+    assert _rel(heat.cpu().numpy(), g1["coco_ski_heat"]) < TOL
+
+
+def test_hand_forward_golden():
+    g1 = np.load(os.path.join(GOLDEN, "g1_networks.npz"))
+    net = rt.Net(rt.ISL_HAND)
+    net.load_weights(synth.synth_weights(2))
+    for s in (184, 368):
+        x = _inputs(1, s, s, int(g1["hand_%d_seed" % s]))
+        out = net.forward(torch.from_numpy(x).cuda())
+        assert _rel(out.cpu().numpy(), g1["hand_%d" % s]) < TOL
+
+
+@pytest.mark.parametrize("H,W,scale", [(368, 656, 0.5), (368, 656, 1.0), (300, 500, 368 / 300 * 0.5),
+                                       (97, 131, 1.7), (674, 712, 0.5 * 368 / 674)])
+def test_preprocess_bit_exact(net25, H, W, scale):
+    frames = synth.synth_frames(2, H, W, seed=7)
+    nh, nw = net25.preprocess(torch.from_numpy(frames).cuda(), scale)
+    got = net25.debug_input(2, nh, nw).cpu().numpy()
+    for i in range(2):
+        ref, _, _ = cpu_ref.net_input(frames[i], scale)
+        assert ref.shape[2:] == (nh, nw)
+        assert np.array_equal(got[i:i + 1], ref)
+
+
+def _golden_cases():
+    z = np.load(os.path.join(GOLDEN, "g2_body_post.npz"))
+    return z, sorted({k.split("/")[0] for k in z.files})
+
+
+@pytest.fixture(scope="module")
+def est25(w25):
+    return BodyEstimator(w25, "body25")
+
+
+@pytest.fixture(scope="module")
+def estcoco():
+    return BodyEstimator(synth.synth_weights(1), "coco")
+
+
+def test_body_post_golden_bit_exact(est25, estcoco):
+    """Designed low-res maps replayed through the GPU post kernels == reference Body.__call__."""
+    z, names = _golden_cases()
+    for name in names:
+        mt = str(z[name + "/model_type"])
+        est = est25 if mt == "body25" else estcoco
+        H, W = (int(v) for v in z[name + "/frame_hw"])
+        scales = tuple(float(s) for s in z[name + "/scales"])
+        geoms = [g[1:] for g in scale_geometry(H, W, scales)]
+        pafs = [torch.from_numpy(z[name + "/paf%d" % i][None]).cuda() for i in range(len(scales))]
+        heats = [torch.from_numpy(z[name + "/heat%d" % i][None]).cuda() for i in range(len(scales))]
+        r = est.post_maps(H, W, geoms, pafs, heats)[0]
+        assert r.candidate.shape == z[name + "/candidate"].shape, name
+        assert np.array_equal(r.candidate, z[name + "/candidate"]), name
+        assert np.array_equal(r.subset, z[name + "/subset"]), name
+
+
+def test_body_estimate_end_to_end(est25, w25):
+    """Frames -> GPU pre-proc + net + post; the GPU's own low-res maps replayed through
+    the oracle post must give identical candidate / subset / connections."""
+    frames = synth.synth_frames(2, 368, 656, seed=3)
+    t = torch.from_numpy(frames).cuda()
+    geoms, pafs, heats = est25.run_scales(t, keep_maps=True)
+    res = est25.post_maps(368, 656, geoms, pafs, heats)
+    for i in range(2):
+        pl, hl = pafs[0][i].cpu().numpy(), heats[0][i].cpu().numpy()
+        heat_avg, paf_avg = cpu_ref.body_maps(frames[i], lambda im: (pl[None], hl[None]), "body25", (0.5,))
+        cand, subset, all_peaks, conn = cpu_ref.body_post(heat_avg, paf_avg, "body25", 368)
+        assert np.array_equal(res[i].candidate, cand)
+        assert np.array_equal(res[i].subset, subset)
+        for a, b in zip(res[i].connection_all, conn):
+            assert np.array_equal(np.asarray(a).reshape(-1, 5), np.asarray(b).reshape(-1, 5))
+    # and the net outputs themselves are within tolerance of the oracle network
+    for i in range(2):
+        im, _, _ = cpu_ref.net_input(frames[i], 0.5)
+        rp, rh = cpu_ref.make_net_fn("body25", w25)(im)
+        assert _rel(pafs[0][i:i + 1].cpu().numpy(), rp) < TOL
+        assert _rel(heats[0][i:i + 1].cpu().numpy(), rh) < TOL
+
+
+def test_designed_maps_batch_bit_exact(est25):
+    """A batch of designed maps (P = 0..6 persons) through the GPU post == oracle post."""
+    H, W = 368, 656
+    geoms = [g[1:] for g in scale_geometry(H, W, (1.0,))]
+    maps = [synth.designed_pose_maps(46, 82, p, 100 + p) for p in range(7)]
+    paf = torch.from_numpy(np.stack([m[0] for m in maps])).cuda()
+    heat = torch.from_numpy(np.stack([m[1] for m in maps])).cuda()
+    res = est25.post_maps(H, W, geoms, [paf], [heat])
+    for i, (pl, hl) in enumerate(maps):
+        heat_avg, paf_avg = cpu_ref.body_maps(np.zeros((H, W, 3), np.uint8), lambda im: (pl[None], hl[None]),
+                                              "body25", (1.0,))
+        cand, subset, _, _ = cpu_ref.body_post(heat_avg, paf_avg, "body25", H)
+        assert np.array_equal(res[i].candidate, cand), i
+        assert np.array_equal(res[i].subset, subset), i
+        assert len(subset) == i, i

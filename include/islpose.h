@@ -129,9 +129,11 @@ int isl_body_post(isl_net* net, int n, int H, int W, int nscales, const isl_scal
                   const float* const* d_paf, const float* const* d_heat,
                   const isl_caps* caps, void* d_result, void* stream);
 
-/* Hand post-processing (hand.py:35-74) for n crops of size w x w: 4 scales of
- * low-res hand maps (NCHW [n,22,g.net_h/8,g.net_w/8]) -> int64 peaks [n][21][2]. */
-int isl_hand_post(isl_net* net, int n, int w, int nscales, const isl_scale_geom* geom,
+/* Hand post-processing (hand.py:51-74) for n crops of size h x w: per scale,
+ * low-res hand maps (NCHW [n,22,net_h/8,net_w/8], NULL = the net's arena output
+ * for nscales == 1) -> int64 peaks [n][21][2] as (x, y), [0, 0] when no pixel of
+ * the blurred part map exceeds 0.05. */
+int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, const isl_scale_geom* geom,
                   const float* const* d_heat, int64_t* d_peaks, void* stream);
 
 #ifdef __cplusplus

@@ -466,6 +466,212 @@ __global__ void __launch_bounds__(256) group_kernel(GroupArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Hand peaks (hand.py:58-73): 8-connected components of the thresholded blur,
+// the component with the largest np.sum(map_ori[label == i]) (first on ties,
+// labels numbered in raster order of their first pixel), then util.npmax of
+// map_ori with every other pixel zeroed.  One workgroup per (crop, part).
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ int ld_parent(const int* p, int x) {
+  return __hip_atomic_load(p + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ int uf_find(int* parent, int x) {
+  int p = ld_parent(parent, x);
+  while (p != x) {
+    x = p;
+    p = ld_parent(parent, x);
+  }
+  return x;
+}
+
+// lock-free union: hook the larger root under the smaller with a CAS, so the
+// final root of every component is its smallest raster index (= label order).
+__device__ void uf_union(int* parent, int a, int b) {
+  while (true) {
+    a = uf_find(parent, a);
+    b = uf_find(parent, b);
+    if (a == b) return;
+    if (a < b) { const int t = a; a = b; b = t; }
+    if (atomicCAS(parent + a, a, b) == a) return;
+  }
+}
+
+// numpy pairwise_sum (loops_utils.h.src): < 8 sequential from 0; <= 128: 8
+// accumulators; else split at n/2 rounded down to a multiple of 8.
+__device__ double np_pairwise(const double* a, int n) {
+  // iterative post-order walk of the split tree (depth <= 32)
+  struct Frame { int off, len, state; double left; };
+  Frame st[32];
+  int sp = 0;
+  st[0] = {0, n, 0, 0.0};
+  double ret = 0.0;
+  while (sp >= 0) {
+    Frame& f = st[sp];
+    if (f.len <= 128) {
+      double res;
+      const double* x = a + f.off;
+      if (f.len < 8) {
+        res = 0.0;
+        for (int i = 0; i < f.len; ++i) res += x[i];
+      } else {
+        double r[8];
+        for (int k = 0; k < 8; ++k) r[k] = x[k];
+        int i = 8;
+        for (; i < f.len - (f.len % 8); i += 8)
+          for (int k = 0; k < 8; ++k) r[k] += x[i + k];
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < f.len; ++i) res += x[i];
+      }
+      ret = res;
+      --sp;
+      continue;
+    }
+    int n2 = f.len / 2;
+    n2 -= n2 % 8;
+    if (f.state == 0) {
+      f.state = 1;
+      st[++sp] = {f.off, n2, 0, 0.0};
+    } else if (f.state == 1) {
+      f.left = ret;
+      f.state = 2;
+      st[++sp] = {f.off + n2, f.len - n2, 0, 0.0};
+    } else {
+      ret = f.left + ret;
+      --sp;
+    }
+  }
+  return ret;
+}
+
+// np.sum of a contiguous float64 array: pairwise sums of 8192-element buffers, added left to right
+__device__ double np_sum(const double* a, int n) {
+  double s = 0.0;
+  for (int i = 0; i < n; i += 8192) {
+    const double p = np_pairwise(a + i, min(8192, n - i));
+    s = i == 0 ? p : s + p;
+  }
+  return s;
+}
+
+__global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__ planes,
+                                                      const unsigned long long* __restrict__ mask, int h, int w,
+                                                      int words, int* __restrict__ parent_all,
+                                                      double* __restrict__ vals_all, long long* __restrict__ out) {
+  const int plane = blockIdx.x;   // crop * 21 + part
+  const int P = h * w, tid = threadIdx.x;
+  const double* map = planes + (size_t)plane * P;
+  const unsigned long long* mk = mask + (size_t)plane * h * words;
+  int* parent = parent_all + (size_t)plane * P;
+  double* vals = vals_all + (size_t)plane * P;
+  auto bit = [&](int y, int x) -> bool { return (mk[(size_t)y * words + (x >> 6)] >> (x & 63)) & 1ull; };
+  __shared__ int s_cnt;
+  __shared__ int s_scan[256];
+  __shared__ double s_best_sum;
+  __shared__ int s_best_root;
+  __shared__ double s_red_v[256];
+  __shared__ int s_red_i[256];
+  if (tid == 0) s_cnt = 0;
+  __syncthreads();
+  int local = 0;
+  for (int p = tid; p < P; p += 256) {
+    const bool b = bit(p / w, p % w);
+    parent[p] = b ? p : -1;
+    local += b;
+  }
+  atomicAdd(&s_cnt, local);
+  __syncthreads();
+  if (s_cnt == 0) {                     // np.sum(binary) == 0 -> [0, 0]
+    if (tid == 0) { out[plane * 2] = 0; out[plane * 2 + 1] = 0; }
+    return;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // union over the 4 raster-earlier neighbours (8-connectivity)
+  for (int p = tid; p < P; p += 256) {
+    if (parent[p] < 0) continue;
+    const int y = p / w, x = p - y * w;
+    if (x > 0 && bit(y, x - 1)) uf_union(parent, p, p - 1);
+    if (y > 0) {
+      if (x > 0 && bit(y - 1, x - 1)) uf_union(parent, p, p - w - 1);
+      if (bit(y - 1, x)) uf_union(parent, p, p - w);
+      if (x + 1 < w && bit(y - 1, x + 1)) uf_union(parent, p, p - w + 1);
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  for (int p = tid; p < P; p += 256)
+    if (ld_parent(parent, p) >= 0) parent[p] = uf_find(parent, p);
+  __threadfence();
+  __syncthreads();
+  // components in label order = roots in raster order; keep the first maximal sum
+  if (tid == 0) { s_best_root = -1; s_best_sum = 0.0; }
+  __syncthreads();
+  for (int r0 = 0; r0 < P; ++r0) {
+    // next root (parent[r] == r) at or after r0, found cooperatively
+    int cand = 0x7fffffff;
+    for (int p = r0 + tid; p < P; p += 256)
+      if (parent[p] == p) { cand = p; break; }
+    s_scan[tid] = cand;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (tid < off) s_scan[tid] = min(s_scan[tid], s_scan[tid + off]);
+      __syncthreads();
+    }
+    const int root = s_scan[0];
+    __syncthreads();
+    if (root == 0x7fffffff) break;
+    // compact this component's values in raster order
+    int base = 0;
+    for (int c0 = root; c0 < P; c0 += 256) {
+      const int p = c0 + tid;
+      const int f = (p < P && parent[p] == root) ? 1 : 0;
+      s_scan[tid] = f;
+      __syncthreads();
+      for (int off = 1; off < 256; off <<= 1) {
+        const int v = tid >= off ? s_scan[tid - off] : 0;
+        __syncthreads();
+        s_scan[tid] += v;
+        __syncthreads();
+      }
+      if (f) vals[base + s_scan[tid] - 1] = map[p];
+      base += s_scan[255];
+      __syncthreads();
+    }
+    if (tid == 0) {
+      const double s = np_sum(vals, base);
+      if (s_best_root < 0 || s > s_best_sum) { s_best_sum = s; s_best_root = root; }   // np.argmax: first max
+    }
+    __syncthreads();
+    r0 = root;   // loop increments past this root
+  }
+  // util.npmax on map_ori with the other labels zeroed: first raster-order maximum
+  const int best = s_best_root;
+  double bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int p = tid; p < P; p += 256) {
+    const double v = parent[p] == best ? map[p] : 0.0;
+    if (v > bv || (v == bv && p < bi)) { bv = v; bi = p; }
+  }
+  s_red_v[tid] = bv;
+  s_red_i[tid] = bi;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) {
+      const double v2 = s_red_v[tid + off];
+      const int i2 = s_red_i[tid + off];
+      if (v2 > s_red_v[tid] || (v2 == s_red_v[tid] && i2 < s_red_i[tid])) { s_red_v[tid] = v2; s_red_i[tid] = i2; }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int p = s_red_i[0];
+    out[plane * 2] = p % w;       // [x, y]
+    out[plane * 2 + 1] = p / w;
+  }
+}
+
 __global__ void init_records_kernel(char* result, isl_layout lay, int n, int nlimbs) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n) return;
@@ -654,8 +860,61 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   return ISL_OK;
 }
 
-extern "C" int isl_hand_post(isl_net* net, int n, int w, int nscales, const isl_scale_geom* geom,
+extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, const isl_scale_geom* geom,
                              const float* const* d_heat, int64_t* d_peaks, void* stream) {
-  (void)net; (void)n; (void)w; (void)nscales; (void)geom; (void)d_heat; (void)d_peaks; (void)stream;
-  return post_fail(ISL_E_STATE, "isl_hand_post: not built yet");
+  if (!net || n <= 0 || h <= 0 || w <= 0 || nscales <= 0 || nscales > MAX_SCALES || !geom || !d_peaks)
+    return post_fail(ISL_E_ARG, "isl_hand_post: bad argument");
+  if (net_kind(net) != ISL_HAND) return post_fail(ISL_E_ARG, "isl_hand_post needs the hand net");
+  if (nscales > 1 && !d_heat) return post_fail(ISL_E_ARG, "isl_hand_post: maps required for several scales");
+  PHIP(hipSetDevice(net_device(net)));
+  hipStream_t s = (hipStream_t)stream;
+  const int nparts = 21, nch = 22;
+  const size_t P = (size_t)h * w;
+  const int words = (w + 63) / 64;
+  size_t mid_bytes = 0;
+  for (int si = 0; si < nscales; ++si)
+    if (!(geom[si].valid_h == h && geom[si].valid_w == w))
+      mid_bytes = std::max(mid_bytes, (size_t)n * geom[si].valid_h * geom[si].valid_w * nparts * 4);
+  auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t avg_bytes = (size_t)n * nparts * P * 8, mask_bytes = (size_t)n * nparts * h * words * 8;
+  const size_t par_bytes = (size_t)n * nparts * P * 4, val_bytes = (size_t)n * nparts * P * 8;
+  char* base = (char*)net_scratch(net, up(avg_bytes) + up(mid_bytes) + up(mask_bytes) + up(par_bytes) + up(val_bytes));
+  if (!base) return ISL_E_HIP;
+  double* avg = (double*)base;
+  float* mid = (float*)(base + up(avg_bytes));
+  unsigned long long* mask = (unsigned long long*)((char*)mid + up(mid_bytes));
+  int* parent = (int*)((char*)mask + up(mask_bytes));
+  double* vals = (double*)((char*)parent + up(par_bytes));
+  PHIP(hipMemsetAsync(avg, 0, avg_bytes, s));
+  const float div_f = (float)nscales;
+  for (int si = 0; si < nscales; ++si) {
+    const isl_scale_geom& g = geom[si];
+    const int h8 = g.net_h / 8, w8 = g.net_w / 8;
+    MapSrc lh;
+    int rc = low_src(net, d_heat ? d_heat[si] : nullptr, 0, n, nch, h8, w8, &lh);
+    if (rc) return rc;
+    lh.dh = h8 * 8; lh.dw = w8 * 8; lh.scy = lh.scx = 1.0 / 8.0; lh.cn = nch; lh.identity = 0;
+    MapSrc fh = lh;
+    if (!(g.valid_h == h && g.valid_w == w)) {
+      const long long tm = (long long)n * g.valid_h * g.valid_w * nparts;
+      hipLaunchKernelGGL(resize_kernel, dim3(grid_for(tm)), dim3(256), 0, s, lh, n, nparts, g.valid_h, g.valid_w, 0,
+                         1.f, (void*)mid);
+      PHIP(hipGetLastError());
+      fh.base = mid; fh.xs = nparts; fh.ys = (long long)g.valid_w * nparts; fh.cstr = 1;
+      fh.fs = (long long)g.valid_h * g.valid_w * nparts;
+      fh.sh = g.valid_h; fh.sw = g.valid_w; fh.dh = h; fh.dw = w;
+      fh.scy = 1.0 / ((double)h / g.valid_h); fh.scx = 1.0 / ((double)w / g.valid_w);
+      fh.cn = nch; fh.identity = 0;
+    }
+    const long long tf = (long long)n * nparts * P;
+    hipLaunchKernelGGL(resize_kernel, dim3(grid_for(tf)), dim3(256), 0, s, fh, n, nparts, h, w, 3, div_f, (void*)avg);
+    PHIP(hipGetLastError());
+  }
+  dim3 gb(words, (h + NMS_TY - 1) / NMS_TY, n * nparts);
+  hipLaunchKernelGGL(blur_nms_kernel<double>, gb, dim3(256), 0, s, (const double*)avg, h, w, words, mask, 0.05, 1);
+  PHIP(hipGetLastError());
+  hipLaunchKernelGGL(hand_cc_kernel, dim3(n * nparts), dim3(256), 0, s, (const double*)avg, mask, h, w, words, parent,
+                     vals, (long long*)d_peaks);
+  PHIP(hipGetLastError());
+  return ISL_OK;
 }

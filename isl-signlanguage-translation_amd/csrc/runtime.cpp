@@ -190,6 +190,7 @@ struct isl_net {
   // plan
   int pn = 0, ph = 0, pw = 0;
   std::vector<Act> act;
+  std::map<long long, std::pair<void*, std::vector<Act>>> plans;
   void* arena = nullptr;
   size_t arena_bytes = 0;
   // post scratch
@@ -400,11 +401,21 @@ static int upload_params(isl_net* net) {
   return ISL_OK;
 }
 
+// Activation arena per (n, h, w): cached, so the scales of a pyramid (or the 4
+// hand scales) each keep their own arena instead of reallocating per call.
 static int plan(isl_net* net, int n, int h, int w) {
   if (net->pn == n && net->ph == h && net->pw == w && net->arena) return ISL_OK;
   if (n <= 0 || h < 8 || w < 8) return fail(ISL_E_ARG, "net input must be at least 8x8 with n >= 1");
+  const long long key = ((long long)n << 40) | ((long long)h << 20) | w;
+  auto it = net->plans.find(key);
+  if (it != net->plans.end()) {
+    net->arena = it->second.first;
+    net->act = it->second.second;
+    net->pn = n; net->ph = h; net->pw = w;
+    return ISL_OK;
+  }
   int lh[4] = {h, h / 2, h / 4, h / 8}, lw[4] = {w, w / 2, w / 4, w / 8};
-  if (net->arena) { (void)hipFree(net->arena); net->arena = nullptr; }
+  net->arena = nullptr;
   net->act.assign(net->bufs.size(), Act{});
   size_t total = 0;
   std::vector<size_t> offs;
@@ -420,6 +431,7 @@ static int plan(isl_net* net, int n, int h, int w) {
   for (size_t i = 0; i < net->bufs.size(); ++i) net->act[i].base = (float*)((char*)net->arena + offs[i]);
   net->arena_bytes = total;
   net->pn = n; net->ph = h; net->pw = w;
+  net->plans[key] = {net->arena, net->act};
   return ISL_OK;
 }
 
@@ -514,7 +526,7 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_b) (void)hipFree(c.d_b);
     if (c.d_s) (void)hipFree(c.d_s);
   }
-  if (net->arena) (void)hipFree(net->arena);
+  for (auto& kv : net->plans) (void)hipFree(kv.second.first);
   if (net->scratch) (void)hipFree(net->scratch);
   delete net;
   return ISL_OK;

@@ -67,7 +67,7 @@ def lib():
     L.isl_body_layout.argtypes = [i32, ctypes.POINTER(IslCaps), ctypes.POINTER(IslLayout)]
     L.isl_body_post.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp),
                                 ctypes.POINTER(vp), ctypes.POINTER(IslCaps), vp, vp]
-    L.isl_hand_post.argtypes = [vp, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp), vp, vp]
+    L.isl_hand_post.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp), vp, vp]
     for name in EXPORTS[2:]:
         getattr(L, name).restype = i32
     if L.isl_abi_version() != 1:

@@ -42,7 +42,9 @@ struct ConvArgs {
 };
 
 template <int KS, int WAVES_M, int WAVES_N, int WM, int WN>
-__global__ void __launch_bounds__(WAVES_M * WAVES_N * 64)
+// 4 waves per SIMD (4 blocks of 256 threads per CU, <= 128 VGPR+AGPR, <= 40 KB LDS
+// each): the 46x82 stage layers (960 tiles at batch 32) then fit in one round.
+__global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 4)
 conv_mfma_f32(ConvArgs a) {
   constexpr int NPL = 2;                        // planes of 4 channels per 8-channel chunk
   constexpr int NT = WAVES_M * WAVES_N * 64;

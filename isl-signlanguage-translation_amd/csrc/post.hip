@@ -69,6 +69,24 @@ __device__ __forceinline__ void taps(int d, double scale, int n, int idx[4], flo
   for (int k = 0; k < 4; ++k) idx[k] = min(max(s + k - 1, 0), n - 1);
 }
 
+// one output element of resize `m`, with the row taps (yi, be) precomputed
+__device__ __forceinline__ float sample_row(const MapSrc& m, int f, int c, const int yi[4], const float be[4], int x) {
+  const float* b = m.base + f * m.fs + c * m.cstr;
+  int xi[4];
+  float a[4];
+  taps(x, m.scx, m.sw, xi, a);
+  float hz[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float* r = b + yi[k] * m.ys;
+    hz[k] = ((r[xi[0] * m.xs] * a[0] + r[xi[1] * m.xs] * a[1]) + r[xi[2] * m.xs] * a[2]) + r[xi[3] * m.xs] * a[3];
+  }
+  const int rowlen = m.dw * m.cn;
+  if (x * m.cn + c < rowlen - rowlen % 4)
+    return hz[0] * be[0] + (hz[1] * be[1] + (hz[2] * be[2] + hz[3] * be[3]));
+  return ((hz[0] * be[0] + hz[1] * be[1]) + hz[2] * be[2]) + hz[3] * be[3];
+}
+
 __device__ __forceinline__ float sample(const MapSrc& m, int f, int c, int y, int x) {
   const float* b = m.base + f * m.fs + c * m.cstr;
   if (m.identity) return b[y * m.ys + x * m.xs];
@@ -92,19 +110,28 @@ __device__ __forceinline__ float sample(const MapSrc& m, int f, int c, int y, in
 // mode 0: dense NHWC f32 [n][oh][ow][nch]; 1: planar f32 [n][nch][oh][ow];
 // mode 2: planar f64 accumulate avg = avg + (avg + v/L)  (body.py:80, the doubling quirk)
 // mode 3: planar f64 accumulate avg += v/L                (hand.py:56)
-__global__ void resize_kernel(MapSrc m, int n, int nch, int oh, int ow, int mode, float inv_div_f, void* out) {
-  const long long total = (long long)n * nch * oh * ow;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    int c, x, y, f;
-    long long r = i;
-    if (mode == 0) {
-      c = (int)(r % nch); r /= nch; x = (int)(r % ow); r /= ow; y = (int)(r % oh); f = (int)(r / oh);
-    } else {
-      x = (int)(r % ow); r /= ow; y = (int)(r % oh); r /= oh; c = (int)(r % nch); f = (int)(r / nch);
+// One block per output row: planar modes row = (f*nch + c)*oh + y, NHWC mode row = f*oh + y.
+__global__ void __launch_bounds__(256) resize_kernel(MapSrc m, int n, int nch, int oh, int ow, int mode,
+                                                      float inv_div_f, void* out) {
+  const int row = blockIdx.x;
+  const int y = row % oh, rest = row / oh;
+  int yi[4];
+  float be[4];
+  if (!m.identity) taps(y, m.scy, m.sh, yi, be);
+  if (mode == 0) {
+    float* o = (float*)out + (size_t)row * ow * nch;
+    const int f = rest;
+    for (int i = threadIdx.x; i < ow * nch; i += blockDim.x) {
+      const int x = i / nch, c = i - x * nch;
+      o[i] = m.identity ? m.base[f * m.fs + c * m.cstr + y * m.ys + x * m.xs] : sample_row(m, f, c, yi, be, x);
     }
-    const float v = sample(m, f, c, y, x);
-    if (mode <= 1) {
+    return;
+  }
+  const int c = rest % nch, f = rest / nch;
+  for (int x = threadIdx.x; x < ow; x += blockDim.x) {
+    const float v = m.identity ? m.base[f * m.fs + c * m.cstr + y * m.ys + x * m.xs] : sample_row(m, f, c, yi, be, x);
+    const size_t i = (size_t)row * ow + x;
+    if (mode == 1) {
       ((float*)out)[i] = v;
     } else {
       double* o = (double*)out + i;
@@ -127,64 +154,85 @@ __device__ __forceinline__ int reflect_idx(int i, int n) {
   return i < n ? i : p - 1 - i;
 }
 
-constexpr int NMS_TY = 16, NMS_TX = 64, NMS_R = 12;
+// Tile: 16 output rows x 192 output columns (3 mask words).  The NMS needs g on
+// a one-pixel ring, the blur a 12-pixel apron:
+//   axis 0: one thread per column (218 = 192+2+24), the 42 input rows of that
+//           column held in registers -> 18 rows of v into LDS
+//   axis 1: one thread per 14-column run of one of the 18 rows, 38 v values in
+//           registers -> g into LDS
+//   NMS:    one wave per (row, 64-column word), ballot -> mask word.
+constexpr int NMS_TY = 16, NMS_TX = 192, NMS_R = 12;
+constexpr int NMS_VR = NMS_TY + 2;                 // g / v rows (1-px ring)
+constexpr int NMS_VC = NMS_TX + 2 + 2 * NMS_R;     // v columns (218)
+constexpr int NMS_GC = NMS_TX + 2;                 // g columns (194)
+constexpr int NMS_IR = NMS_VR + 2 * NMS_R;         // input rows (42)
+constexpr int NMS_SEG = 14;                        // g outputs per thread in the horizontal pass
 
 // planes: [n*nparts][H][W] (T = float or double); mask: [n*nparts][H][words]
 template <typename T>
 __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ planes, int H, int W, int words,
                                                         unsigned long long* __restrict__ mask, double thre,
                                                         int mode_hand) {
-  constexpr int IR = NMS_TY + 2 + 2 * NMS_R, IC = NMS_TX + 2 + 2 * NMS_R;  // 42 x 90
-  constexpr int VR = NMS_TY + 2, GC = NMS_TX + 2;                         // 18 rows, 66 cols
-  __shared__ double s_in[IR][IC];
-  __shared__ double s_v[VR][IC];
-  __shared__ double s_g[VR][GC];
+  __shared__ double s_v[NMS_VR][NMS_VC];
+  __shared__ double s_g[NMS_VR][NMS_GC];
   const int plane = blockIdx.z;
   const int y0 = blockIdx.y * NMS_TY, x0 = blockIdx.x * NMS_TX;
   const T* src = planes + (size_t)plane * H * W;
   const int tid = threadIdx.x;
-  for (int i = tid; i < IR * IC; i += 256) {
-    const int r = i / IC, c = i - r * IC;
-    const int yy = reflect_idx(y0 - 1 - NMS_R + r, H), xx = reflect_idx(x0 - 1 - NMS_R + c, W);
-    s_in[r][c] = (double)src[(size_t)yy * W + xx];
-  }
-  __syncthreads();
   // axis 0 (NI_Correlate1D, symmetric): o = c*w0; for j = 12..1: o += (a[-j] + a[+j]) * w[j]
-  for (int i = tid; i < VR * IC; i += 256) {
-    const int r = i / IC, c = i - r * IC;
-    double o = s_in[r + NMS_R][c] * kGauss[0];
+  if (tid < NMS_VC) {
+    const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
+    double in[NMS_IR];
 #pragma unroll
-    for (int j = NMS_R; j >= 1; --j) o = o + (s_in[r + NMS_R - j][c] + s_in[r + NMS_R + j][c]) * kGauss[j];
-    s_v[r][c] = o;
+    for (int r = 0; r < NMS_IR; ++r) in[r] = (double)src[(size_t)reflect_idx(y0 - 1 - NMS_R + r, H) * W + xx];
+#pragma unroll
+    for (int r = 0; r < NMS_VR; ++r) {
+      double o = in[r + NMS_R] * kGauss[0];
+#pragma unroll
+      for (int j = NMS_R; j >= 1; --j) o = o + (in[r + NMS_R - j] + in[r + NMS_R + j]) * kGauss[j];
+      s_v[r][tid] = o;
+    }
   }
   __syncthreads();
-  for (int i = tid; i < VR * GC; i += 256) {
-    const int r = i / GC, c = i - r * GC;
-    double o = s_v[r][c + NMS_R] * kGauss[0];
+  // axis 1, same recurrence along the row
+  {
+    constexpr int SEGS = (NMS_GC + NMS_SEG - 1) / NMS_SEG;   // 14 runs per row, 252 threads
+    if (tid < NMS_VR * SEGS) {
+      const int r = tid / SEGS, c0 = (tid - r * SEGS) * NMS_SEG;
+      double v[NMS_SEG + 2 * NMS_R];
 #pragma unroll
-    for (int j = NMS_R; j >= 1; --j) o = o + (s_v[r][c + NMS_R - j] + s_v[r][c + NMS_R + j]) * kGauss[j];
-    s_g[r][c] = o;
+      for (int k = 0; k < NMS_SEG + 2 * NMS_R; ++k) v[k] = c0 + k < NMS_VC ? s_v[r][c0 + k] : 0.0;
+#pragma unroll
+      for (int k = 0; k < NMS_SEG; ++k) {
+        double o = v[k + NMS_R] * kGauss[0];
+#pragma unroll
+        for (int j = NMS_R; j >= 1; --j) o = o + (v[k + NMS_R - j] + v[k + NMS_R + j]) * kGauss[j];
+        if (c0 + k < NMS_GC) s_g[r][c0 + k] = o;
+      }
+    }
   }
   __syncthreads();
-  // one wave per output row, lane = column -> one 64-bit mask word per (row, tile)
+  // one wave per (row, 64-column word) -> one 64-bit mask word
   const int lane = tid & 63, wave = tid >> 6;
-  for (int ty = wave; ty < NMS_TY; ty += 4) {
-    const int y = y0 + ty, x = x0 + lane;
+  for (int it = wave; it < NMS_TY * 3; it += 4) {
+    const int ty = it / 3, wd = it - ty * 3;
+    const int y = y0 + ty, cx = wd * 64 + lane, x = x0 + cx;
     bool pk = false;
     if (y < H && x < W) {
-      const double g = s_g[ty + 1][lane + 1];
+      const double g = s_g[ty + 1][cx + 1];
       if (mode_hand) {
         pk = g > thre;                                  // hand.py:62 binary map
       } else {
-        const double up = y > 0 ? s_g[ty][lane + 1] : 0.0;
-        const double dn = y + 1 < H ? s_g[ty + 2][lane + 1] : 0.0;
-        const double lf = x > 0 ? s_g[ty + 1][lane] : 0.0;
-        const double rt = x + 1 < W ? s_g[ty + 1][lane + 2] : 0.0;
+        const double up = y > 0 ? s_g[ty][cx + 1] : 0.0;
+        const double dn = y + 1 < H ? s_g[ty + 2][cx + 1] : 0.0;
+        const double lf = x > 0 ? s_g[ty + 1][cx] : 0.0;
+        const double rt = x + 1 < W ? s_g[ty + 1][cx + 2] : 0.0;
         pk = g >= up && g >= dn && g >= lf && g >= rt && g > thre;   // body.py:99-100
       }
     }
     const unsigned long long word = __ballot(pk);
-    if (lane == 0 && y < H) mask[((size_t)plane * H + y) * words + blockIdx.x] = word;
+    const int wi = blockIdx.x * 3 + wd;
+    if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = word;
   }
 }
 
@@ -803,11 +851,11 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       float* mp = mh + (size_t)n * g.valid_h * g.valid_w * nparts;
       midp += (size_t)n * g.valid_h * g.valid_w * (nparts + npaf) * 4;
       const long long th = (long long)n * g.valid_h * g.valid_w * nparts;
-      hipLaunchKernelGGL(resize_kernel, dim3(grid_for(th)), dim3(256), 0, s, lh, n, nparts, g.valid_h, g.valid_w, 0,
+      hipLaunchKernelGGL(resize_kernel, dim3(n * g.valid_h), dim3(256), 0, s, lh, n, nparts, g.valid_h, g.valid_w, 0,
                          1.f, (void*)mh);
       PHIP(hipGetLastError());
       const long long tp = (long long)n * g.valid_h * g.valid_w * npaf;
-      hipLaunchKernelGGL(resize_kernel, dim3(grid_for(tp)), dim3(256), 0, s, lp, n, npaf, g.valid_h, g.valid_w, 0,
+      hipLaunchKernelGGL(resize_kernel, dim3(n * g.valid_h), dim3(256), 0, s, lp, n, npaf, g.valid_h, g.valid_w, 0,
                          1.f, (void*)mp);
       PHIP(hipGetLastError());
       // stage 2: cv2.resize(crop, (W, H)): inv_scale = W / valid_w, scale = 1 / inv_scale
@@ -824,13 +872,13 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       fp = lp;
     }
     const long long tf = (long long)n * nparts * H * W;
-    hipLaunchKernelGGL(resize_kernel, dim3(grid_for(tf)), dim3(256), 0, s, fh, n, nparts, H, W, multi ? 2 : 1, div_f,
+    hipLaunchKernelGGL(resize_kernel, dim3(n * nparts * H), dim3(256), 0, s, fh, n, nparts, H, W, multi ? 2 : 1, div_f,
                        (void*)heat);
     PHIP(hipGetLastError());
     ga.paf[si] = fp;
   }
   // blur + NMS (body.py:86-100)
-  dim3 gb(words, (H + NMS_TY - 1) / NMS_TY, n * nparts);
+  dim3 gb((W + NMS_TX - 1) / NMS_TX, (H + NMS_TY - 1) / NMS_TY, n * nparts);
   if (multi)
     hipLaunchKernelGGL(blur_nms_kernel<double>, gb, dim3(256), 0, s, (const double*)heat, H, W, words, mask, 0.1, 0);
   else
@@ -897,7 +945,7 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
     MapSrc fh = lh;
     if (!(g.valid_h == h && g.valid_w == w)) {
       const long long tm = (long long)n * g.valid_h * g.valid_w * nparts;
-      hipLaunchKernelGGL(resize_kernel, dim3(grid_for(tm)), dim3(256), 0, s, lh, n, nparts, g.valid_h, g.valid_w, 0,
+      hipLaunchKernelGGL(resize_kernel, dim3(n * g.valid_h), dim3(256), 0, s, lh, n, nparts, g.valid_h, g.valid_w, 0,
                          1.f, (void*)mid);
       PHIP(hipGetLastError());
       fh.base = mid; fh.xs = nparts; fh.ys = (long long)g.valid_w * nparts; fh.cstr = 1;
@@ -907,10 +955,10 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
       fh.cn = nch; fh.identity = 0;
     }
     const long long tf = (long long)n * nparts * P;
-    hipLaunchKernelGGL(resize_kernel, dim3(grid_for(tf)), dim3(256), 0, s, fh, n, nparts, h, w, 3, div_f, (void*)avg);
+    hipLaunchKernelGGL(resize_kernel, dim3(n * nparts * h), dim3(256), 0, s, fh, n, nparts, h, w, 3, div_f, (void*)avg);
     PHIP(hipGetLastError());
   }
-  dim3 gb(words, (h + NMS_TY - 1) / NMS_TY, n * nparts);
+  dim3 gb((w + NMS_TX - 1) / NMS_TX, (h + NMS_TY - 1) / NMS_TY, n * nparts);
   hipLaunchKernelGGL(blur_nms_kernel<double>, gb, dim3(256), 0, s, (const double*)avg, h, w, words, mask, 0.05, 1);
   PHIP(hipGetLastError());
   hipLaunchKernelGGL(hand_cc_kernel, dim3(n * nparts), dim3(256), 0, s, (const double*)avg, mask, h, w, words, parent,

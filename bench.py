@@ -161,7 +161,7 @@ def main():
                      "net_ms_per_step": round(net_ms, 3), "conv_gflop_per_step": round(conv_flop / 1e9, 1)},
         "cpu_baseline": None,
     }
-    if not args.no_cpu and args.cpu_frames > 0:
+    if not args.no_cpu and args.cpu_frames > 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(args, mult, nh, nw)
     print(json.dumps(out))
     if dist:

@@ -47,14 +47,18 @@ class FrameResult:
 
 
 class BodyEstimator:
-    def __init__(self, weights: dict, model_type: str = "body25", device: int = 0, scale_search=(0.5,), caps=None):
+    def __init__(self, weights: dict = None, model_type: str = "body25", device: int = 0, scale_search=(0.5,),
+                 caps=None, net: "rt.Net" = None):
         self.kind = KINDS[model_type]
         self.model_type = model_type
         self.device = device
         self.scale_search = tuple(scale_search)
         self.caps = dict(DEFAULT_CAPS, **(caps or {}))
-        self.net = rt.Net(self.kind, device)
-        self.net.load_weights(weights)
+        if net is None:
+            net = rt.Net(self.kind, device)
+            net.load_weights(weights)
+        assert net.kind == self.kind
+        self.net = net
         self.njoint, self.npaf = NJOINT[self.kind], NPAF[self.kind]
 
     # -- network -----------------------------------------------------------------

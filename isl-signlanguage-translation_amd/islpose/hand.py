@@ -20,11 +20,14 @@ HAND_SCALES = (0.5, 1.0, 1.5, 2.0)
 
 
 class HandEstimator:
-    def __init__(self, weights: dict, device: int = 0, scale_search=HAND_SCALES):
+    def __init__(self, weights: dict = None, device: int = 0, scale_search=HAND_SCALES, net: "rt.Net" = None):
         self.device = device
         self.scale_search = tuple(scale_search)
-        self.net = rt.Net(rt.ISL_HAND, device)
-        self.net.load_weights(weights)
+        if net is None:
+            net = rt.Net(rt.ISL_HAND, device)
+            net.load_weights(weights)
+        assert net.kind == rt.ISL_HAND
+        self.net = net
 
     def run_scales(self, crops):
         import torch

@@ -1,0 +1,52 @@
+"""Frame sharding across GPUs (one process per GPU, no collective on the data path).
+
+Frames are independent units: each rank takes a contiguous shard
+of the frame index range, runs the whole hot path on its own device, and the
+per-frame keypoints (a few KB) are gathered on rank 0 on the host -- the
+MI355X counterpart of the reference's mp.Process + mp.Queue pipeline
+(extract_features_mp.py:183-239), which ran every worker on cuda:0.
+"""
+from __future__ import annotations
+
+import os
+
+
+def shard_bounds(n_items: int, rank: int, world: int):
+    """Contiguous [start, end) of `rank`'s shard; sizes differ by at most one."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    q, r = divmod(n_items, world)
+    start = rank * q + min(rank, r)
+    return start, start + q + (1 if rank < r else 0)
+
+
+def dist_env():
+    """(rank, local_rank, world) from the torch.distributed.run environment (1 process = 1 GPU)."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def run_sharded(n_frames, get_frames, estimate, batch: int, rank: int, world: int):
+    """Process this rank's shard in batches: get_frames(start, end) -> frames,
+    estimate(frames) -> list of per-frame results. Returns [(frame_index, result)]."""
+    start, end = shard_bounds(n_frames, rank, world)
+    out = []
+    for s in range(start, end, batch):
+        e = min(s + batch, end)
+        res = estimate(get_frames(s, e))
+        out.extend(zip(range(s, e), res))
+    return out
+
+
+def gather_to_rank0(local, rank: int, world: int, group=None):
+    """Host-side gather of per-frame results (no device collective); rank 0 gets
+    them ordered by frame index, other ranks get None."""
+    if world == 1:
+        return [r for _, r in sorted(local, key=lambda t: t[0])]
+    import torch.distributed as dist
+    bucket = [None] * world if rank == 0 else None
+    dist.gather_object(local, bucket, dst=0, group=group)
+    if rank != 0:
+        return None
+    merged = [item for part in bucket for item in part]
+    return [r for _, r in sorted(merged, key=lambda t: t[0])]

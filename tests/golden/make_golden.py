@@ -262,8 +262,50 @@ def g5_hand_detect(cases):
     print("handDetect cases", n)
 
 
+def g7_state_dict_keys():
+    """Ordered state_dict keys + shapes of the reference modules (the module-seam contract)."""
+    from src.model import bodypose_25_model, bodypose_model, handpose_model
+    out = {}
+    for name, cls in (("body25", bodypose_25_model), ("coco", bodypose_model), ("hand", handpose_model)):
+        out[name] = [[k, list(v.shape)] for k, v in cls().state_dict().items()]
+    json.dump(out, open(os.path.join(HERE, "state_dict_keys.json"), "w"))
+
+
+def g8_export_formats():
+    """util.get_bodypose / get_handpose on the G2 outputs and G4-style hand peaks (§8f#2)."""
+    from src import util
+    z = np.load(os.path.join(HERE, "g2_body_post.npz"))
+    out = {"body": [], "hand": []}
+    for name in sorted({k.split("/")[0] for k in z.files}):
+        cand, subset = z[name + "/candidate"], z[name + "/subset"]
+        mt = str(z[name + "/model_type"])
+        if cand.ndim != 2:
+            continue
+        circles, sticks = util.get_bodypose(cand, subset, mt)
+        out["body"].append({"case": name, "model_type": mt,
+                            "circles": [[float(a), float(b)] for a, b in circles],
+                            "sticks": [[float(v) for v in s] for s in sticks]})
+    rng = np.random.RandomState(5)
+    for nh in (0, 1, 2, 3):
+        hands = []
+        for _ in range(nh):
+            p = rng.randint(0, 200, size=(21, 2)).astype(np.int64)
+            p[rng.rand(21) < 0.2] = 0
+            hands.append(p)
+        try:
+            edges, peaks = util.get_handpose(hands)
+            res = {"edges": [[[int(e[0]), [int(v) for v in e[1]], [int(v) for v in e[2]]] for e in h] for h in edges],
+                   "peaks": [[[int(p[0]), int(p[1]), p[2]] for p in h] for h in peaks], "error": ""}
+        except IndexError as e:
+            res = {"error": "IndexError"}
+        out["hand"].append({"hands": [h.tolist() for h in hands], **res})
+    json.dump(out, open(os.path.join(HERE, "g8_export_formats.json"), "w"))
+
+
 def main():
     install_shims()
+    g7_state_dict_keys()
+    g8_export_formats()
     shutil.copy(os.path.join(REF, "src/hand_model_output_size.json"),
                 os.path.join(HERE, "hand_model_output_size.json"))
     g1_networks()

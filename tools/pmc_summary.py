@@ -1,0 +1,60 @@
+"""Summarise rocprofv3 --pmc passes of bench.py into per-step HBM traffic.
+
+Usage: python tools/pmc_summary.py <fetch_dir> <write_dir> [<sq_dir>] --steps S --out profiles/rNN/pmc_summary.json
+
+FETCH_SIZE / WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (§HBM), gfx950's
+FETCH_SIZE reports half of the bytes of wide coalesced reads: the read side is
+doubled before it is compared with algorithmic bytes; WRITE_SIZE is exact for
+16-byte-per-lane stores.  The conv kernels load 16 B per lane and store 16 B per
+lane.  Counts are divided by the number of bench steps that ran under the
+profiler (warmup + validation-free timed steps).
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+
+def load(d, name):
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    out = collections.defaultdict(float)
+    for r in csv.DictReader(open(f)):
+        if r["Counter_Name"] != name:
+            continue
+        k = r["Kernel_Name"]
+        if "conv_mfma" in k or "maxpool" in k:
+            cls = "net_run"
+        else:
+            cls = k.split("(")[0].replace("void ", "").split("<")[0]
+        out[cls] += float(r["Counter_Value"])
+    return out
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("fetch")
+    p.add_argument("write")
+    p.add_argument("--steps", type=int, required=True)
+    p.add_argument("--out", required=True)
+    p.add_argument("--traffic-out", default=None)
+    a = p.parse_args()
+    fe, wr = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fe) | set(wr)):
+        rb = fe.get(k, 0.0) * 1024 * 2 / a.steps
+        wb = wr.get(k, 0.0) * 1024 / a.steps
+        res[k] = {"read_bytes_per_step": rb, "write_bytes_per_step": wb, "hbm_bytes_per_step": rb + wb,
+                  "raw_fetch_kib_per_step": fe.get(k, 0.0) / a.steps, "raw_write_kib_per_step": wr.get(k, 0.0) / a.steps}
+    json.dump(res, open(a.out, "w"), indent=1)
+    if a.traffic_out and "net_run" in res:
+        json.dump({"hbm_bytes_per_net_run": res["net_run"]["hbm_bytes_per_step"],
+                   "source": os.path.relpath(a.out), "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->B, per bench step (one net run over the batch)"},
+                  open(a.traffic_out, "w"), indent=1)
+    for k, v in res.items():
+        print("%-40s read %10.1f MB  write %10.1f MB" % (k, v["read_bytes_per_step"] / 1e6, v["write_bytes_per_step"] / 1e6))
+
+
+if __name__ == "__main__":
+    main()

@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--scale", type=float, default=1.0,
                    help="scale_search entry: 1.0 = net at 368x656 (metric shape); 0.5 = reference default")
     p.add_argument("--persons", type=int, default=3)
+    p.add_argument("--streams", type=int, default=2,
+                   help="split the per-GPU batch over this many HIP streams (own arena each) so one "
+                        "sub-batch's layer tail overlaps the other's next layer")
     p.add_argument("--cpu-frames", type=int, default=6, help="frames for the CPU baseline sample (0 = skip)")
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()
@@ -66,7 +69,9 @@ def main():
     from islpose.body import BodyEstimator, scale_geometry
 
     B, H, W = args.batch, args.height, args.width
-    est = BodyEstimator(synth.synth_weights(0), "body25", device=local, scale_search=(args.scale,))
+    S = args.streams
+    assert B % S == 0, "batch must split evenly over the streams"
+    weights = synth.synth_weights(0)
     # frames of this rank (frame index = rank * B + i: disjoint shards)
     frames = torch.from_numpy(synth.synth_frames(B, H, W, seed=1000 + rank)).to(dev)
     (mult, nh, nw, vh, vw), = scale_geometry(H, W, (args.scale,))
@@ -74,42 +79,70 @@ def main():
     maps = [synth.designed_pose_maps(nh // 8, nw // 8, args.persons, seed=rank * B + i) for i in range(B)]
     d_paf = torch.from_numpy(np.stack([m[0] for m in maps])).to(dev)
     d_heat = torch.from_numpy(np.stack([m[1] for m in maps])).to(dev)
-    net = est.net
     import ctypes
     from islpose import runtime as rt
-    caps = rt.IslCaps(**est.caps)
-    lay = rt.body_layout(est.kind, caps)
-    d_res = torch.empty(B * lay.record_bytes, dtype=torch.uint8, device=dev)
-    h_res = torch.empty(B * lay.record_bytes, dtype=torch.uint8, pin_memory=True)
-    g = (rt.IslScaleGeom * 1)(rt.IslScaleGeom(*geoms[0]))
-    pp = (ctypes.c_void_p * 1)(d_paf.data_ptr())
-    hp = (ctypes.c_void_p * 1)(d_heat.data_ptr())
-    stream = torch.cuda.current_stream(dev)
-    sh = rt.stream_handle(stream)
     L = rt.lib()
+    main_stream = torch.cuda.current_stream(dev)
+
+    class Lane:
+        """One sub-batch on its own stream with its own net arena; lanes overlap on the GPU."""
+
+        def __init__(self, s):
+            self.est = BodyEstimator(weights, "body25", device=local, scale_search=(args.scale,))
+            self.net = self.est.net
+            self.b = B // S
+            sl = slice(s * self.b, (s + 1) * self.b)
+            self.frames, self.paf, self.heat = frames[sl], d_paf[sl], d_heat[sl]
+            self.caps = rt.IslCaps(**self.est.caps)
+            self.lay = rt.body_layout(self.est.kind, self.caps)
+            self.d_res = torch.empty(self.b * self.lay.record_bytes, dtype=torch.uint8, device=dev)
+            self.h_res = torch.empty(self.b * self.lay.record_bytes, dtype=torch.uint8, pin_memory=True)
+            self.g = (rt.IslScaleGeom * 1)(rt.IslScaleGeom(*geoms[0]))
+            self.pp = (ctypes.c_void_p * 1)(self.paf.data_ptr())
+            self.hp = (ctypes.c_void_p * 1)(self.heat.data_ptr())
+            self.stream = main_stream if S == 1 else torch.cuda.Stream(dev)
+            self.sh = rt.stream_handle(self.stream)
+
+    lanes = [Lane(s) for s in range(S)]
     ev = []
 
     def step(timed):
-        net.preprocess(frames, mult, stream=stream)
-        if timed:
+        ref = torch.cuda.Event(enable_timing=True)
+        ref.record(main_stream)
+        marks = []
+        for ln in lanes:
+            ln.stream.wait_event(ref)
+            ln.net.preprocess(ln.frames, mult, stream=ln.stream)
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-        net.run(stream=stream)
+            e0.record(ln.stream)
+            ln.net.run(stream=ln.stream)
+            e1.record(ln.stream)
+            marks.append((e0, e1))
+            rt.check(L.isl_body_post(ln.net.h, ln.b, H, W, 1, ln.g, ln.pp, ln.hp, ctypes.byref(ln.caps),
+                                     rt.ptr(ln.d_res), ln.sh), "post")
+            with torch.cuda.stream(ln.stream):
+                ln.h_res.copy_(ln.d_res, non_blocking=True)
+        for ln in lanes:
+            if ln.stream is not main_stream:
+                main_stream.wait_stream(ln.stream)
         if timed:
-            e1.record(stream)
-            ev.append((e0, e1))
-        rt.check(L.isl_body_post(net.h, B, H, W, 1, g, pp, hp, ctypes.byref(caps), rt.ptr(d_res), sh), "post")
-        h_res.copy_(d_res, non_blocking=True)
+            ev.append((ref, marks))
+
+    def net_window_ms(ref, marks):
+        # conv stage wall time of one step: first net start -> last net end over all lanes
+        return max(ref.elapsed_time(e1) for _, e1 in marks) - min(ref.elapsed_time(e0) for e0, _ in marks)
 
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize(dev)
     # validate one step's records (no overflow / errors) outside the timed region
-    host = h_res.numpy()
-    for f in range(B):
-        st = int(host[f * lay.record_bytes + lay.status:f * lay.record_bytes + lay.status + 4].view(np.int32)[0])
-        assert st == 0, "post status %d on frame %d" % (st, f)
+    for ln in lanes:
+        host = ln.h_res.numpy()
+        for f in range(ln.b):
+            o = f * ln.lay.record_bytes + ln.lay.status
+            st = int(host[o:o + 4].view(np.int32)[0])
+            assert st == 0, "post status %d on frame %d" % (st, f)
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize(dev)
@@ -120,7 +153,7 @@ def main():
     if dist:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
-    net_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    net_ms = float(np.mean([net_window_ms(r, m) for r, m in ev]))
     if dist:
         t = torch.tensor([elapsed, net_ms], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -154,6 +187,7 @@ def main():
         "config": {"workload": "configs[1]: body_25 single-scale %dx%d frames, batch %d per GPU, net input %dx%d"
                                % (H, W, B, nh, nw),
                    "batch_per_gpu": B, "frame_hw": [H, W], "scale_search": [args.scale], "net_hw": [nh, nw],
+                   "streams_per_gpu": S,
                    "parallelism": "frame-sharded x%d (no collective)" % world},
         "roofline": {"bound": "mfma", "kernel": "conv_mfma_f32 (body_25 net run, 114 convs + 3 pools)",
                      "achieved": round(achieved, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",

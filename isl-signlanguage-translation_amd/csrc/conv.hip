@@ -41,7 +41,7 @@ struct ConvArgs {
   int H, W, cin_chunks, cout, co_tiles, px_tiles, act, nblocks;
 };
 
-template <int KS, int WAVES_M, int WAVES_N, int WM, int WN>
+template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, bool GLDS>
 // 4 waves per SIMD (4 blocks of 256 threads per CU, <= 128 VGPR+AGPR, <= 40 KB LDS
 // each): the 46x82 stage layers (960 tiles at batch 32) then fit in one round.
 __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 4)
@@ -131,6 +131,30 @@ conv_mfma_f32(ConvArgs a) {
     }
   };
 
+  // LDS-DMA staging (global_load_lds_dwordx4): every wave-instruction fills 1 KiB
+  // of LDS lane-linearly (64 pixels of one channel plane, or 64 float4 of the
+  // weight slab), no staging VGPRs and no ds_write; the barrier's vmcnt(0) retires it.
+  constexpr int NWAVES = WAVES_M * WAVES_N;
+  const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto issue = [&](int t, int buf) {
+    const int c = t / KS, ky = t - c * KS;
+    const float* src = in_f + (size_t)(La + (ky - P) * Wi - P) * a.in_cs + c * 8;
+    f32x4* s = smem + buf * BUF;
+    const int nchunk = (seg + 63) >> 6;
+    for (int q = wave_u; q < NPL * nchunk; q += NWAVES) {
+      const int pl = q / nchunk, ch = q - pl * nchunk;
+      const int px = min(ch * 64 + lane, seg - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)px * a.in_cs + 4 * pl),
+                                       (__attribute__((address_space(3))) void*)(s + pl * SEGMAX + ch * 64), 16, 0,
+                                       0);
+    }
+    const f32x4* wsrc = (const f32x4*)a.wpk + ((size_t)(co_t * a.cin_chunks + c) * KS + ky) * WTILE;
+    for (int qq = wave_u; qq < WTILE / 64; qq += NWAVES)
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc + qq * 64 + lane),
+                                       (__attribute__((address_space(3))) void*)(s + NPL * SEGMAX + qq * 64), 16, 0,
+                                       0);
+  };
+
   f32x16 acc[WM][WN];
 #pragma unroll
   for (int wm = 0; wm < WM; ++wm)
@@ -139,12 +163,20 @@ conv_mfma_f32(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[wm][wn][r] = 0.f;
 
-  gload(0);
-  lstore(0);
+  if constexpr (GLDS) {
+    issue(0, 0);
+  } else {
+    gload(0);
+    lstore(0);
+  }
   __syncthreads();
   for (int t = 0; t < T; ++t) {
     const int buf = t & 1;
-    if (t + 1 < T) gload(t + 1);
+    if constexpr (GLDS) {
+      if (t + 1 < T) issue(t + 1, buf ^ 1);
+    } else {
+      if (t + 1 < T) gload(t + 1);
+    }
     const f32x4* sa = smem + buf * BUF + h * SEGMAX;
     const f32x4* sw = smem + buf * BUF + NPL * SEGMAX + h * BCO + wave_m * WM * 32 + l32;
 #pragma unroll
@@ -162,7 +194,9 @@ conv_mfma_f32(ConvArgs a) {
           for (int wn = 0; wn < WN; ++wn)
             acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[wm][e], B[wn][e], acc[wm][wn], 0, 0, 0);
     }
-    if (t + 1 < T) lstore(buf ^ 1);
+    if constexpr (!GLDS) {
+      if (t + 1 < T) lstore(buf ^ 1);
+    }
     __syncthreads();
   }
 
@@ -204,6 +238,14 @@ conv_mfma_f32(ConvArgs a) {
   }
 }
 
+// Staging variant: register staging (default) or LDS-DMA (ISLPOSE_CONV_STAGING=glds).
+// Measured equal at batch 32 (122.2 vs 122.4 TF over the net run, r01), so the
+// register path stays the default; the DMA path frees 25 VGPRs for larger tiles.
+static bool conv_staging_glds() {
+  const char* e = getenv("ISLPOSE_CONV_STAGING");
+  return e && e[0] == 'g';
+}
+
 int conv_bco_for(int cout) {
   if (cout % 128 == 0) return 128;
   if (cout == 96) return 96;
@@ -233,8 +275,12 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   const long long nb = (long long)c.n * a.px_tiles * a.co_tiles;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
-  hipLaunchKernelGGL((conv_mfma_f32<KS, WAVES_M, WAVES_N, WM, WN>), dim3(a.nblocks),
-                     dim3(WAVES_M * WAVES_N * 64), 0, s, a);
+  if (conv_staging_glds())
+    hipLaunchKernelGGL((conv_mfma_f32<KS, WAVES_M, WAVES_N, WM, WN, true>), dim3(a.nblocks),
+                       dim3(WAVES_M * WAVES_N * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_mfma_f32<KS, WAVES_M, WAVES_N, WM, WN, false>), dim3(a.nblocks),
+                       dim3(WAVES_M * WAVES_N * 64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -49,6 +49,16 @@ def test_body25_forward_vs_oracle(net25, w25, n, h, w):
     assert _rel(heat.cpu().numpy(), rh) < TOL
 
 
+def test_body25_forward_lds_dma_staging(net25, w25, monkeypatch):
+    """The LDS-DMA staging variant of the conv kernel gives the same results."""
+    x = torch.from_numpy(_inputs(2, 50, 70, seed=9)).cuda()
+    paf0, heat0 = net25.forward(x)
+    monkeypatch.setenv("ISLPOSE_CONV_STAGING", "glds")
+    paf1, heat1 = net25.forward(x)
+    torch.cuda.synchronize()
+    assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
+
+
 def test_body25_forward_golden(net25):
     g1 = np.load(os.path.join(GOLDEN, "g1_networks.npz"))
     x = _inputs(1, 184, 328, int(g1["body25_184x328_seed"]))

@@ -1,0 +1,37 @@
+"""Per-layer durations of the last bench step from a rocprofv3 kernel trace."""
+import csv
+import sys
+
+sys.path.insert(0, "isl-signlanguage-translation_amd")
+from islpose import netspec  # noqa: E402
+
+
+def main(path, h=368, w=656, B=32, kind=0, quiet=False):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "preprocess" in r["Kernel_Name"]]
+    seq = rows[idx[-1]:]
+    convs = netspec.convs_for(kind)
+    ci, tot, groups = 0, 0.0, {}
+    for r in seq:
+        n = r["Kernel_Name"]
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        tot += d
+        if "conv_mfma" in n:
+            c = convs[ci]
+            fl = 2 * c.cout * c.cin * c.k * c.k * h * w * B
+            key = "%dx%d c%d->%d k%d" % (h, w, c.cin, c.cout, c.k)
+            g = groups.setdefault(key, [0, 0.0, 0.0])
+            g[0] += 1; g[1] += d; g[2] += fl
+            if c.name in ("conv1_2", "conv2_2", "conv3_4"):
+                h //= 2; w //= 2
+            ci += 1
+        else:
+            g = groups.setdefault(n.split("(")[0][:40], [0, 0.0, 0.0])
+            g[0] += 1; g[1] += d
+    for k, (cnt, d, fl) in sorted(groups.items(), key=lambda t: -t[1][1]):
+        print("%-42s x%-3d %9.1f us  %5.1f%%  %s" % (k, cnt, d, 100 * d / tot, ("%.1f TF" % (fl / d / 1e6)) if fl else ""))
+    print("total %.1f us" % tot)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

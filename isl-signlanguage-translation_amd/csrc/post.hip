@@ -1,16 +1,19 @@
 // Post-network kernels of Body.__call__ (src/body.py:64-235) and
 // Hand.__call__ (src/hand.py:51-74):
 //
-//   resize_kernel      cv2.resize INTER_CUBIC of the low-res maps (x8, crop,
-//                      to frame size), fp32, OpenCV operation order
+//   resize_sep_kernel  cv2.resize INTER_CUBIC of the low-res maps (x8, crop,
+//                      to frame size), fp32, OpenCV operation order; planar
+//                      tiles, horizontal pass per source row staged in LDS
 //   blur_nms_kernel    gaussian_filter(sigma=3) in fp64 (scipy order) fused
 //                      with the 4-neighbour NMS -> one 64-bit mask word per
 //                      (row, 64 columns), written by a wave ballot
 //   compact_kernel     raster-order peak lists (np.nonzero order) + scores
-//   group_kernel       PAF line integral for every (A,B) pair (PAF sampled on
-//                      demand from the low-res / intermediate maps), stable
-//                      score sort, greedy matching, person assembly and
-//                      pruning -- one workgroup per frame
+//   limb_kernel        PAF line integral for every (A,B) pair of one limb
+//                      (PAF sampled on demand from the low-res / intermediate
+//                      maps), stable score sort, greedy matching -- one
+//                      workgroup per (limb, frame)
+//   assemble_kernel    person assembly, merge / delete, pruning (body.py:164-
+//                      232) -- one lane per frame
 //
 // Every floating-point expression follows the reference's evaluation order;
 // the file is built with -ffp-contract=off so no FMA is formed.
@@ -106,38 +109,70 @@ __device__ __forceinline__ float sample(const MapSrc& m, int f, int c, int y, in
   return ((hz[0] * be[0] + hz[1] * be[1]) + hz[2] * be[2]) + hz[3] * be[3];   // scalar tail
 }
 
-// out(f, c, y, x) for c < nch, y < oh, x < ow of resize `m`.
-// mode 0: dense NHWC f32 [n][oh][ow][nch]; 1: planar f32 [n][nch][oh][ow];
-// mode 2: planar f64 accumulate avg = avg + (avg + v/L)  (body.py:80, the doubling quirk)
-// mode 3: planar f64 accumulate avg += v/L                (hand.py:56)
-// One block per output row: planar modes row = (f*nch + c)*oh + y, NHWC mode row = f*oh + y.
-__global__ void __launch_bounds__(256) resize_kernel(MapSrc m, int n, int nch, int oh, int ow, int mode,
-                                                      float inv_div_f, void* out) {
-  const int row = blockIdx.x;
-  const int y = row % oh, rest = row / oh;
-  int yi[4];
-  float be[4];
-  if (!m.identity) taps(y, m.scy, m.sh, yi, be);
-  if (mode == 0) {
-    float* o = (float*)out + (size_t)row * ow * nch;
-    const int f = rest;
-    for (int i = threadIdx.x; i < ow * nch; i += blockDim.x) {
-      const int x = i / nch, c = i - x * nch;
-      o[i] = m.identity ? m.base[f * m.fs + c * m.cstr + y * m.ys + x * m.xs] : sample_row(m, f, c, yi, be, x);
-    }
-    return;
+// Separable tiled resize, planar output [n][nch][oh][ow] (f32, or f64 accumulation):
+// a block covers RS_TY output rows x RS_TX output columns of one plane.  The
+// horizontal pass is computed once per source row the tile needs (OpenCV's
+// HResizeCubic, stored in LDS), then every output combines 4 of those rows
+// (VResizeCubic) -- the same values OpenCV computes, with 4-5x fewer loads.
+constexpr int RS_TY = 8, RS_TX = 256, RS_MAXR = 40;
+__global__ void __launch_bounds__(256) resize_sep_kernel(MapSrc m, int nch, int oh, int ow, int ty_rows, int mode,
+                                                          float inv_div_f, void* out) {
+  __shared__ float s_h[RS_MAXR][RS_TX];
+  const int plane = blockIdx.x, f = plane / nch, c = plane - f * nch;
+  const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * RS_TX + threadIdx.x;
+  const int ny = min(ty_rows, oh - y0);
+  const float* b = m.base + (size_t)f * m.fs + (size_t)c * m.cstr;
+  // source rows the tile needs: [r_lo, r_lo + nr)
+  int r_lo = y0, nr = ny;
+  if (!m.identity) {
+    int lo[4], hi[4];
+    float dummy[4];
+    taps(y0, m.scy, m.sh, lo, dummy);
+    taps(y0 + ny - 1, m.scy, m.sh, hi, dummy);
+    r_lo = lo[0];
+    nr = hi[3] - r_lo + 1;
   }
-  const int c = rest % nch, f = rest / nch;
-  for (int x = threadIdx.x; x < ow; x += blockDim.x) {
-    const float v = m.identity ? m.base[f * m.fs + c * m.cstr + y * m.ys + x * m.xs] : sample_row(m, f, c, yi, be, x);
-    const size_t i = (size_t)row * ow + x;
+  if (nr > RS_MAXR) __builtin_trap();   // the host sizes ty_rows so that this cannot happen
+  if (x < ow) {
+    if (m.identity) {
+      for (int r = 0; r < nr; ++r) s_h[r][threadIdx.x] = b[(size_t)(r_lo + r) * m.ys + (size_t)x * m.xs];
+    } else {
+      int xi[4];
+      float a[4];
+      taps(x, m.scx, m.sw, xi, a);
+      const long long o0 = xi[0] * m.xs, o1 = xi[1] * m.xs, o2 = xi[2] * m.xs, o3 = xi[3] * m.xs;
+      for (int r = 0; r < nr; ++r) {
+        const float* row = b + (size_t)(r_lo + r) * m.ys;
+        s_h[r][threadIdx.x] = ((row[o0] * a[0] + row[o1] * a[1]) + row[o2] * a[2]) + row[o3] * a[3];
+      }
+    }
+  }
+  __syncthreads();
+  if (x >= ow) return;
+  const int rowlen = m.dw * m.cn, body = rowlen - rowlen % 4;
+  const bool simd = x * m.cn + c < body;
+  for (int t = 0; t < ny; ++t) {
+    const int y = y0 + t;
+    float v;
+    if (m.identity) {
+      v = s_h[t][threadIdx.x];
+    } else {
+      int yi[4];
+      float be[4];
+      taps(y, m.scy, m.sh, yi, be);
+      const float h0 = s_h[yi[0] - r_lo][threadIdx.x], h1 = s_h[yi[1] - r_lo][threadIdx.x];
+      const float h2 = s_h[yi[2] - r_lo][threadIdx.x], h3 = s_h[yi[3] - r_lo][threadIdx.x];
+      v = simd ? h0 * be[0] + (h1 * be[1] + (h2 * be[2] + h3 * be[3]))   // VResizeCubicVec_32f body
+               : ((h0 * be[0] + h1 * be[1]) + h2 * be[2]) + h3 * be[3];   // scalar tail
+    }
+    const size_t i = ((size_t)plane * oh + y) * ow + x;
     if (mode == 1) {
       ((float*)out)[i] = v;
     } else {
       double* o = (double*)out + i;
       const float q = v / inv_div_f;   // heatmap / len(multiplier), float32
-      if (mode == 2) *o = *o + (*o + (double)q);
-      else *o = *o + (double)q;
+      if (mode == 2) *o = *o + (*o + (double)q);   // body.py:80, the doubling quirk
+      else *o = *o + (double)q;                    // hand.py:56
     }
   }
 }
@@ -334,184 +369,258 @@ __device__ __forceinline__ double paf_value(const GroupArgs& a, int f, int c, in
   return acc;
 }
 
-__global__ void __launch_bounds__(256) group_kernel(GroupArgs a) {
-  const int f = blockIdx.x, tid = threadIdx.x;
+// One workgroup per (limb, frame): score every (A, B) pair (body.py:142-164),
+// stable descending sort by rank counting, greedy matching (body.py:166-175).
+__global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
+  const int k = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
   char* rec = a.result + (size_t)f * a.lay.record_bytes;
   int* status = (int*)(rec + a.lay.status);
   const int* n_peaks = (const int*)(rec + a.lay.n_peaks);
   int* n_conns = (int*)(rec + a.lay.n_conns);
-  int* n_rows = (int*)(rec + a.lay.n_rows);
   const double* peaks = (const double*)(rec + a.lay.peaks);
   double* conns = (double*)(rec + a.lay.conns);
-  double* subset = (double*)(rec + a.lay.subset);
-  double* pscore = a.pair_score + (size_t)f * a.max_pairs;
-  int* pkeep = a.pair_keep + (size_t)f * a.max_pairs;
-  int* order = a.order + (size_t)f * a.max_pairs;
-  unsigned char* usedA = a.used + (size_t)f * 2 * a.max_peaks;
+  const size_t slot = (size_t)f * a.nlimbs + k;
+  double* pscore = a.pair_score + slot * a.max_pairs;
+  int* pkeep = a.pair_keep + slot * a.max_pairs;
+  int* order = a.order + slot * a.max_pairs;
+  unsigned char* usedA = a.used + slot * 2 * a.max_peaks;
   unsigned char* usedB = usedA + a.max_peaks;
-  const int RW = a.njoint + 1;   // subset row width
-
-  __shared__ int s_off[32];
-  __shared__ int s_nkeep;
-  __shared__ int s_rows;
-  __shared__ int s_abort;
+  __shared__ int s_offA, s_offB, s_nkeep;
+  if (*status != ISL_OK) return;    // capacity overflow in compaction: host re-runs with larger caps
+  const int A = a.model == ISL_BODY25 ? kLimbs25[k][0] : kLimbsCoco[k][0];
+  const int B = a.model == ISL_BODY25 ? kLimbs25[k][1] : kLimbsCoco[k][1];
+  const int mx = a.model == ISL_BODY25 ? kMap25[k][0] : kMapCoco[k][0];
+  const int my = a.model == ISL_BODY25 ? kMap25[k][1] : kMapCoco[k][1];
+  const int nA = n_peaks[A], nB = n_peaks[B];
+  if (nA == 0 || nB == 0) {            // special_k
+    if (tid == 0) n_conns[k] = -1;
+    return;
+  }
+  const int np = nA * nB;
+  if (np > a.max_pairs) {
+    if (tid == 0) { atomicExch(status, ISL_E_CAPACITY); n_conns[k] = -2; }
+    return;
+  }
   if (tid == 0) {
     int acc = 0;
-    for (int p = 0; p < a.njoint - 1; ++p) { s_off[p] = acc; acc += n_peaks[p]; }
-    s_rows = 0;
-    s_abort = *status != ISL_OK;
+    for (int p = 0; p < a.njoint - 1; ++p) {
+      if (p == A) s_offA = acc;
+      if (p == B) s_offB = acc;
+      acc += n_peaks[p];
+    }
+    s_nkeep = 0;
+  }
+  const double* pA = peaks + (size_t)A * a.max_peaks * 3;
+  const double* pB = peaks + (size_t)B * a.max_peaks * 3;
+  for (int p = tid; p < np; p += 256) {
+    const int i = p / nB, j = p - i * nB;
+    const long long ax = (long long)pA[i * 3], ay = (long long)pA[i * 3 + 1];
+    const long long bx = (long long)pB[j * 3], by = (long long)pB[j * 3 + 1];
+    const long long vx = bx - ax, vy = by - ay;
+    double norm = sqrt((double)(vx * vx + vy * vy));     // math.sqrt of an exact integer
+    norm = 0.001 < norm ? norm : 0.001;                   // max(0.001, norm)
+    const double ux = (double)vx / norm, uy = (double)vy / norm;
+    const double stx = ((double)bx - (double)ax) / 9.0, sty = ((double)by - (double)ay) / 9.0;
+    double sum = 0.0;
+    int cnt = 0;
+    for (int I = 0; I < 10; ++I) {
+      const double sx = I == 9 ? (double)bx : (double)I * stx + (double)ax;   // np.linspace
+      const double sy = I == 9 ? (double)by : (double)I * sty + (double)ay;
+      const int xi = (int)rint(sx), yi = (int)rint(sy);                      // round half to even
+      const double s = paf_value(a, f, mx, yi, xi) * ux + paf_value(a, f, my, yi, xi) * uy;
+      sum = sum + s;                                                          // builtin sum(), left to right
+      cnt += s > 0.05;
+    }
+    const double prior = 0.5 * (double)a.H / norm - 1.0;
+    const double score = sum / 10.0 + (0.0 < prior ? 0.0 : prior);
+    pscore[p] = score;
+    pkeep[p] = (cnt > 8 && score > 0.0) ? 1 : 0;
+  }
+  for (int i = tid; i < nA; i += 256) usedA[i] = 0;
+  for (int j = tid; j < nB; j += 256) usedB[j] = 0;
+  __syncthreads();
+  // stable descending sort of the kept pairs (sorted(..., reverse=True)): rank = #(better)
+  for (int p = tid; p < np; p += 256) {
+    if (!pkeep[p]) continue;
+    const double sp = pscore[p];
+    int rank = 0;
+    for (int q = 0; q < np; ++q)
+      if (pkeep[q] && (pscore[q] > sp || (pscore[q] == sp && q < p))) ++rank;
+    order[rank] = p;
+    atomicAdd(&s_nkeep, 1);
   }
   __syncthreads();
-  if (s_abort) return;
+  if (tid == 0) {
+    double* cw = conns + (size_t)k * a.max_conns * 5;
+    const int lim = nA < nB ? nA : nB;
+    int m = 0;
+    for (int r = 0; r < s_nkeep && m < lim; ++r) {
+      const int p = order[r];
+      const int i = p / nB, j = p - i * nB;
+      if (usedA[i] || usedB[j]) continue;
+      usedA[i] = usedB[j] = 1;
+      if (m >= a.max_conns) { atomicExch(status, ISL_E_CAPACITY); break; }
+      double* c = cw + (size_t)m * 5;
+      c[0] = (double)(s_offA + i);
+      c[1] = (double)(s_offB + j);
+      c[2] = pscore[p];
+      c[3] = (double)i;
+      c[4] = (double)j;
+      ++m;
+    }
+    n_conns[k] = m;
+  }
+}
 
+// Person assembly (body.py:180-235), serial per frame: one lane per frame.
+// Person assembly (body.py:164-232) -- one wave per frame.  The subset table
+// lives in LDS when it fits (`in_lds`), so the row scans of the greedy merge are
+// LDS ballots instead of dependent global loads; the kept rows are written to
+// the record in one pass at the end.
+constexpr int ASM_LDS_ROWS = 256;   // subset rows that fit the LDS table (256 x 27 doubles = 55 KB)
+__global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds) {
+  extern __shared__ double s_subset[];
+  const int f = blockIdx.x, lane = threadIdx.x;
+  char* rec = a.result + (size_t)f * a.lay.record_bytes;
+  int* status = (int*)(rec + a.lay.status);
+  const int* n_peaks = (const int*)(rec + a.lay.n_peaks);
+  const int* n_conns = (const int*)(rec + a.lay.n_conns);
+  int* n_rows = (int*)(rec + a.lay.n_rows);
+  const double* peaks = (const double*)(rec + a.lay.peaks);
+  const double* conns = (const double*)(rec + a.lay.conns);
+  double* out = (double*)(rec + a.lay.subset);
+  double* subset = in_lds ? s_subset : out;
+  if (*status != ISL_OK) return;
+  const int RW = a.njoint + 1;   // subset row width
+  int off[32];
+  for (int p = 0, acc = 0; p < a.njoint - 1; ++p) { off[p] = acc; acc += n_peaks[p]; }
+  auto score_of = [&](int part, double id) {
+    return peaks[((size_t)part * a.max_peaks + (int)(id - off[part])) * 3 + 2];   // candidate[id, 2]
+  };
+  int rows = 0;
   for (int k = 0; k < a.nlimbs; ++k) {
+    const int m = n_conns[k];
+    if (m < 0) continue;                 // special_k
     const int A = a.model == ISL_BODY25 ? kLimbs25[k][0] : kLimbsCoco[k][0];
     const int B = a.model == ISL_BODY25 ? kLimbs25[k][1] : kLimbsCoco[k][1];
-    const int mx = a.model == ISL_BODY25 ? kMap25[k][0] : kMapCoco[k][0];
-    const int my = a.model == ISL_BODY25 ? kMap25[k][1] : kMapCoco[k][1];
-    const int nA = n_peaks[A], nB = n_peaks[B];
-    if (nA == 0 || nB == 0) {            // special_k
-      if (tid == 0) n_conns[k] = -1;
-      continue;
-    }
-    const int np = nA * nB;
-    if (np > a.max_pairs) {
-      if (tid == 0) { *status = ISL_E_CAPACITY; n_conns[k] = -2; }
-      return;
-    }
-    const double* pA = peaks + (size_t)A * a.max_peaks * 3;
-    const double* pB = peaks + (size_t)B * a.max_peaks * 3;
-    // --- score every (i, j) pair (body.py:142-164) ---
-    for (int p = tid; p < np; p += 256) {
-      const int i = p / nB, j = p - i * nB;
-      const long long ax = (long long)pA[i * 3], ay = (long long)pA[i * 3 + 1];
-      const long long bx = (long long)pB[j * 3], by = (long long)pB[j * 3 + 1];
-      const long long vx = bx - ax, vy = by - ay;
-      double norm = sqrt((double)(vx * vx + vy * vy));
-      norm = 0.001 < norm ? norm : 0.001;              // max(0.001, norm)
-      const double ux = (double)vx / norm, uy = (double)vy / norm;
-      const double stx = ((double)bx - (double)ax) / 9.0, sty = ((double)by - (double)ay) / 9.0;
-      double sum = 0.0;
-      int cnt = 0;
-      for (int I = 0; I < 10; ++I) {
-        const double sx = I == 9 ? (double)bx : (double)I * stx + (double)ax;   // np.linspace
-        const double sy = I == 9 ? (double)by : (double)I * sty + (double)ay;
-        const int xi = (int)rint(sx), yi = (int)rint(sy);                      // round half to even
-        const double s = paf_value(a, f, mx, yi, xi) * ux + paf_value(a, f, my, yi, xi) * uy;
-        sum = sum + s;
-        cnt += s > 0.05;
-      }
-      const double prior = 0.5 * (double)a.H / norm - 1.0;
-      const double score = sum / 10.0 + (0.0 < prior ? 0.0 : prior);
-      pscore[p] = score;
-      pkeep[p] = (cnt > 8 && score > 0.0) ? 1 : 0;
-    }
-    __syncthreads();
-    // --- stable descending sort of kept pairs: rank = #(better) ---
-    if (tid == 0) s_nkeep = 0;
-    __syncthreads();
-    for (int p = tid; p < np; p += 256) {
-      if (!pkeep[p]) continue;
-      const double sp = pscore[p];
-      int rank = 0;
-      for (int q = 0; q < np; ++q)
-        if (pkeep[q] && (pscore[q] > sp || (pscore[q] == sp && q < p))) ++rank;
-      order[rank] = p;
-      atomicAdd(&s_nkeep, 1);
-    }
-    for (int i = tid; i < nA; i += 256) usedA[i] = 0;
-    for (int j = tid; j < nB; j += 256) usedB[j] = 0;
-    __syncthreads();
-    if (tid == 0) {
-      // --- greedy matching (body.py:166-175) ---
-      double* cw = conns + (size_t)k * a.max_conns * 5;
-      const int lim = nA < nB ? nA : nB;
-      int m = 0;
-      for (int r = 0; r < s_nkeep && m < lim; ++r) {
-        const int p = order[r];
-        const int i = p / nB, j = p - i * nB;
-        if (usedA[i] || usedB[j]) continue;
-        usedA[i] = usedB[j] = 1;
-        if (m >= a.max_conns) { *status = ISL_E_CAPACITY; break; }
-        double* c = cw + (size_t)m * 5;
-        c[0] = (double)(s_off[A] + i);
-        c[1] = (double)(s_off[B] + j);
-        c[2] = pscore[p];
-        c[3] = (double)i;
-        c[4] = (double)j;
-        ++m;
-      }
-      n_conns[k] = m;
-      // --- assembly for limb k (body.py:185-225) ---
-      int rows = s_rows;
-      for (int ci = 0; ci < m && *status == ISL_OK; ++ci) {
-        const double* c = cw + (size_t)ci * 5;
-        const double idA = c[0], idB = c[1], sc = c[2];
-        int hit[2] = {-1, -1}, found = 0;
-        for (int r = 0; r < rows; ++r) {
+    const double* cw = conns + (size_t)k * a.max_conns * 5;
+    for (int ci = 0; ci < m; ++ci) {
+      const double* c = cw + (size_t)ci * 5;
+      const double idA = c[0], idB = c[1], sc = c[2];
+      // rows j with subset[j][A] == idA or subset[j][B] == idB, in order (body.py:191-196)
+      int hit[2] = {-1, -1}, found = 0;
+      for (int r0 = 0; r0 < rows; r0 += 64) {
+        const int r = r0 + lane;
+        bool hitr = false;
+        if (r < rows) {
           const double* row = subset + (size_t)r * RW;
-          if (row[A] == idA || row[B] == idB) {
-            if (found == 2) { found = 3; break; }
-            hit[found++] = r;
-          }
+          hitr = row[A] == idA || row[B] == idB;
         }
-        if (found == 3) { *status = ISL_E_INDEX; break; }   // body.py:196 IndexError
-        if (found == 1) {
-          double* row = subset + (size_t)hit[0] * RW;
-          if (row[B] != idB) {
-            row[B] = idB;
-            row[RW - 1] += 1.0;
-            row[RW - 2] += peaks[((size_t)B * a.max_peaks + (int)(idB - s_off[B])) * 3 + 2] + sc;
-          }
-        } else if (found == 2) {
-          double* r1 = subset + (size_t)hit[0] * RW;
-          double* r2 = subset + (size_t)hit[1] * RW;
-          bool overlap = false;
-          for (int q = 0; q < RW - 2; ++q) overlap |= (r1[q] >= 0.0) && (r2[q] >= 0.0);
-          if (!overlap) {
-            for (int q = 0; q < RW - 2; ++q) r1[q] += r2[q] + 1.0;
+        unsigned long long mask = __ballot(hitr);
+        while (mask && found < 3) {
+          const int j = __builtin_ctzll(mask);
+          mask &= mask - 1;
+          if (found < 2) hit[found] = r0 + j;
+          ++found;
+        }
+        if (found == 3) break;
+      }
+      if (found == 3) {                  // body.py:196 IndexError
+        if (lane == 0) *status = ISL_E_INDEX;
+        return;
+      }
+      if (found == 1) {
+        double* row = subset + (size_t)hit[0] * RW;
+        const bool upd = row[B] != idB;
+        __syncthreads();
+        if (upd && lane == 0) {
+          row[B] = idB;
+          row[RW - 1] += 1.0;
+          row[RW - 2] += score_of(B, idB) + sc;
+        }
+      } else if (found == 2) {
+        double* r1 = subset + (size_t)hit[0] * RW;
+        double* r2 = subset + (size_t)hit[1] * RW;
+        bool ov = false;
+        for (int q = lane; q < RW - 2; q += 64) ov |= (r1[q] >= 0.0) && (r2[q] >= 0.0);
+        const bool overlap = __ballot(ov) != 0ull;
+        __syncthreads();
+        if (!overlap) {
+          for (int q = lane; q < RW - 2; q += 64) r1[q] += r2[q] + 1.0;
+          if (lane == 0) {
             r1[RW - 2] += r2[RW - 2];
             r1[RW - 1] += r2[RW - 1];
             r1[RW - 2] += sc;
-            for (int r = hit[1]; r + 1 < rows; ++r)     // np.delete(subset, j2, 0)
-              for (int q = 0; q < RW; ++q) subset[(size_t)r * RW + q] = subset[(size_t)(r + 1) * RW + q];
-            --rows;
-          } else {
-            r1[B] = idB;
-            r1[RW - 1] += 1.0;
-            r1[RW - 2] += peaks[((size_t)B * a.max_peaks + (int)(idB - s_off[B])) * 3 + 2] + sc;
           }
-        } else if (k < a.njoint - 2) {
-          if (rows >= a.max_rows) { *status = ISL_E_CAPACITY; break; }
-          double* row = subset + (size_t)rows * RW;
-          for (int q = 0; q < RW; ++q) row[q] = -1.0;
+          __syncthreads();
+          // np.delete(subset, j2, 0): every element after row j2 moves up one row;
+          // each wave step loads its 64 elements before storing them
+          const int tail = (rows - 1 - hit[1]) * RW;
+          double* d = subset + (size_t)hit[1] * RW;
+          for (int i0 = 0; i0 < tail; i0 += 64) {
+            const int i = i0 + lane;
+            const double v = i < tail ? d[i + RW] : 0.0;
+            __syncthreads();
+            if (i < tail) d[i] = v;
+            __syncthreads();
+          }
+          --rows;
+        } else if (lane == 0) {
+          r1[B] = idB;
+          r1[RW - 1] += 1.0;
+          r1[RW - 2] += score_of(B, idB) + sc;
+        }
+      } else if (k < a.njoint - 2) {
+        if (rows >= a.max_rows) {
+          if (lane == 0) *status = ISL_E_CAPACITY;
+          return;
+        }
+        double* row = subset + (size_t)rows * RW;
+        const double sAB = lane == 0 ? (score_of(A, idA) + score_of(B, idB)) + sc : 0.0;
+        for (int q = lane; q < RW; q += 64) row[q] = -1.0;
+        __syncthreads();
+        if (lane == 0) {
           row[A] = idA;
           row[B] = idB;
           row[RW - 1] = 2.0;
-          const double sa = peaks[((size_t)A * a.max_peaks + (int)(idA - s_off[A])) * 3 + 2];
-          const double sb = peaks[((size_t)B * a.max_peaks + (int)(idB - s_off[B])) * 3 + 2];
-          row[RW - 2] = (sa + sb) + sc;
-          ++rows;
+          row[RW - 2] = sAB;
         }
+        ++rows;
       }
-      s_rows = rows;
-      s_abort = *status != ISL_OK;
+      __syncthreads();
     }
-    __syncthreads();
-    if (s_abort) return;
   }
-  if (tid == 0) {
-    // prune (body.py:227-231)
-    int w = 0;
-    for (int r = 0; r < s_rows; ++r) {
+  // prune (body.py:227-231): keep rows with count >= 4 and mean score >= 0.4, in order
+  int w = 0;
+  for (int r0 = 0; r0 < rows; r0 += 64) {
+    const int r = r0 + lane;
+    bool keep = false;
+    if (r < rows) {
       const double* row = subset + (size_t)r * RW;
-      if (row[RW - 1] < 4.0 || row[RW - 2] / row[RW - 1] < 0.4) continue;
-      if (w != r)
-        for (int q = 0; q < RW; ++q) subset[(size_t)w * RW + q] = row[q];
-      ++w;
+      keep = !(row[RW - 1] < 4.0 || row[RW - 2] / row[RW - 1] < 0.4);
     }
-    *n_rows = w;
+    const unsigned long long km = __ballot(keep);
+    if (in_lds) {
+      if (keep) {
+        const int dst = w + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(km >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)km, 0u));
+        for (int q = 0; q < RW; ++q) out[(size_t)dst * RW + q] = subset[(size_t)r * RW + q];
+      }
+    } else {
+      // in place, in order (destination rows never pass their source rows)
+      unsigned long long mm = km;
+      int dst = w;
+      while (mm) {
+        const int j = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        if (dst != r0 + j)
+          for (int q = lane; q < RW; q += 64) out[(size_t)dst * RW + q] = out[(size_t)(r0 + j) * RW + q];
+        ++dst;
+        __syncthreads();
+      }
+    }
+    w += __builtin_popcountll(km);
   }
+  if (lane == 0) *n_rows = w;
 }
 
 // ---------------------------------------------------------------------------
@@ -773,7 +882,20 @@ static int post_fail(int code, const char* msg) {
     }                                                       \
   } while (0)
 
-static int grid_for(long long total) { return (int)std::min<long long>((total + 255) / 256, 256 * 32); }
+// planar resize of n*nch planes (see resize_sep_kernel); rows per tile sized to the LDS window
+static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mode, float div_f, void* out,
+                         hipStream_t s) {
+  int ty = RS_TY;
+  if (!m.identity)
+    while (ty > 1 && (ty - 1) * m.scy + 5.0 > (double)RS_MAXR) --ty;
+  const long long ty_tiles = (oh + ty - 1) / ty;
+  if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "resize: output too tall");
+  hipLaunchKernelGGL(resize_sep_kernel, dim3(n * nch, (unsigned)ty_tiles, (ow + RS_TX - 1) / RS_TX), dim3(RS_TX), 0, s,
+                     m, nch, oh, ow, ty, mode, div_f, out);
+  PHIP(hipGetLastError());
+  return ISL_OK;
+}
+
 
 // Low-res map of scale s: caller NCHW array or the net's arena output.
 static int low_src(isl_net* net, const float* p, int which, int n, int C, int h8, int w8, MapSrc* m) {
@@ -813,8 +935,8 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   }
   const int words = (W + 63) / 64;
   const size_t mask_bytes = (size_t)n * nparts * H * words * 8;
-  const size_t pair_bytes = (size_t)n * caps->max_pairs * (8 + 4 + 4);
-  const size_t used_bytes = (size_t)n * 2 * caps->max_peaks;
+  const size_t pair_bytes = (size_t)n * nlimbs * caps->max_pairs * (8 + 4 + 4);
+  const size_t used_bytes = (size_t)n * nlimbs * 2 * caps->max_peaks;
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t total = up(heat_bytes) + up(mid_bytes) + up(mask_bytes) + up(pair_bytes) + up(used_bytes);
   char* base = (char*)net_scratch(net, total);
@@ -850,17 +972,12 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       float* mh = (float*)midp;
       float* mp = mh + (size_t)n * g.valid_h * g.valid_w * nparts;
       midp += (size_t)n * g.valid_h * g.valid_w * (nparts + npaf) * 4;
-      const long long th = (long long)n * g.valid_h * g.valid_w * nparts;
-      hipLaunchKernelGGL(resize_kernel, dim3(n * g.valid_h), dim3(256), 0, s, lh, n, nparts, g.valid_h, g.valid_w, 0,
-                         1.f, (void*)mh);
-      PHIP(hipGetLastError());
-      const long long tp = (long long)n * g.valid_h * g.valid_w * npaf;
-      hipLaunchKernelGGL(resize_kernel, dim3(n * g.valid_h), dim3(256), 0, s, lp, n, npaf, g.valid_h, g.valid_w, 0,
-                         1.f, (void*)mp);
-      PHIP(hipGetLastError());
+      if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, mh, s))) return rc;
+      if ((rc = launch_resize(lp, n, npaf, g.valid_h, g.valid_w, 1, 1.f, mp, s))) return rc;
       // stage 2: cv2.resize(crop, (W, H)): inv_scale = W / valid_w, scale = 1 / inv_scale
       auto stage2 = [&](MapSrc& m, const float* p, int C, int cn) {
-        m.base = p; m.xs = C; m.ys = (long long)g.valid_w * C; m.cstr = 1; m.fs = (long long)g.valid_h * g.valid_w * C;
+        m.base = p; m.xs = 1; m.ys = g.valid_w; m.cstr = (long long)g.valid_h * g.valid_w;
+        m.fs = (long long)C * g.valid_h * g.valid_w;
         m.sh = g.valid_h; m.sw = g.valid_w; m.dh = H; m.dw = W;
         m.scy = 1.0 / ((double)H / g.valid_h); m.scx = 1.0 / ((double)W / g.valid_w);
         m.cn = cn; m.identity = 0;
@@ -871,10 +988,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       fh = lh;
       fp = lp;
     }
-    const long long tf = (long long)n * nparts * H * W;
-    hipLaunchKernelGGL(resize_kernel, dim3(n * nparts * H), dim3(256), 0, s, fh, n, nparts, H, W, multi ? 2 : 1, div_f,
-                       (void*)heat);
-    PHIP(hipGetLastError());
+    if ((rc = launch_resize(fh, n, nparts, H, W, multi ? 2 : 1, div_f, heat, s))) return rc;
     ga.paf[si] = fp;
   }
   // blur + NMS (body.py:86-100)
@@ -899,11 +1013,16 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   ga.max_rows = caps->max_rows;
   ga.lay = lay;
   ga.result = (char*)d_result;
+  const size_t slots = (size_t)n * nlimbs;
   ga.pair_score = (double*)pairs;
-  ga.pair_keep = (int*)(pairs + (size_t)n * caps->max_pairs * 8);
-  ga.order = ga.pair_keep + (size_t)n * caps->max_pairs;
+  ga.pair_keep = (int*)(pairs + slots * caps->max_pairs * 8);
+  ga.order = ga.pair_keep + slots * caps->max_pairs;
   ga.used = used;
-  hipLaunchKernelGGL(group_kernel, dim3(n), dim3(256), 0, s, ga);
+  hipLaunchKernelGGL(limb_kernel, dim3(nlimbs, n), dim3(256), 0, s, ga);
+  PHIP(hipGetLastError());
+  const int asm_lds = caps->max_rows <= ASM_LDS_ROWS;
+  hipLaunchKernelGGL(assemble_kernel, dim3(n), dim3(64), asm_lds ? (size_t)caps->max_rows * (njoint + 1) * 8 : 0, s,
+                     ga, asm_lds);
   PHIP(hipGetLastError());
   return ISL_OK;
 }
@@ -944,19 +1063,14 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
     lh.dh = h8 * 8; lh.dw = w8 * 8; lh.scy = lh.scx = 1.0 / 8.0; lh.cn = nch; lh.identity = 0;
     MapSrc fh = lh;
     if (!(g.valid_h == h && g.valid_w == w)) {
-      const long long tm = (long long)n * g.valid_h * g.valid_w * nparts;
-      hipLaunchKernelGGL(resize_kernel, dim3(n * g.valid_h), dim3(256), 0, s, lh, n, nparts, g.valid_h, g.valid_w, 0,
-                         1.f, (void*)mid);
-      PHIP(hipGetLastError());
-      fh.base = mid; fh.xs = nparts; fh.ys = (long long)g.valid_w * nparts; fh.cstr = 1;
-      fh.fs = (long long)g.valid_h * g.valid_w * nparts;
+      if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, mid, s))) return rc;
+      fh.base = mid; fh.xs = 1; fh.ys = g.valid_w; fh.cstr = (long long)g.valid_h * g.valid_w;
+      fh.fs = (long long)nparts * g.valid_h * g.valid_w;
       fh.sh = g.valid_h; fh.sw = g.valid_w; fh.dh = h; fh.dw = w;
       fh.scy = 1.0 / ((double)h / g.valid_h); fh.scx = 1.0 / ((double)w / g.valid_w);
       fh.cn = nch; fh.identity = 0;
     }
-    const long long tf = (long long)n * nparts * P;
-    hipLaunchKernelGGL(resize_kernel, dim3(n * nparts * h), dim3(256), 0, s, fh, n, nparts, h, w, 3, div_f, (void*)avg);
-    PHIP(hipGetLastError());
+    if ((rc = launch_resize(fh, n, nparts, h, w, 3, div_f, avg, s))) return rc;
   }
   dim3 gb((w + NMS_TX - 1) / NMS_TX, (h + NMS_TY - 1) / NMS_TY, n * nparts);
   hipLaunchKernelGGL(blur_nms_kernel<double>, gb, dim3(256), 0, s, (const double*)avg, h, w, words, mask, 0.05, 1);

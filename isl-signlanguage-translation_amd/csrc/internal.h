@@ -39,6 +39,11 @@ struct ConvLaunch {
 // Returns the block tile width (output channels) the conv kernels use for cout.
 int conv_bco_for(int cout);
 hipError_t launch_conv(const ConvLaunch& c, hipStream_t s);
+// Winograd F(2x2,3x3) path for 3x3 layers: output channels per block tile
+// (64, 96 or 32), or 0 when cout does not fit one of them; `c.wpk` then holds
+// the transformed filters [co_tile][chunk][xi 16][plane 2][BCO][4].
+int wino_bco_for(int cout);
+hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
 
 hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s);
 hipError_t launch_pack_nchw(const float* x, int n, int C, int h, int w, const Act& out, hipStream_t s);

@@ -53,7 +53,9 @@ struct ConvLayer {
   bool has_w = false, has_b = false, has_s = false;
   std::vector<Seg> cmap;
   int cin_phys = 0, bco = 0;
+  int wbco = 0;                  // Winograd tile (3x3 layers), 0 = direct only
   float *d_w = nullptr, *d_b = nullptr, *d_s = nullptr;
+  float* d_wu = nullptr;         // Winograd-transformed filters
 };
 
 static ConvLayer mk(const std::string& name, int cin, int cout, int k, int act, const std::string& prelu = "") {
@@ -226,6 +228,7 @@ struct Builder {
     c.cmap = cmap;
     c.cin_phys = cin_phys;
     c.bco = conv_bco_for(c.cout);
+    c.wbco = c.k == 3 ? wino_bco_for(c.cout) : 0;
     net->ops.push_back({0, li, in, in_coff, out, out_coff, 0});
   }
   void pool(int in, int out, int C) { net->ops.push_back({1, -1, in, 0, out, 0, C}); }
@@ -381,6 +384,34 @@ static std::vector<float> pack_weights(const ConvLayer& c) {
   return out;
 }
 
+// U = G g G^T of every (co, physical ci) 3x3 filter, in double, rounded once to
+// fp32; layout [co_tile][chunk][xi = 4*row + col][plane][BCO][4] (wino.hip).
+static std::vector<float> pack_wino(const ConvLayer& c) {
+  const int bco = c.wbco, chunks = c.cin_phys / 8, co_tiles = c.cout / bco;
+  std::vector<int> p2l(c.cin_phys, -1);
+  for (const Seg& s : c.cmap)
+    for (int i = 0; i < s.len; ++i) p2l[s.phys + i] = s.logical + i;
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  std::vector<float> out((size_t)co_tiles * chunks * 16 * 2 * bco * 4, 0.f);
+  for (int co = 0; co < c.cout; ++co)
+    for (int pc = 0; pc < c.cin_phys; ++pc) {
+      const int lci = p2l[pc];
+      if (lci < 0) continue;
+      const float* g = &c.w[((size_t)co * c.cin + lci) * 9];
+      double t[4][3];
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 3; ++j) t[i][j] = G[i][0] * g[0 * 3 + j] + G[i][1] * g[1 * 3 + j] + G[i][2] * g[2 * 3 + j];
+      const int ct = co / bco, i_co = co % bco, ch = pc / 8, pl = (pc % 8) / 4, e = pc % 4;
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+          const double u = t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2];
+          const int xi = 4 * i + j;
+          out[((((size_t)ct * chunks + ch) * 16 + xi) * 2 + pl) * bco * 4 + (size_t)i_co * 4 + e] = (float)u;
+        }
+    }
+  return out;
+}
+
 static int upload_params(isl_net* net) {
   for (ConvLayer& c : net->layers) {
     if (!c.has_w || !c.has_b || (c.act == ACT_PRELU && !c.has_s))
@@ -396,6 +427,11 @@ static int upload_params(isl_net* net) {
     HIP_OK(hipMemcpy(c.d_w, wp.data(), wp.size() * sizeof(float), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(c.d_b, bp.data(), bp.size() * sizeof(float), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(c.d_s, sp.data(), sp.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (c.wbco) {
+      std::vector<float> up = pack_wino(c);
+      if (!c.d_wu) HIP_OK(hipMalloc(&c.d_wu, up.size() * sizeof(float)));
+      HIP_OK(hipMemcpy(c.d_wu, up.data(), up.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
   }
   net->packed = true;
   return ISL_OK;
@@ -435,6 +471,13 @@ static int plan(isl_net* net, int n, int h, int w) {
   return ISL_OK;
 }
 
+// 3x3 layers: Winograd F(2x2,3x3) by default; ISLPOSE_CONV_ALGO=direct selects the
+// direct implicit-GEMM kernel for every layer (read per call, for A/B tests).
+static bool conv_algo_wino() {
+  const char* e = getenv("ISLPOSE_CONV_ALGO");
+  return !(e && e[0] == 'd');
+}
+
 static int run_ops(isl_net* net, hipStream_t s) {
   for (const Op& op : net->ops) {
     const Act& in = net->act[op.in];
@@ -450,7 +493,12 @@ static int run_ops(isl_net* net, hipStream_t s) {
     L.wpk = c.d_w; L.bias = c.d_b; L.slope = c.d_s;
     L.n = in.n; L.H = in.H; L.W = in.W; L.ks = c.k; L.cin_chunks = c.cin_phys / 8;
     L.cout = c.cout; L.bco = c.bco; L.act = c.act;
-    HIP_OK(launch_conv(L, s));
+    if (c.wbco && conv_algo_wino()) {
+      L.wpk = c.d_wu; L.bco = c.wbco;
+      HIP_OK(launch_wino(L, s));
+    } else {
+      HIP_OK(launch_conv(L, s));
+    }
   }
   return ISL_OK;
 }
@@ -525,6 +573,7 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_w) (void)hipFree(c.d_w);
     if (c.d_b) (void)hipFree(c.d_b);
     if (c.d_s) (void)hipFree(c.d_s);
+    if (c.d_wu) (void)hipFree(c.d_wu);
   }
   for (auto& kv : net->plans) (void)hipFree(kv.second.first);
   if (net->scratch) (void)hipFree(net->scratch);

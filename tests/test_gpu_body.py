@@ -49,9 +49,24 @@ def test_body25_forward_vs_oracle(net25, w25, n, h, w):
     assert _rel(heat.cpu().numpy(), rh) < TOL
 
 
+@pytest.mark.parametrize("algo", ["direct", "wino"])
+def test_body25_forward_algo_vs_oracle(net25, w25, monkeypatch, algo):
+    """Both 3x3 algorithms (direct implicit GEMM, Winograd F(2x2,3x3)) against the
+    oracle; 2 x 184x328 puts odd sizes (23x41) on the stage layers."""
+    monkeypatch.setenv("ISLPOSE_CONV_ALGO", algo)
+    x = _inputs(2, 184, 328, seed=77)
+    paf, heat = net25.forward(torch.from_numpy(x).cuda())
+    torch.cuda.synchronize()
+    rp, rh = cpu_ref.make_net_fn("body25", w25)(x)
+    ep, eh = _rel(paf.cpu().numpy(), rp), _rel(heat.cpu().numpy(), rh)
+    print("algo %s: rel err paf %.3g heat %.3g" % (algo, ep, eh))
+    assert ep < TOL and eh < TOL
+
+
 def test_body25_forward_lds_dma_staging(net25, w25, monkeypatch):
     """The LDS-DMA staging variant of the conv kernel gives the same results."""
     x = torch.from_numpy(_inputs(2, 50, 70, seed=9)).cuda()
+    monkeypatch.setenv("ISLPOSE_CONV_ALGO", "direct")
     paf0, heat0 = net25.forward(x)
     monkeypatch.setenv("ISLPOSE_CONV_STAGING", "glds")
     paf1, heat1 = net25.forward(x)

@@ -12,10 +12,10 @@
 //
 // Pixel tiles: BPX consecutive output pixels of one frame in raster order
 // (flattened M; a frame's last tile is partial, nothing else is wasted).  The
-// input buffer is stored with a zero ring (Act.pad >= k/2), so in its padded
-// linear pixel index L = (y+p)*(W+2p) + (x+p) the input row dy of a whole tile
-// is ONE contiguous segment [La + dy*Wp - P, Lb + dy*Wp + P]: no bounds checks,
-// no im2col, no halo logic beyond a per-lane offset.
+// input buffer is stored in 8-channel chunks with a zero ring (Act.pad >= k/2),
+// so in its padded linear pixel index L = (y+p)*(W+2p) + (x+p) the input row dy
+// of a whole tile is ONE contiguous segment [La + dy*Wp - P, Lb + dy*Wp + P] of
+// 32-byte pixels: no bounds checks, no im2col, fully coalesced loads.
 //
 // K loop: one step = (8-channel chunk, kernel row ky): stage that row's input
 // segment (8 ch) and the KS x 8 x BCO weight slab into LDS (register-staged,
@@ -36,8 +36,9 @@ struct ConvArgs {
   const float* wpk;
   const float* bias;
   const float* slope;
-  int in_pad, in_cs, in_coff;
-  int out_pad, out_cs, out_coff;
+  long long in_fs, in_chs;      // frame / chunk strides (floats) of the input buffer
+  long long out_fs, out_chs;
+  int in_pad, out_pad;
   int H, W, cin_chunks, cout, co_tiles, px_tiles, act, nblocks;
 };
 
@@ -79,7 +80,7 @@ conv_mfma_f32(ConvArgs a) {
   const int La = (ya + a.in_pad) * Wi + xa + a.in_pad;
   const int Lb = (yb + a.in_pad) * Wi + xb + a.in_pad;
   const int seg = Lb - La + 2 * P + 1;
-  const float* in_f = a.in + (size_t)n * (a.H + 2 * a.in_pad) * Wi * a.in_cs + a.in_coff;
+  const float* in_f = a.in + (size_t)n * a.in_fs;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wave_m = wave % WAVES_M, wave_n = wave / WAVES_M;
@@ -100,13 +101,13 @@ conv_mfma_f32(ConvArgs a) {
 
   auto gload = [&](int t) {
     const int c = t / KS, ky = t - c * KS;
-    const float* src = in_f + (size_t)(La + (ky - P) * Wi - P) * a.in_cs + c * 8;
+    const float* src = in_f + (size_t)c * a.in_chs + (size_t)(La + (ky - P) * Wi - P) * 8;
 #pragma unroll
     for (int pl = 0; pl < NPL; ++pl)
 #pragma unroll
       for (int i = 0; i < ACT_IT; ++i) {
         const int px = tid + i * NT;
-        ra[pl][i] = (px < seg) ? *(const f32x4*)(src + (size_t)px * a.in_cs + 4 * pl) : f32x4{0.f, 0.f, 0.f, 0.f};
+        ra[pl][i] = (px < seg) ? *(const f32x4*)(src + (size_t)px * 8 + 4 * pl) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     const f32x4* wsrc = (const f32x4*)a.wpk + ((size_t)(co_t * a.cin_chunks + c) * KS + ky) * WTILE;
 #pragma unroll
@@ -138,13 +139,13 @@ conv_mfma_f32(ConvArgs a) {
   const int wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto issue = [&](int t, int buf) {
     const int c = t / KS, ky = t - c * KS;
-    const float* src = in_f + (size_t)(La + (ky - P) * Wi - P) * a.in_cs + c * 8;
+    const float* src = in_f + (size_t)c * a.in_chs + (size_t)(La + (ky - P) * Wi - P) * 8;
     f32x4* s = smem + buf * BUF;
     const int nchunk = (seg + 63) >> 6;
     for (int q = wave_u; q < NPL * nchunk; q += NWAVES) {
       const int pl = q / nchunk, ch = q - pl * nchunk;
       const int px = min(ch * 64 + lane, seg - 1);
-      __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)px * a.in_cs + 4 * pl),
+      __builtin_amdgcn_global_load_lds((const void*)(src + (size_t)px * 8 + 4 * pl),
                                        (__attribute__((address_space(3))) void*)(s + pl * SEGMAX + ch * 64), 16, 0,
                                        0);
     }
@@ -202,13 +203,13 @@ conv_mfma_f32(ConvArgs a) {
 
   // epilogue: bias + activation, masked float4 stores into the output slice
   const int Wo = a.W + 2 * a.out_pad;
-  float* out_f = a.out + (size_t)n * (a.H + 2 * a.out_pad) * Wo * a.out_cs + a.out_coff;
+  float* out_f = a.out + (size_t)n * a.out_fs;
 #pragma unroll
   for (int wn = 0; wn < WN; ++wn) {
     const int m = m0 + (wave_n * WN + wn) * 32 + l32;
     if (m > mlast) continue;
     const int y = m / a.W, x = m - y * a.W;
-    float* op = out_f + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * a.out_cs;
+    float* op = out_f + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8;
 #pragma unroll
     for (int wm = 0; wm < WM; ++wm) {
       const int cob = co_t * BCO + (wave_m * WM + wm) * 32 + 4 * h;
@@ -226,12 +227,13 @@ conv_mfma_f32(ConvArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
         }
+        float* oc = op + (size_t)(co >> 3) * a.out_chs + (co & 7);
         if (co + 3 < a.cout) {
-          *(f32x4*)(op + co) = v;
+          *(f32x4*)oc = v;
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            if (co + e < a.cout) op[co + e] = v[e];
+            if (co + e < a.cout) oc[e] = v[e];
         }
       }
     }
@@ -264,10 +266,16 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   const int max_seg = BPX - 1 + 2 * c.in_pad * max_rows + 2 * P + 1;
   if (max_seg > 2 * BPX) { set_error("conv: image too narrow for the pixel tile"); return hipErrorInvalidValue; }
   if (c.bco != BCO) { set_error("conv: tile mismatch"); return hipErrorInvalidValue; }
+  if ((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 7) { set_error("conv: slice not on a chunk"); return hipErrorInvalidValue; }
   ConvArgs a;
-  a.in = c.in; a.out = c.out; a.wpk = c.wpk; a.bias = c.bias; a.slope = c.slope;
-  a.in_pad = c.in_pad; a.in_cs = c.in_cs; a.in_coff = c.in_coff;
-  a.out_pad = c.out_pad; a.out_cs = c.out_cs; a.out_coff = c.out_coff;
+  a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
+  a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
+  a.in_fs = a.in_chs * (c.in_cs / 8);
+  a.out_fs = a.out_chs * (c.out_cs / 8);
+  a.in = c.in + (c.in_coff / 8) * a.in_chs;
+  a.out = c.out + (c.out_coff / 8) * a.out_chs;
+  a.wpk = c.wpk; a.bias = c.bias; a.slope = c.slope;
+  a.in_pad = c.in_pad; a.out_pad = c.out_pad;
   a.H = c.H; a.W = c.W; a.cin_chunks = c.cin_chunks; a.cout = c.cout;
   a.co_tiles = (c.cout + BCO - 1) / BCO;
   a.px_tiles = (c.H * c.W + BPX - 1) / BPX;

@@ -7,15 +7,18 @@
 
 namespace isl {
 
-// Activation buffer: NHWC float32 with a zero ring of `pad` pixels around every
-// frame, i.e. element (n, y, x, c) lives at
-//   base + ((n*(H+2p) + y+p) * (W+2p) + x+p) * cs + c.
-// Convolutions read/write channel slices [coff, coff+C) of such buffers, which
-// is how every torch.cat of the reference becomes zero-copy.
+// Activation buffer: float32 in 8-channel chunks ("NC8HW8"), with a zero ring of
+// `pad` pixels around every frame, i.e. element (n, y, x, c) lives at
+//   base + ((n*(cs/8) + c/8) * (H+2p) + y+p) * (W+2p) * 8 + (x+p) * 8 + c%8.
+// A chunk of consecutive pixels is contiguous, so every kernel that walks pixels
+// for a K step of 8 channels reads whole cache lines.  Convolutions read/write
+// channel slices [coff, coff+C) (coff a multiple of 8) of such buffers, which is
+// how every torch.cat of the reference becomes zero-copy.
 struct Act {
   float* base = nullptr;
-  int n = 0, H = 0, W = 0, pad = 0, cs = 0;
-  size_t frame_elems() const { return (size_t)(H + 2 * pad) * (W + 2 * pad) * cs; }
+  int n = 0, H = 0, W = 0, pad = 0, cs = 0;   // cs: channel capacity, a multiple of 8
+  size_t chunk_elems() const { return (size_t)(H + 2 * pad) * (W + 2 * pad) * 8; }
+  size_t frame_elems() const { return chunk_elems() * (cs / 8); }
   size_t bytes() const { return frame_elems() * n * sizeof(float); }
 };
 
@@ -40,7 +43,7 @@ struct ConvLaunch {
 int conv_bco_for(int cout);
 hipError_t launch_conv(const ConvLaunch& c, hipStream_t s);
 // Winograd F(2x2,3x3) path for 3x3 layers: output channels per block tile
-// (64, 96 or 32), or 0 when cout does not fit one of them; `c.wpk` then holds
+// (64 or 96), or 0 when cout does not fit one of them; `c.wpk` then holds
 // the transformed filters [co_tile][chunk][xi 16][plane 2][BCO][4].
 int wino_bco_for(int cout);
 hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
@@ -52,8 +55,10 @@ hipError_t launch_preprocess(const uint8_t* frames, int n, int H, int W, double 
                              int rh, int rw, const Act& out, hipStream_t s);
 
 struct MapSrc {            // one single-stage cubic resize, sampled per output element
-  const float* base;       // element (f, c, y, x) at base + f*fs + c*cstr + y*ys + x*xs
-  long long fs, cstr, ys, xs;
+  const float* base;       // element (f, c, y, x) at base + f*fs + chan(c) + y*ys + x*xs,
+  long long fs, cstr, ys, xs;   //   chan(c) = (c >> cshift) * cbig + (c & (2^cshift - 1)) * cstr
+  long long cbig;          // chunk stride of a chunked (arena) map; planar maps: cshift = 30, cbig = 0
+  int cshift;
   int sh, sw;              // source size (tap clamping)
   int dh, dw;              // destination size of this resize
   double scy, scx;         // source pixels per destination pixel (1/inv_scale)

@@ -1,54 +1,58 @@
-// Byte-moving kernels around the convolutions: 2x2 max-pool, NCHW <-> padded
-// NHWC packing, and the frame pre-processing of Body/Hand.__call__.
+// Byte-moving kernels around the convolutions: 2x2 max-pool, NCHW <-> chunked
+// padded packing, and the frame pre-processing of Body/Hand.__call__.
 #include "internal.h"
 
 namespace isl {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// nn.MaxPool2d(2, 2, 0) (model.py:30-31): floor mode, NHWC, 4 channels per thread.
-__global__ void maxpool2_kernel(const float* __restrict__ in, int ip, int ics, int iH, int iW,
-                                float* __restrict__ out, int op, int ocs, int oH, int oW, int C4, int n) {
-  const long long total = (long long)n * oH * oW * C4;
+// nn.MaxPool2d(2, 2, 0) (model.py:30-31): floor mode, 4 channels per thread;
+// thread order (frame, chunk, y, x, half) so a wave reads and writes contiguous bytes.
+__global__ void maxpool2_kernel(const float* __restrict__ in, int ip, int iH, int iW, float* __restrict__ out,
+                                int op, int oH, int oW, int chunks, int in_chunks, int out_chunks, int n) {
+  const long long total = (long long)n * chunks * oH * oW * 2;
+  const int iWp = iW + 2 * ip, oWp = oW + 2 * op;
+  const size_t ich = (size_t)(iH + 2 * ip) * iWp * 8, och = (size_t)(oH + 2 * op) * oWp * 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c4 = (int)(i % C4);
-    long long r = i / C4;
+    const int half = (int)(i & 1);
+    long long r = i >> 1;
     const int x = (int)(r % oW); r /= oW;
-    const int y = (int)(r % oH);
-    const int f = (int)(r / oH);
-    const int iWp = iW + 2 * ip, oWp = oW + 2 * op;
-    const float* p = in + ((size_t)f * (iH + 2 * ip) * iWp + (size_t)(2 * y + ip) * iWp + 2 * x + ip) * ics + 4 * c4;
-    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + ics);
-    const f32x4 c = *(const f32x4*)(p + (size_t)iWp * ics), d = *(const f32x4*)(p + (size_t)iWp * ics + ics);
+    const int y = (int)(r % oH); r /= oH;
+    const int k = (int)(r % chunks);
+    const int f = (int)(r / chunks);
+    const float* p = in + ((size_t)f * in_chunks + k) * ich + ((size_t)(2 * y + ip) * iWp + 2 * x + ip) * 8 + 4 * half;
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 8);
+    const f32x4 c = *(const f32x4*)(p + (size_t)iWp * 8), d = *(const f32x4*)(p + (size_t)iWp * 8 + 8);
     f32x4 m;
 #pragma unroll
     for (int e = 0; e < 4; ++e) m[e] = fmaxf(fmaxf(a[e], b[e]), fmaxf(c[e], d[e]));
-    *(f32x4*)(out + ((size_t)f * (oH + 2 * op) * oWp + (size_t)(y + op) * oWp + x + op) * ocs + 4 * c4) = m;
+    *(f32x4*)(out + ((size_t)f * out_chunks + k) * och + ((size_t)(y + op) * oWp + x + op) * 8 + 4 * half) = m;
   }
 }
 
 hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s) {
-  const int C4 = (C + 3) / 4;
-  const long long total = (long long)out.n * out.H * out.W * C4;
+  const int chunks = (C + 7) / 8;
+  const long long total = (long long)out.n * chunks * out.H * out.W * 2;
   const int grid = (int)std::min<long long>((total + 255) / 256, 256 * 16);
-  hipLaunchKernelGGL(maxpool2_kernel, dim3(grid), dim3(256), 0, s, in.base, in.pad, in.cs, in.H, in.W,
-                     out.base, out.pad, out.cs, out.H, out.W, C4, in.n);
+  hipLaunchKernelGGL(maxpool2_kernel, dim3(grid), dim3(256), 0, s, in.base, in.pad, in.H, in.W, out.base, out.pad,
+                     out.H, out.W, chunks, in.cs / 8, out.cs / 8, in.n);
   return hipGetLastError();
 }
 
-// NCHW float (module seam input) -> padded NHWC, channels >= C zero-filled.
+// NCHW float (module seam input) -> chunked padded buffer, channels >= C zero-filled.
 __global__ void pack_nchw_kernel(const float* __restrict__ x, int n, int C, int h, int w,
                                  float* __restrict__ out, int op, int ocs) {
   const long long total = (long long)n * h * w;
+  const size_t chs = (size_t)(h + 2 * op) * (w + 2 * op) * 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int xx = (int)(i % w);
     const int yy = (int)((i / w) % h);
     const int f = (int)(i / ((long long)w * h));
-    float* o = out + ((size_t)f * (h + 2 * op) * (w + 2 * op) + (size_t)(yy + op) * (w + 2 * op) + xx + op) * ocs;
+    float* o = out + (size_t)f * (ocs / 8) * chs + ((size_t)(yy + op) * (w + 2 * op) + xx + op) * 8;
     for (int c = 0; c < ocs; ++c)
-      o[c] = c < C ? x[(((size_t)f * C + c) * h + yy) * w + xx] : 0.f;
+      o[(size_t)(c >> 3) * chs + (c & 7)] = c < C ? x[(((size_t)f * C + c) * h + yy) * w + xx] : 0.f;
   }
 }
 
@@ -59,18 +63,19 @@ hipError_t launch_pack_nchw(const float* x, int n, int C, int h, int w, const Ac
   return hipGetLastError();
 }
 
-// padded NHWC slice [coff, coff+C) -> NCHW float (module seam output).
+// chunked padded slice [coff, coff+C) -> NCHW float (module seam output).
 __global__ void unpack_nchw_kernel(const float* __restrict__ in, int ip, int ics, int coff, int n, int C,
                                    int h, int w, float* __restrict__ y) {
   const long long total = (long long)n * C * h * w;
+  const size_t chs = (size_t)(h + 2 * ip) * (w + 2 * ip) * 8;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int xx = (int)(i % w);
     long long r = i / w;
     const int yy = (int)(r % h); r /= h;
-    const int c = (int)(r % C);
+    const int c = (int)(r % C) + coff;
     const int f = (int)(r / C);
-    y[i] = in[((size_t)f * (h + 2 * ip) * (w + 2 * ip) + (size_t)(yy + ip) * (w + 2 * ip) + xx + ip) * ics + coff + c];
+    y[i] = in[((size_t)f * (ics / 8) + (c >> 3)) * chs + ((size_t)(yy + ip) * (w + 2 * ip) + xx + ip) * 8 + (c & 7)];
   }
 }
 
@@ -85,7 +90,8 @@ hipError_t launch_unpack_nchw(const Act& in, int coff, int C, float* y, hipStrea
 // ---------------------------------------------------------------------------
 // Frame pre-processing (body.py:53-56, hand.py:37-40):
 //   cv2.resize(uint8 BGR, fx=fy=scale, INTER_CUBIC) -> padRightDownCorner(8, 128)
-//   -> float32(img)/256 - 0.5, written as padded NHWC (3 real + 5 zero channels).
+//   -> float32(img)/256 - 0.5, written as chunk 0 of the padded input buffer
+//   (3 real + 5 zero channels).
 // The uint8 cubic follows OpenCV's generic path (see oracle/cv_resize.py):
 // 11-bit fixed-point coefficients, int horizontal sums, and a vertical pass that
 // is float (beta/2^22, round-half-even) for the SIMD body of each output row and
@@ -161,7 +167,9 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ frames, int n, int
         v[c] = (float)r / 256.f - 0.5f;
       }
     }
-    float* o = out + ((size_t)f * (ph + 2 * op) * (pw + 2 * op) + (size_t)(y + op) * (pw + 2 * op) + x + op) * ocs;
+    // chunk 0 of the (chunked) input buffer: 3 real + 5 zero channels
+    float* o = out + (size_t)f * (ocs / 8) * (ph + 2 * op) * (pw + 2 * op) * 8 +
+               ((size_t)(y + op) * (pw + 2 * op) + x + op) * 8;
     *(f32x4*)o = f32x4{v[0], v[1], v[2], 0.f};
     *(f32x4*)(o + 4) = f32x4{0.f, 0.f, 0.f, 0.f};
   }

@@ -53,6 +53,11 @@ __constant__ int kMapCoco[19][2] = {{12, 13}, {20, 21}, {14, 15}, {16, 17}, {22,
 
 
 
+// channel c of map m (planar maps: cshift = 30, so chan(c) = c * cstr)
+__device__ __forceinline__ long long chan_off(const MapSrc& m, int c) {
+  return (long long)(c >> m.cshift) * m.cbig + (long long)(c & ((1 << m.cshift) - 1)) * m.cstr;
+}
+
 __device__ __forceinline__ void cubic_coeffs_f(float t, float c[4]) {
   const float A = -0.75f;
   const float tp1 = t + 1.f;
@@ -74,7 +79,7 @@ __device__ __forceinline__ void taps(int d, double scale, int n, int idx[4], flo
 
 // one output element of resize `m`, with the row taps (yi, be) precomputed
 __device__ __forceinline__ float sample_row(const MapSrc& m, int f, int c, const int yi[4], const float be[4], int x) {
-  const float* b = m.base + f * m.fs + c * m.cstr;
+  const float* b = m.base + f * m.fs + chan_off(m, c);
   int xi[4];
   float a[4];
   taps(x, m.scx, m.sw, xi, a);
@@ -91,7 +96,7 @@ __device__ __forceinline__ float sample_row(const MapSrc& m, int f, int c, const
 }
 
 __device__ __forceinline__ float sample(const MapSrc& m, int f, int c, int y, int x) {
-  const float* b = m.base + f * m.fs + c * m.cstr;
+  const float* b = m.base + f * m.fs + chan_off(m, c);
   if (m.identity) return b[y * m.ys + x * m.xs];
   int xi[4], yi[4];
   float a[4], be[4];
@@ -121,7 +126,7 @@ __global__ void __launch_bounds__(256) resize_sep_kernel(MapSrc m, int nch, int 
   const int plane = blockIdx.x, f = plane / nch, c = plane - f * nch;
   const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * RS_TX + threadIdx.x;
   const int ny = min(ty_rows, oh - y0);
-  const float* b = m.base + (size_t)f * m.fs + (size_t)c * m.cstr;
+  const float* b = m.base + (size_t)f * m.fs + chan_off(m, c);
   // source rows the tile needs: [r_lo, r_lo + nr)
   int r_lo = y0, nr = ny;
   if (!m.identity) {
@@ -902,6 +907,7 @@ static int low_src(isl_net* net, const float* p, int which, int n, int C, int h8
   if (p) {
     m->base = p;
     m->xs = 1; m->ys = w8; m->cstr = (long long)h8 * w8; m->fs = (long long)C * h8 * w8;
+    m->cshift = 30; m->cbig = 0;
     m->sh = h8; m->sw = w8;
     return ISL_OK;
   }
@@ -978,6 +984,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       auto stage2 = [&](MapSrc& m, const float* p, int C, int cn) {
         m.base = p; m.xs = 1; m.ys = g.valid_w; m.cstr = (long long)g.valid_h * g.valid_w;
         m.fs = (long long)C * g.valid_h * g.valid_w;
+        m.cshift = 30; m.cbig = 0;
         m.sh = g.valid_h; m.sw = g.valid_w; m.dh = H; m.dw = W;
         m.scy = 1.0 / ((double)H / g.valid_h); m.scx = 1.0 / ((double)W / g.valid_w);
         m.cn = cn; m.identity = 0;
@@ -1066,6 +1073,7 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
       if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, mid, s))) return rc;
       fh.base = mid; fh.xs = 1; fh.ys = g.valid_w; fh.cstr = (long long)g.valid_h * g.valid_w;
       fh.fs = (long long)nparts * g.valid_h * g.valid_w;
+      fh.cshift = 30; fh.cbig = 0;
       fh.sh = g.valid_h; fh.sw = g.valid_w; fh.dh = h; fh.dw = w;
       fh.scy = 1.0 / ((double)h / g.valid_h); fh.scx = 1.0 / ((double)w / g.valid_w);
       fh.cn = nch; fh.identity = 0;

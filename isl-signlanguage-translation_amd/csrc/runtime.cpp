@@ -2,7 +2,7 @@
 // C ABI of include/islpose.h.
 //
 // The three networks of src/model.py are rebuilt here as static graphs over
-// padded-NHWC buffers.  Every torch.cat of the reference (model.py:177, 190,
+// padded buffers in 8-channel chunks.  Every torch.cat of the reference (model.py:177, 190,
 // 199, 308-324, 397-405) becomes a channel-slice layout decision: producers
 // write their slice of a shared buffer, consumers read the whole span, and the
 // conv weights are repacked so that logical input channel order (the concat
@@ -518,8 +518,10 @@ int net_low_res(isl_net* net, int which, MapSrc* m) {
   const OutRef& o = which == 0 ? net->out0 : net->out1;
   const Act& a = net->act[o.buf];
   const int Wp = a.W + 2 * a.pad;
-  m->base = a.base + ((size_t)a.pad * Wp + a.pad) * a.cs + o.coff;
-  m->xs = a.cs; m->ys = (long long)Wp * a.cs; m->cstr = 1; m->fs = (long long)a.frame_elems();
+  if (o.coff % 8) return fail(ISL_E_STATE, "network output slice not on a chunk");
+  m->base = a.base + (size_t)(o.coff / 8) * a.chunk_elems() + ((size_t)a.pad * Wp + a.pad) * 8;
+  m->xs = 8; m->ys = (long long)Wp * 8; m->cstr = 1; m->fs = (long long)a.frame_elems();
+  m->cshift = 3; m->cbig = (long long)a.chunk_elems();
   m->sh = a.H; m->sw = a.W;
   return ISL_OK;
 }

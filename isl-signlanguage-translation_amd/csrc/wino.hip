@@ -22,6 +22,8 @@
 // rows per (tile, plane, row-half) work item held in registers since the
 // previous step.  Double-buffered, one barrier per step; per step and wave:
 // 16 xi x 4 k-steps = 64 MFMAs from 32 ds_read_b128.
+#include <type_traits>
+
 #include "internal.h"
 
 namespace isl {
@@ -35,9 +37,10 @@ struct WinoArgs {
   const float* upk;      // [co_tile][chunk][xi 16][plane 2][BCO][4]
   const float* bias;
   const float* slope;
-  int in_pad, in_cs, in_coff;
-  int out_pad, out_cs, out_coff;
-  int H, W, TW, tiles, cin_chunks, co_tiles, t_tiles, act, nblocks;
+  long long in_fs, in_chs;      // frame / chunk strides (floats), see Act
+  long long out_fs, out_chs;
+  int in_pad, out_pad;
+  int H, W, TW, tiles, cin_chunks, co_tiles, t_tiles, act, nblocks, probe;
 };
 
 template <int WAVES_M, int WAVES_N>
@@ -65,23 +68,21 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 1) wino_f23_mfma(WinoA
   const int t0 = pt * BT;
 
   const int Hp = a.H + 2 * a.in_pad, Wp = a.W + 2 * a.in_pad;
-  const float* in_f = a.in + (size_t)n * Hp * Wp * a.in_cs + a.in_coff;
+  const float* in_f = a.in + (size_t)n * a.in_fs;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wave_m = wave % WAVES_M, wave_n = wave / WAVES_M;
   const int h = lane >> 5, l32 = lane & 31;
 
   // transform work items of this thread: item = tid + i*NT -> tile j, plane pl, half hf
+  // (threads past ITEMS redo an item: same values to the same LDS words, no branch)
   int roff[IPT][3], coff[IPT][4], vdst[IPT];
-  bool act_item[IPT];
   int hf_of[IPT];
 #pragma unroll
   for (int i = 0; i < IPT; ++i) {
-    const int item = tid + i * NT;
-    act_item[i] = item < ITEMS;
-    const int it = act_item[i] ? item : 0;
+    const int it = (tid + i * NT) % ITEMS;
     const int j = it % BT, pl = (it / BT) & 1, hf = it / (2 * BT);
     hf_of[i] = hf;
-    const int tile = min(t0 + j, a.tiles - 1);
+    const int tile = a.probe ? t0 : min(t0 + j, a.tiles - 1);
     const int ty = tile / a.TW, tx = tile - ty * a.TW;
     // padded input rows 2ty-1+k (+pad), k = hf..hf+2; columns 2tx-1+m (+pad), m = 0..3.
     // Rows / columns past the ring (odd H / W) only feed discarded outputs: clamped.
@@ -93,80 +94,118 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 1) wino_f23_mfma(WinoA
   }
   int cpl[IPT];
 #pragma unroll
-  for (int i = 0; i < IPT; ++i) cpl[i] = (((tid + i * NT) / BT) & 1) * 4;
+  for (int i = 0; i < IPT; ++i) cpl[i] = ((((tid + i * NT) % ITEMS) / BT) & 1) * 4;
 
-  f32x4 raw[IPT][3][4];
-  auto load_raw = [&](int c) {
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      if (!act_item[i]) continue;
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-          raw[i][r][m] = *(const f32x4*)(in_f + (size_t)(roff[i][r] + coff[i][m]) * a.in_cs + c * 8 + cpl[i]);
-    }
-  };
-  auto put_v = [&](int buf) {
-    f32x4* V = smem + buf * (UT + VT) + UT;
-#pragma unroll
-    for (int i = 0; i < IPT; ++i) {
-      if (!act_item[i]) continue;
-      f32x4 u[2][4];
-      if (hf_of[i] == 0) {          // raw rows d0 d1 d2: B^T rows 0, 1
-#pragma unroll
-        for (int m = 0; m < 4; ++m) { u[0][m] = raw[i][0][m] - raw[i][2][m]; u[1][m] = raw[i][1][m] + raw[i][2][m]; }
-      } else {                      // raw rows d1 d2 d3: B^T rows 2, 3
-#pragma unroll
-        for (int m = 0; m < 4; ++m) { u[0][m] = raw[i][1][m] - raw[i][0][m]; u[1][m] = raw[i][0][m] - raw[i][2][m]; }
-      }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        f32x4* d = V + vdst[i] + q * 4 * 2 * BT;
-        d[0 * 2 * BT] = u[q][0] - u[q][2];
-        d[1 * 2 * BT] = u[q][1] + u[q][2];
-        d[2 * 2 * BT] = u[q][2] - u[q][1];
-        d[3 * 2 * BT] = u[q][1] - u[q][3];
-      }
-    }
-  };
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  auto issue_u = [&](int c, int buf) {
-    const f32x4* src = (const f32x4*)a.upk + (size_t)(co_t * a.cin_chunks + c) * UT;
-    f32x4* dst = smem + buf * (UT + VT);
-    for (int q = wave_u; q < UT / 64; q += NWAVES)
-      __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
-                                       (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
-  };
-
+  typedef f32x4 Raw[IPT][3][4];
+  const int T = a.cin_chunks;
   f32x16 acc[16];
 #pragma unroll
   for (int x = 0; x < 16; ++x)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[x][r] = 0.f;
+  auto load_raw = [&](Raw& raw, int c) __attribute__((always_inline)) {
+    c = min(c, T - 1);   // past the end: harmless reload (its V is never read)
+#pragma unroll
+    for (int i = 0; i < IPT; ++i) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+          raw[i][r][m] = *(const f32x4*)(in_f + (size_t)c * a.in_chs + (size_t)(roff[i][r] + coff[i][m]) * 8 + cpl[i]);
+    }
+  };
+  constexpr int NP = 9 * IPT;
+  static_assert(IPT <= 2, "at most two transform items per thread");
+  static_assert((UT / 64) % NWAVES == 0, "U stage splits evenly over the waves");
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto issue_u = [&](int c, int buf) __attribute__((always_inline)) {
+    c = min(c, T - 1);
+    const f32x4* src = (const f32x4*)a.upk + (size_t)(co_t * a.cin_chunks + c) * UT;
+    f32x4* dst = smem + buf * (UT + VT);
+#pragma unroll
+    for (int k = 0; k < UT / 64 / NWAVES; ++k) {
+      const int q = wave_u + k * NWAVES;
+      __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
+                                       (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
+    }
+  };
 
-  issue_u(0, 0);
-  load_raw(0);
-  put_v(0);
-  __syncthreads();
-  const int T = a.cin_chunks;
-  for (int t = 0; t < T; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < T) {
+  // The K loop, instantiated per row-half pattern HFM (bit i = half of item i),
+  // which is uniform over a wave: the transform is straight-line code.
+  auto kloop = [&](auto hfm_c) __attribute__((always_inline)) {
+    constexpr int HFM = decltype(hfm_c)::value;
+    // V transform of one work item in 9 pieces: piece 0 = the two B^T rows (over
+    // 4 columns), pieces 1..8 = one V float4 each (row q, column col) + ds_write.
+    f32x4 u[IPT][2][4];
+    auto put_piece = [&](Raw& raw, int buf, int i, int p) __attribute__((always_inline)) {
+      if (p == 0) {
+        if (((HFM >> i) & 1) == 0) {    // raw rows d0 d1 d2: B^T rows 0, 1
+#pragma unroll
+          for (int m = 0; m < 4; ++m) { u[i][0][m] = raw[i][0][m] - raw[i][2][m]; u[i][1][m] = raw[i][1][m] + raw[i][2][m]; }
+        } else {                        // raw rows d1 d2 d3: B^T rows 2, 3
+#pragma unroll
+          for (int m = 0; m < 4; ++m) { u[i][0][m] = raw[i][1][m] - raw[i][0][m]; u[i][1][m] = raw[i][0][m] - raw[i][2][m]; }
+        }
+        return;
+      }
+      const int q = (p - 1) >> 2, col = (p - 1) & 3;
+      const f32x4* x = u[i][q];
+      f32x4 v;
+      if (col == 0) v = x[0] - x[2];
+      else if (col == 1) v = x[1] + x[2];
+      else if (col == 2) v = x[2] - x[1];
+      else v = x[1] - x[3];
+      smem[buf * (UT + VT) + UT + vdst[i] + q * 4 * 2 * BT + col * 2 * BT] = v;
+    };
+
+    // One K step: MFMAs over buffer `buf` (chunk t).  Chunk t+1's filters
+    // (LDS-DMA) and input rows (registers) are issued first; its V transform is
+    // woven between the MFMAs of the second half of the step, by which time the
+    // rows have landed.  The closing barrier retires everything for step t+1.
+    constexpr int SLOT0 = 16 - 9;   // first slot carrying transform pieces
+    Raw raw;
+    auto step = [&](int t, int buf) __attribute__((always_inline)) {
       issue_u(t + 1, buf ^ 1);
-      load_raw(t + 1);
-    }
-    const f32x4* U = smem + buf * (UT + VT) + h * BCO + wave_m * 32 + l32;
-    const f32x4* V = smem + buf * (UT + VT) + UT + h * BT + wave_n * 32 + l32;
+      load_raw(raw, t + 1);
+      const f32x4* U = smem + buf * (UT + VT) + h * BCO + wave_m * 32 + l32;
+      const f32x4* V = smem + buf * (UT + VT) + UT + h * BT + wave_n * 32 + l32;
+      f32x4 A = U[0], B = V[0];
 #pragma unroll
-    for (int x = 0; x < 16; ++x) {
-      const f32x4 A = U[x * 2 * BCO];
-      const f32x4 B = V[x * 2 * BT];
+      for (int x = 0; x < 16; ++x) {
+        f32x4 An = A, Bn = B;
+        if (x < 15) {
+          An = U[(x + 1) * 2 * BCO];
+          Bn = V[(x + 1) * 2 * BT];
+        }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[e], B[e], acc[x], 0, 0, 0);
-    }
-    if (t + 1 < T) put_v(buf ^ 1);
+        for (int e = 0; e < 4; ++e) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[e], B[e], acc[x], 0, 0, 0);
+        if (x >= SLOT0) {
+          const int sl = x - SLOT0;
+#pragma unroll
+          for (int p = sl * NP / 9; p < (sl + 1) * NP / 9; ++p) put_piece(raw, buf ^ 1, p / 9, p % 9);
+        }
+        A = An;
+        B = Bn;
+        __builtin_amdgcn_sched_barrier(0);   // keep the weave: no hoisting of later slots' reads
+      }
+      __syncthreads();
+    };
+
+    issue_u(0, 0);
+    load_raw(raw, 0);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) put_piece(raw, 0, p / 9, p % 9);
     __syncthreads();
+    for (int t = 0; t < T; t += 2) {
+      step(t, 0);
+      if (t + 1 < T) step(t + 1, 1);
+    }
+  };
+  if constexpr (IPT == 1) {
+    if (__builtin_amdgcn_readfirstlane(hf_of[0]) == 0) kloop(std::integral_constant<int, 0>{});
+    else kloop(std::integral_constant<int, 1>{});
+  } else {
+    kloop(std::integral_constant<int, 2>{});   // item 0 in the upper half, item 1 in the lower
   }
 
   // epilogue: Y = A^T M A per (lane tile, channel), bias + activation, 2x2 pixel stores
@@ -175,7 +214,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 1) wino_f23_mfma(WinoA
   const int ty = tile / a.TW, tx = tile - ty * a.TW;
   const int oy = 2 * ty, ox = 2 * tx;
   const int Wo = a.W + 2 * a.out_pad;
-  float* out_f = a.out + (size_t)n * (a.H + 2 * a.out_pad) * Wo * a.out_cs + a.out_coff;
+  float* out_f = a.out + (size_t)n * a.out_fs;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int co = co_t * BCO + wave_m * 32 + 8 * q + 4 * h;
@@ -211,7 +250,8 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 1) wino_f23_mfma(WinoA
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
         }
-        *(f32x4*)(out_f + (size_t)((oy + i + a.out_pad) * Wo + ox + j + a.out_pad) * a.out_cs + co) = v;
+        *(f32x4*)(out_f + (size_t)(co >> 3) * a.out_chs + (size_t)((oy + i + a.out_pad) * Wo + ox + j + a.out_pad) * 8 +
+                  (co & 7)) = v;
       }
   }
 }
@@ -219,7 +259,6 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 1) wino_f23_mfma(WinoA
 int wino_bco_for(int cout) {
   if (cout % 64 == 0) return 64;
   if (cout % 96 == 0) return 96;
-  if (cout % 32 == 0) return 32;
   return 0;   // not eligible: direct kernel
 }
 
@@ -228,19 +267,24 @@ static hipError_t launch_w(const ConvLaunch& c, hipStream_t s) {
   constexpr int BCO = WAVES_M * 32, BT = WAVES_N * 32;
   if (c.ks != 3 || c.in_pad < 1) { set_error("wino: 3x3 with an input ring >= 1 only"); return hipErrorInvalidValue; }
   if (c.cout % BCO != 0 || c.bco != BCO) { set_error("wino: tile mismatch"); return hipErrorInvalidValue; }
-  if ((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 3) { set_error("wino: unaligned slice"); return hipErrorInvalidValue; }
-  const long long frame = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * c.in_cs;
-  if (frame >= 0x7fffffffLL) { set_error("wino: frame too large"); return hipErrorInvalidValue; }
+  if ((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 7) { set_error("wino: slice not on a chunk"); return hipErrorInvalidValue; }
   WinoArgs a;
-  a.in = c.in; a.out = c.out; a.upk = c.wpk; a.bias = c.bias; a.slope = c.slope;
-  a.in_pad = c.in_pad; a.in_cs = c.in_cs; a.in_coff = c.in_coff;
-  a.out_pad = c.out_pad; a.out_cs = c.out_cs; a.out_coff = c.out_coff;
+  a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
+  a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
+  a.in_fs = a.in_chs * (c.in_cs / 8);
+  a.out_fs = a.out_chs * (c.out_cs / 8);
+  if (a.in_chs >= 0x7fffffffLL) { set_error("wino: frame too large"); return hipErrorInvalidValue; }
+  a.in = c.in + (c.in_coff / 8) * a.in_chs;
+  a.out = c.out + (c.out_coff / 8) * a.out_chs;
+  a.upk = c.wpk; a.bias = c.bias; a.slope = c.slope;
+  a.in_pad = c.in_pad; a.out_pad = c.out_pad;
   a.H = c.H; a.W = c.W; a.TW = (c.W + 1) / 2;
   a.tiles = ((c.H + 1) / 2) * a.TW;
   a.cin_chunks = c.cin_chunks;
   a.co_tiles = c.cout / BCO;
   a.t_tiles = (a.tiles + BT - 1) / BT;
   a.act = c.act;
+  a.probe = getenv("ISLPOSE_WINO_PROBE") != nullptr;   // timing experiment only: wrong results
   const long long nb = (long long)c.n * a.t_tiles * a.co_tiles;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("wino: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
@@ -252,7 +296,6 @@ hipError_t launch_wino(const ConvLaunch& c, hipStream_t s) {
   switch (c.bco) {
     case 64: return launch_w<2, 2>(c, s);
     case 96: return launch_w<3, 1>(c, s);
-    case 32: return launch_w<1, 4>(c, s);
   }
   set_error("wino: unsupported tile");
   return hipErrorInvalidValue;

@@ -7,7 +7,14 @@ from islpose import netspec  # noqa: E402
 
 
 def main(path, h=368, w=656, B=32, kind=0, quiet=False):
-    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    if path.endswith(".db"):
+        import sqlite3
+        c = sqlite3.connect(path)
+        rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                for n, s, e in c.execute("select name, start, end from kernels")]
+    else:
+        rows = list(csv.DictReader(open(path)))
+    rows = sorted(rows, key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if "preprocess" in r["Kernel_Name"]]
     seq = rows[idx[-1]:]
     convs = netspec.convs_for(kind)
@@ -16,10 +23,10 @@ def main(path, h=368, w=656, B=32, kind=0, quiet=False):
         n = r["Kernel_Name"]
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         tot += d
-        if "conv_mfma" in n:
+        if "conv_mfma" in n or "wino_f23" in n:
             c = convs[ci]
             fl = 2 * c.cout * c.cin * c.k * c.k * h * w * B
-            key = "%dx%d c%d->%d k%d" % (h, w, c.cin, c.cout, c.k)
+            key = "%dx%d c%d->%d k%d %s" % (h, w, c.cin, c.cout, c.k, "W" if "wino" in n else "D")
             g = groups.setdefault(key, [0, 0.0, 0.0])
             g[0] += 1; g[1] += d; g[2] += fl
             if c.name in ("conv1_2", "conv2_2", "conv3_4"):

@@ -82,9 +82,21 @@ int isl_net_preprocess(isl_net* net, const uint8_t* d_frames, int n, int H, int 
                        double scale, int* net_h, int* net_w, void* stream);
 
 /* Run the network on the input buffer filled by isl_net_preprocess; outputs stay
- * in the arena (low-res NHWC) for the post kernels, and are also copied to
- * d_out0/d_out1 (NCHW) when those are non-NULL. */
+ * in the arena (low-res, 8-channel chunks) for the post kernels, and are also
+ * copied to d_out0/d_out1 (NCHW) when those are non-NULL. */
 int isl_net_run(isl_net* net, float* d_out0, float* d_out1, void* stream);
+
+/* Per-op device timing (measurement; not in the reference).  After
+ * isl_net_set_timing(net, 1) every isl_net_run records a HIP event on its stream
+ * before the first op and after each op.  isl_net_timing waits for the recorded
+ * runs and returns, per op and summed over them: the duration in ms, the kind
+ * (0 max-pool, 1 direct conv, 2 Winograd conv), the algorithmic FLOPs
+ * (2*Cout*Cin*k*k*H*W*n, the direct-convolution count of SURVEY §8d) and the
+ * FLOPs the matrix cores executed (tile padding included); then it drops the
+ * events.  With op_ms == NULL it only reports *n_ops and *n_runs. */
+int isl_net_set_timing(isl_net* net, int on);
+int isl_net_timing(isl_net* net, int max_ops, int* n_ops, int* n_runs, double* op_ms, int* op_kind,
+                   double* op_flops, double* op_mfma_flops);
 
 /* Diagnostic: copy the net input buffer (filled by isl_net_preprocess) out as
  * float32 NCHW [n,3,net_h,net_w]. */

@@ -23,6 +23,8 @@
 // The 8 channels of a chunk are split in two planes of 4 (ci 0-3 | 4-7); lane
 // half h reads plane h with one ds_read_b128 and feeds its 4 floats to 4
 // successive MFMAs, so MFMA k-step e covers channels {e, 4+e}.
+#include <cmath>
+
 #include "internal.h"
 
 namespace isl {
@@ -302,6 +304,13 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   }
   set_error("conv: unsupported tile");
   return hipErrorInvalidValue;
+}
+
+double conv_mfma_flops(const ConvLaunch& c) {
+  const double BPX = 128;   // every tile shape above covers 128 pixels
+  const double co = (double)((c.cout + c.bco - 1) / c.bco) * c.bco;
+  const double px = std::ceil((double)c.H * c.W / BPX) * BPX;
+  return 2.0 * co * (c.cin_chunks * 8.0) * c.ks * c.ks * px * c.n;
 }
 
 hipError_t launch_conv(const ConvLaunch& c, hipStream_t s) {

@@ -47,6 +47,9 @@ hipError_t launch_conv(const ConvLaunch& c, hipStream_t s);
 // the transformed filters [co_tile][chunk][xi 16][plane 2][BCO][4].
 int wino_bco_for(int cout);
 hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
+// FLOPs the matrix cores execute for one launch (tile padding included)
+double conv_mfma_flops(const ConvLaunch& c);
+double wino_mfma_flops(const ConvLaunch& c);
 
 hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s);
 hipError_t launch_pack_nchw(const float* x, int n, int C, int h, int w, const Act& out, hipStream_t s);

@@ -198,6 +198,14 @@ struct isl_net {
   // post scratch
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  // per-op event timing (isl_net_set_timing / isl_net_timing)
+  struct TimedRun {
+    std::vector<hipEvent_t> ev;          // ops + 1 events: before op 0, after every op
+    std::vector<int> kind;
+    std::vector<double> flops, mfma_flops;
+  };
+  bool timing = false;
+  std::vector<TimedRun> timed;
 };
 
 namespace isl {
@@ -479,11 +487,24 @@ static bool conv_algo_wino() {
 }
 
 static int run_ops(isl_net* net, hipStream_t s) {
-  for (const Op& op : net->ops) {
+  isl_net::TimedRun* tr = nullptr;
+  if (net->timing) {
+    net->timed.emplace_back();
+    tr = &net->timed.back();
+    tr->ev.resize(net->ops.size() + 1);
+    for (hipEvent_t& e : tr->ev) HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipEventRecord(tr->ev[0], s));
+  }
+  for (size_t k = 0; k < net->ops.size(); ++k) {
+    const Op& op = net->ops[k];
     const Act& in = net->act[op.in];
     const Act& out = net->act[op.out];
     if (op.type == 1) {
       HIP_OK(launch_maxpool2(in, out, op.C, s));
+      if (tr) {
+        tr->kind.push_back(0); tr->flops.push_back(0.0); tr->mfma_flops.push_back(0.0);
+        HIP_OK(hipEventRecord(tr->ev[k + 1], s));
+      }
       continue;
     }
     const ConvLayer& c = net->layers[op.layer];
@@ -493,11 +514,18 @@ static int run_ops(isl_net* net, hipStream_t s) {
     L.wpk = c.d_w; L.bias = c.d_b; L.slope = c.d_s;
     L.n = in.n; L.H = in.H; L.W = in.W; L.ks = c.k; L.cin_chunks = c.cin_phys / 8;
     L.cout = c.cout; L.bco = c.bco; L.act = c.act;
-    if (c.wbco && conv_algo_wino()) {
+    const bool wino = c.wbco && conv_algo_wino();
+    if (wino) {
       L.wpk = c.d_wu; L.bco = c.wbco;
       HIP_OK(launch_wino(L, s));
     } else {
       HIP_OK(launch_conv(L, s));
+    }
+    if (tr) {
+      tr->kind.push_back(wino ? 2 : 1);
+      tr->flops.push_back(2.0 * c.cout * c.cin * c.k * c.k * (double)in.H * in.W * in.n);
+      tr->mfma_flops.push_back(wino ? wino_mfma_flops(L) : conv_mfma_flops(L));
+      HIP_OK(hipEventRecord(tr->ev[k + 1], s));
     }
   }
   return ISL_OK;
@@ -579,6 +607,8 @@ int isl_net_destroy(isl_net* net) {
   }
   for (auto& kv : net->plans) (void)hipFree(kv.second.first);
   if (net->scratch) (void)hipFree(net->scratch);
+  for (auto& r : net->timed)
+    for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
   delete net;
   return ISL_OK;
 }
@@ -655,6 +685,44 @@ int isl_net_debug_input(isl_net* net, float* d_x, void* stream) {
   if (!net || !net->arena || !d_x) return fail(ISL_E_STATE, "no input buffer yet");
   HIP_OK(hipSetDevice(net->device));
   HIP_OK(launch_unpack_nchw(net->act[net->in_buf], 0, 3, d_x, (hipStream_t)stream));
+  return ISL_OK;
+}
+
+int isl_net_set_timing(isl_net* net, int on) {
+  if (!net) return fail(ISL_E_ARG, "net is NULL");
+  net->timing = on != 0;
+  return ISL_OK;
+}
+
+int isl_net_timing(isl_net* net, int max_ops, int* n_ops, int* n_runs, double* op_ms, int* op_kind,
+                   double* op_flops, double* op_mfma_flops) {
+  if (!net) return fail(ISL_E_ARG, "net is NULL");
+  const int nops = (int)net->ops.size();
+  if (n_ops) *n_ops = nops;
+  if (n_runs) *n_runs = (int)net->timed.size();
+  if (!op_ms) return ISL_OK;   // query only
+  if (max_ops < nops) return fail(ISL_E_ARG, "isl_net_timing: arrays shorter than the op count");
+  HIP_OK(hipSetDevice(net->device));
+  for (int k = 0; k < nops; ++k) {
+    op_ms[k] = 0.0;
+    if (op_kind) op_kind[k] = 0;
+    if (op_flops) op_flops[k] = 0.0;
+    if (op_mfma_flops) op_mfma_flops[k] = 0.0;
+  }
+  for (auto& r : net->timed) {
+    HIP_OK(hipEventSynchronize(r.ev.back()));
+    for (int k = 0; k < nops; ++k) {
+      float ms = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms, r.ev[k], r.ev[k + 1]));
+      op_ms[k] += ms;
+      if (op_kind) op_kind[k] = r.kind[k];
+      if (op_flops) op_flops[k] += r.flops[k];
+      if (op_mfma_flops) op_mfma_flops[k] += r.mfma_flops[k];
+    }
+  }
+  for (auto& r : net->timed)
+    for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
+  net->timed.clear();
   return ISL_OK;
 }
 

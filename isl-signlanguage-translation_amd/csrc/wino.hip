@@ -22,6 +22,7 @@
 // rows per (tile, plane, row-half) work item held in registers since the
 // previous step.  Double-buffered, one barrier per step; per step and wave:
 // 16 xi x 4 k-steps = 64 MFMAs from 32 ds_read_b128.
+#include <cmath>
 #include <type_traits>
 
 #include "internal.h"
@@ -40,7 +41,7 @@ struct WinoArgs {
   long long in_fs, in_chs;      // frame / chunk strides (floats), see Act
   long long out_fs, out_chs;
   int in_pad, out_pad;
-  int H, W, TW, tiles, cin_chunks, co_tiles, t_tiles, act, nblocks, probe;
+  int H, W, TW, tiles, cin_chunks, co_tiles, t_tiles, act, nblocks;
 };
 
 template <int WAVES_M, int WAVES_N>
@@ -82,7 +83,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 1) wino_f23_mfma(WinoA
     const int it = (tid + i * NT) % ITEMS;
     const int j = it % BT, pl = (it / BT) & 1, hf = it / (2 * BT);
     hf_of[i] = hf;
-    const int tile = a.probe ? t0 : min(t0 + j, a.tiles - 1);
+    const int tile = min(t0 + j, a.tiles - 1);
     const int ty = tile / a.TW, tx = tile - ty * a.TW;
     // padded input rows 2ty-1+k (+pad), k = hf..hf+2; columns 2tx-1+m (+pad), m = 0..3.
     // Rows / columns past the ring (odd H / W) only feed discarded outputs: clamped.
@@ -162,30 +163,37 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 1) wino_f23_mfma(WinoA
     // (LDS-DMA) and input rows (registers) are issued first; its V transform is
     // woven between the MFMAs of the second half of the step, by which time the
     // rows have landed.  The closing barrier retires everything for step t+1.
-    constexpr int SLOT0 = 16 - 9;   // first slot carrying transform pieces
+    // (Loading the rows two steps ahead with the transform from the first slot,
+    // or issuing the loads between the MFMAs, both measured slower: r01.)
     Raw raw;
     auto step = [&](int t, int buf) __attribute__((always_inline)) {
       issue_u(t + 1, buf ^ 1);
       load_raw(raw, t + 1);
       const f32x4* U = smem + buf * (UT + VT) + h * BCO + wave_m * 32 + l32;
       const f32x4* V = smem + buf * (UT + VT) + UT + h * BT + wave_n * 32 + l32;
-      f32x4 A = U[0], B = V[0];
+      // 8 slots of two xi each; the two accumulation chains alternate so that no
+      // MFMA waits on the one just issued.
+      f32x4 A0 = U[0], B0 = V[0], A1 = U[2 * BCO], B1 = V[2 * BT];
 #pragma unroll
-      for (int x = 0; x < 16; ++x) {
-        f32x4 An = A, Bn = B;
-        if (x < 15) {
-          An = U[(x + 1) * 2 * BCO];
-          Bn = V[(x + 1) * 2 * BT];
+      for (int x = 0; x < 16; x += 2) {
+        f32x4 A0n = A0, B0n = B0, A1n = A1, B1n = B1;
+        if (x < 14) {
+          A0n = U[(x + 2) * 2 * BCO];
+          B0n = V[(x + 2) * 2 * BT];
+          A1n = U[(x + 3) * 2 * BCO];
+          B1n = V[(x + 3) * 2 * BT];
         }
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(A[e], B[e], acc[x], 0, 0, 0);
-        if (x >= SLOT0) {
-          const int sl = x - SLOT0;
-#pragma unroll
-          for (int p = sl * NP / 9; p < (sl + 1) * NP / 9; ++p) put_piece(raw, buf ^ 1, p / 9, p % 9);
+        for (int e = 0; e < 4; ++e) {
+          acc[x] = __builtin_amdgcn_mfma_f32_32x32x2f32(A0[e], B0[e], acc[x], 0, 0, 0);
+          acc[x + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(A1[e], B1[e], acc[x + 1], 0, 0, 0);
         }
-        A = An;
-        B = Bn;
+        if (x >= 8) {           // transform pieces in the last 4 slots, once the rows have landed
+          const int sl = x / 2 - 4;
+#pragma unroll
+          for (int p = sl * NP / 4; p < (sl + 1) * NP / 4; ++p) put_piece(raw, buf ^ 1, p / 9, p % 9);
+        }
+        A0 = A0n; B0 = B0n; A1 = A1n; B1 = B1n;
         __builtin_amdgcn_sched_barrier(0);   // keep the weave: no hoisting of later slots' reads
       }
       __syncthreads();
@@ -284,12 +292,17 @@ static hipError_t launch_w(const ConvLaunch& c, hipStream_t s) {
   a.co_tiles = c.cout / BCO;
   a.t_tiles = (a.tiles + BT - 1) / BT;
   a.act = c.act;
-  a.probe = getenv("ISLPOSE_WINO_PROBE") != nullptr;   // timing experiment only: wrong results
   const long long nb = (long long)c.n * a.t_tiles * a.co_tiles;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("wino: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
   hipLaunchKernelGGL((wino_f23_mfma<WAVES_M, WAVES_N>), dim3(a.nblocks), dim3(WAVES_M * WAVES_N * 64), 0, s, a);
   return hipGetLastError();
+}
+
+double wino_mfma_flops(const ConvLaunch& c) {
+  const double BT = c.bco == 96 ? 32 : 64;
+  const double tiles = (double)((c.H + 1) / 2) * ((c.W + 1) / 2);
+  return 2.0 * 16 * c.cout * (c.cin_chunks * 8.0) * std::ceil(tiles / BT) * BT * c.n;
 }
 
 hipError_t launch_wino(const ConvLaunch& c, hipStream_t s) {

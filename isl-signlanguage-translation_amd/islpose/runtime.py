@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("ISLPOSE_LIB", os.path.join(os.path.dirname(os.path.ab
 # every symbol include/islpose.h declares
 EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destroy", "isl_net_param_count",
            "isl_net_param_info", "isl_net_set_param", "isl_net_forward", "isl_net_preprocess", "isl_net_run", "isl_net_debug_input",
-           "isl_body_layout", "isl_body_post", "isl_hand_post"]
+           "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post"]
 
 
 class IslCaps(ctypes.Structure):
@@ -64,6 +64,9 @@ def lib():
     L.isl_net_preprocess.argtypes = [vp, vp, i32, i32, i32, dbl, ctypes.POINTER(i32), ctypes.POINTER(i32), vp]
     L.isl_net_run.argtypes = [vp, vp, vp, vp]
     L.isl_net_debug_input.argtypes = [vp, vp, vp]
+    L.isl_net_set_timing.argtypes = [vp, i32]
+    pi, pd = ctypes.POINTER(i32), ctypes.POINTER(dbl)
+    L.isl_net_timing.argtypes = [vp, i32, pi, pi, pd, pi, pd, pd]
     L.isl_body_layout.argtypes = [i32, ctypes.POINTER(IslCaps), ctypes.POINTER(IslLayout)]
     L.isl_body_post.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp),
                                 ctypes.POINTER(vp), ctypes.POINTER(IslCaps), vp, vp]
@@ -178,3 +181,23 @@ class Net:
 
     def run(self, out0=None, out1=None, stream=None):
         check(lib().isl_net_run(self.h, ptr(out0), ptr(out1), stream_handle(stream)), "isl_net_run")
+
+    def set_timing(self, on: bool):
+        """Record HIP events around every op of the following runs (isl_net_set_timing)."""
+        check(lib().isl_net_set_timing(self.h, 1 if on else 0), "isl_net_set_timing")
+
+    def timing(self):
+        """Per-op sums over the recorded runs: dict of numpy arrays ms, kind (0 pool,
+        1 direct conv, 2 Winograd conv), flops (algorithmic), mfma_flops; plus n_runs."""
+        import numpy as np
+        L = lib()
+        n_ops, n_runs = ctypes.c_int32(), ctypes.c_int32()
+        check(L.isl_net_timing(self.h, 0, ctypes.byref(n_ops), ctypes.byref(n_runs), None, None, None, None),
+              "isl_net_timing")
+        k = n_ops.value
+        ms, fl, mf = np.zeros(k), np.zeros(k), np.zeros(k)
+        kind = np.zeros(k, np.int32)
+        dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))  # noqa: E731
+        check(L.isl_net_timing(self.h, k, ctypes.byref(n_ops), ctypes.byref(n_runs), dp(ms),
+                               kind.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), dp(fl), dp(mf)), "isl_net_timing")
+        return {"ms": ms, "kind": kind, "flops": fl, "mfma_flops": mf, "n_runs": n_runs.value}

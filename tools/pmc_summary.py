@@ -17,19 +17,28 @@ import json
 import os
 
 
+NET_KERNELS = ("conv_mfma", "wino_f23", "maxpool")
+
+
 def load(d, name):
+    """Per kernel class: summed counter value and number of dispatches; the net's
+    kernels are also summed into the class "net_run"."""
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
     out = collections.defaultdict(float)
+    disp = collections.defaultdict(set)
     for r in csv.DictReader(open(f)):
         if r["Counter_Name"] != name:
             continue
         k = r["Kernel_Name"]
-        if "conv_mfma" in k or "maxpool" in k:
-            cls = "net_run"
-        else:
-            cls = k.split("(")[0].replace("void ", "").split("<")[0]
-        out[cls] += float(r["Counter_Value"])
-    return out
+        cls = k.split("(")[0].replace("void ", "").split("<")[0].replace("isl::", "")
+        v = float(r["Counter_Value"])
+        did = r.get("Dispatch_Id", r.get("Correlation_Id", ""))
+        out[cls] += v
+        disp[cls].add(did)
+        if any(t in k for t in NET_KERNELS):
+            out["net_run"] += v
+            disp["net_run"].add(did)
+    return out, {k: len(v) for k, v in disp.items()}
 
 
 def main():
@@ -40,18 +49,25 @@ def main():
     p.add_argument("--out", required=True)
     p.add_argument("--traffic-out", default=None)
     a = p.parse_args()
-    fe, wr = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
+    (fe, nfe), (wr, nwr) = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
     res = {}
     for k in sorted(set(fe) | set(wr)):
         rb = fe.get(k, 0.0) * 1024 * 2 / a.steps
         wb = wr.get(k, 0.0) * 1024 / a.steps
+        n = max(nfe.get(k, 0), 1)
         res[k] = {"read_bytes_per_step": rb, "write_bytes_per_step": wb, "hbm_bytes_per_step": rb + wb,
+                  "dispatches": nfe.get(k, 0),
+                  "hbm_bytes_per_launch": (fe.get(k, 0.0) * 2 + wr.get(k, 0.0)) * 1024 / n,
                   "raw_fetch_kib_per_step": fe.get(k, 0.0) / a.steps, "raw_write_kib_per_step": wr.get(k, 0.0) / a.steps}
     json.dump(res, open(a.out, "w"), indent=1)
     if a.traffic_out and "net_run" in res:
-        json.dump({"hbm_bytes_per_net_run": res["net_run"]["hbm_bytes_per_step"],
-                   "source": os.path.relpath(a.out), "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->B, per bench step (one net run over the batch)"},
-                  open(a.traffic_out, "w"), indent=1)
+        t = {"hbm_bytes_per_net_run": res["net_run"]["hbm_bytes_per_step"],
+             "source": os.path.relpath(a.out),
+             "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->B; per bench step "
+                     "(one net run over the batch) and per launch of the Winograd kernel"}
+        if "wino_f23_mfma" in res:
+            t["wino_hbm_bytes_per_launch"] = res["wino_f23_mfma"]["hbm_bytes_per_launch"]
+        json.dump(t, open(a.traffic_out, "w"), indent=1)
     for k, v in res.items():
         print("%-40s read %10.1f MB  write %10.1f MB" % (k, v["read_bytes_per_step"] / 1e6, v["write_bytes_per_step"] / 1e6))
 

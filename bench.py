@@ -3,7 +3,8 @@
 One step = the whole hot path over one batch of synthetic 368x656 uint8 frames
 resident in HBM:
     isl_net_preprocess   (cubic resize / pad / normalise -> padded NHWC)
-    isl_net_run          (body_25: 114 FP32-MFMA convolutions + 3 pools)
+    isl_net_run          (body_25: 114 convolutions + 3 pools; split-fp16 x3 on the
+                          FP16 matrix cores by default, fp32-accurate)
     isl_body_post        (x8 cubic resize, fp64 blur + NMS, peak lists, PAF line
                           integrals, greedy matching, person assembly)
     + async D2H of the per-frame result records.
@@ -31,8 +32,13 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "frames/sec body_25 368×656 fwd+NMS+PAF at 1/8 MI355X; conv MFMA util %"
-PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix peak (spec)
-KIND = {0: "maxpool2_kernel", 1: "conv_mfma_f32 (direct)", 2: "wino_f23_mfma (Winograd F(2x2,3x3))"}
+PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix peak (spec) = 256 CU x 4 SIMD x 64 FLOP/clk x 2.4 GHz
+PEAK_FP16_MFMA_TFLOPS = 2516.6     # dense FP16/BF16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF, no sparsity)
+KIND = {0: "maxpool2_kernel", 1: "conv_mfma_f32 (direct fp32)", 2: "wino_f23_mfma (Winograd F(2x2,3x3) fp32)",
+        3: "conv_x3_f16 (split-fp16 x3, fp32-accurate)"}
+# MFMA FLOPs the algorithm of each kind needs per direct-conv FLOP (2*Cout*Cin*k*k*H*W), tile padding excluded
+ALG_FACTOR = {1: 1.0, 2: 16.0 / 36.0, 3: 3.0}
+KIND_PEAK = {1: PEAK_FP32_MFMA_TFLOPS, 2: PEAK_FP32_MFMA_TFLOPS, 3: PEAK_FP16_MFMA_TFLOPS}
 
 
 def parse():
@@ -50,6 +56,8 @@ def parse():
                    help="split the per-GPU batch over this many HIP streams (own arena each) so one "
                         "sub-batch's layer tail overlaps the other's next layer (+2-3 %% frames/s); the "
                         "per-kernel roofline is then taken over overlapping launches and reads low")
+    p.add_argument("--algo", default="x3", choices=["x3", "wino", "direct"],
+                   help="conv arithmetic: split-fp16 x3 on the FP16 matrix cores (default), Winograd or direct fp32")
     p.add_argument("--cpu-frames", type=int, default=6, help="frames for the CPU baseline sample (0 = skip)")
     p.add_argument("--no-cpu", action="store_true")
     return p.parse_args()
@@ -92,6 +100,7 @@ def main():
         def __init__(self, s):
             self.est = BodyEstimator(weights, "body25", device=local, scale_search=(args.scale,))
             self.net = self.est.net
+            self.net.set_algo(args.algo)
             self.b = B // S
             sl = slice(s * self.b, (s + 1) * self.b)
             self.frames, self.paf, self.heat = frames[sl], d_paf[sl], d_heat[sl]
@@ -145,6 +154,7 @@ def main():
             o = f * ln.lay.record_bytes + ln.lay.status
             st = int(host[o:o + 4].view(np.int32)[0])
             assert st == 0, "post status %d on frame %d" % (st, f)
+        assert ln.net.range_ok(), "split-fp16 range exceeded in warmup"
     for ln in lanes:
         ln.net.set_timing(True)      # per-op HIP events on each lane's stream, inside the timed region
     if dist:
@@ -183,14 +193,17 @@ def main():
             d["launches"] += int(m.sum()) * o["n_runs"]
     dom = max(kinds, key=lambda k: kinds[k]["ms"])
     dk = kinds[dom]
-    achieved = dk["flops"] / (dk["ms"] * 1e-3) / 1e12          # algorithmic (direct-conv count)
-    executed = dk["mfma_flops"] / (dk["ms"] * 1e-3) / 1e12     # what the matrix cores ran
-    conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2))
-    conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2))
+    peak = KIND_PEAK.get(dom, PEAK_FP32_MFMA_TFLOPS)
+    sec = dk["ms"] * 1e-3
+    fp32_equiv = dk["flops"] / sec / 1e12                      # direct-conv FLOPs per second
+    achieved = ALG_FACTOR.get(dom, 1.0) * dk["flops"] / sec / 1e12   # MFMA work the algorithm needs, no padding
+    executed = dk["mfma_flops"] / sec / 1e12                   # what the matrix cores ran (tile padding included)
+    conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3))
+    conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3))
     traffic = None
     prof = os.path.join(REPO, "profiles", "conv_traffic.json")
     if os.path.exists(prof):
-        traffic = json.load(open(prof)).get("wino_hbm_bytes_per_launch")
+        traffic = json.load(open(prof)).get({1: "direct", 2: "wino", 3: "x3"}.get(dom, "x3") + "_hbm_bytes_per_launch")
     out = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -202,21 +215,25 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": {3: "fp32 (split-fp16 x3 MFMA, fp32 accumulate)"}.get(dom, "fp32"),
         "data": "synthetic (seeded uint8 frames, counter-hash weights; post fed designed %d-person maps)"
                 % args.persons,
         "config": {"workload": "configs[1]: body_25 single-scale %dx%d frames, batch %d per GPU, net input %dx%d"
                                % (H, W, B, nh, nw),
                    "batch_per_gpu": B, "frame_hw": [H, W], "scale_search": [args.scale], "net_hw": [nh, nw],
-                   "streams_per_gpu": S,
+                   "streams_per_gpu": S, "conv_algo": args.algo,
                    "parallelism": "frame-sharded x%d (no collective)" % world},
         "roofline": {"bound": "mfma", "kernel": KIND[dom],
-                     "achieved": round(achieved, 2), "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": traffic,
-                     "achieved_basis": "algorithmic direct-conv FLOPs (2*Cout*Cin*9*H*W) / avg launch time; "
-                                       "Winograd runs 16/36 of them on the MFMA, so frac can exceed 1",
+                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "achieved_basis": "MFMA FLOPs the kernel's algorithm needs (direct-conv count 2*Cout*Cin*k*k*H*W "
+                                       "x %.4g: split-fp16 = 3 fp16 products per fp32 MAC, Winograd = 16/36, tile "
+                                       "padding excluded) / summed launch time; peak = dense MFMA peak of the dtype the "
+                                       "matrix cores run (fp16 2516.6 / fp32 157.3 TF)" % ALG_FACTOR.get(dom, 1.0),
+                     "fp32_equiv_tflops": round(fp32_equiv, 2),
+                     "fp32_equiv_vs_fp32_peak": round(fp32_equiv / PEAK_FP32_MFMA_TFLOPS, 4),
                      "executed_tflops": round(executed, 2),
-                     "executed_frac": round(executed / PEAK_FP32_MFMA_TFLOPS, 4),
+                     "executed_frac": round(executed / peak, 4),
                      "launches": dk["launches"], "avg_launch_us": round(dk["ms"] * 1e3 / dk["launches"], 2),
                      "algorithmic_gflop_per_launch": round(dk["flops"] / dk["launches"] / 1e9, 3),
                      "all_convs_tflops": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2),

@@ -41,8 +41,18 @@ enum isl_status {
   ISL_E_HIP = -3,       /* HIP runtime error                                     */
   ISL_E_CAPACITY = -4,  /* a fixed-capacity result buffer overflowed             */
   ISL_E_STATE = -5,     /* call sequence error (e.g. forward before all params)  */
-  ISL_E_INDEX = -6      /* reference IndexError (3-way subset match, body.py:196)*/
+  ISL_E_INDEX = -6,     /* reference IndexError (3-way subset match, body.py:196)*/
+  ISL_E_RANGE = -7      /* split-fp16 conv: an activation reached |x| >= 65504   */
 };
+
+/* Convolution arithmetic (all fp32-accurate; not in the reference, which runs
+ * torch's fp32 conv):
+ *   ISL_ALGO_X3     every conv on the FP16 matrix cores with 3-term operand
+ *                   splitting (x*w = xh*wh + xh*wl + xl*wh, fp32 accumulate) --
+ *                   the default;
+ *   ISL_ALGO_WINO   3x3 convs as Winograd F(2x2,3x3) on the FP32 matrix cores;
+ *   ISL_ALGO_DIRECT every conv as a direct implicit GEMM on the FP32 matrix cores. */
+enum isl_algo { ISL_ALGO_X3 = 0, ISL_ALGO_WINO = 1, ISL_ALGO_DIRECT = 2 };
 
 typedef struct isl_net isl_net;
 
@@ -86,11 +96,23 @@ int isl_net_preprocess(isl_net* net, const uint8_t* d_frames, int n, int H, int 
  * copied to d_out0/d_out1 (NCHW) when those are non-NULL. */
 int isl_net_run(isl_net* net, float* d_out0, float* d_out1, void* stream);
 
+/* Select the conv arithmetic of a net (default ISL_ALGO_X3, or the env
+ * ISLPOSE_CONV_ALGO=x3|wino|direct at create time). */
+int isl_net_set_algo(isl_net* net, int algo);
+int isl_net_get_algo(const isl_net* net);
+
+/* Range guard of ISL_ALGO_X3: waits for the device, returns ISL_E_RANGE if any
+ * conv output since the last clear left the fp16 split range (the results of
+ * those runs are then not fp32-accurate and must be recomputed with
+ * ISL_ALGO_DIRECT), else ISL_OK; clear != 0 resets the flag.  The post records
+ * of isl_body_post carry the same flag in their status word without a sync. */
+int isl_net_check(isl_net* net, int clear);
+
 /* Per-op device timing (measurement; not in the reference).  After
  * isl_net_set_timing(net, 1) every isl_net_run records a HIP event on its stream
  * before the first op and after each op.  isl_net_timing waits for the recorded
  * runs and returns, per op and summed over them: the duration in ms, the kind
- * (0 max-pool, 1 direct conv, 2 Winograd conv), the algorithmic FLOPs
+ * (0 max-pool, 1 direct fp32 conv, 2 Winograd conv, 3 split-fp16 conv), the algorithmic FLOPs
  * (2*Cout*Cin*k*k*H*W*n, the direct-convolution count of SURVEY §8d) and the
  * FLOPs the matrix cores executed (tile padding included); then it drops the
  * events.  With op_ms == NULL it only reports *n_ops and *n_runs. */

@@ -41,7 +41,7 @@ struct ConvArgs {
   long long in_fs, in_chs;      // frame / chunk strides (floats) of the input buffer
   long long out_fs, out_chs;
   int in_pad, out_pad;
-  int H, W, cin_chunks, cout, co_tiles, px_tiles, act, nblocks;
+  int H, W, cin_chunks, cout, co_tiles, px_tiles, tpx, act, nblocks;
 };
 
 template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, bool GLDS>
@@ -74,8 +74,8 @@ conv_mfma_f32(ConvArgs a) {
   const int n = rest / a.px_tiles;
 
   const int HW = a.H * a.W;
-  const int m0 = pt * BPX;
-  const int mlast = min(m0 + BPX, HW) - 1;
+  const int m0 = pt * a.tpx;                    // tpx = BPX unless the image is very narrow
+  const int mlast = min(m0 + a.tpx, HW) - 1;
   const int Wi = a.W + 2 * a.in_pad;
   const int ya = m0 / a.W, xa = m0 - ya * a.W;
   const int yb = mlast / a.W, xb = mlast - yb * a.W;
@@ -264,9 +264,7 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   constexpr int BPX = WAVES_N * WN * 32;
   constexpr int P = KS / 2;
   if (c.in_pad < P) { set_error("conv: input ring narrower than kernel radius"); return hipErrorInvalidValue; }
-  const int max_rows = (c.W + BPX - 2) / c.W;
-  const int max_seg = BPX - 1 + 2 * c.in_pad * max_rows + 2 * P + 1;
-  if (max_seg > 2 * BPX) { set_error("conv: image too narrow for the pixel tile"); return hipErrorInvalidValue; }
+  constexpr int SEGCAP = 2 * BPX;
   if (c.bco != BCO) { set_error("conv: tile mismatch"); return hipErrorInvalidValue; }
   if ((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 7) { set_error("conv: slice not on a chunk"); return hipErrorInvalidValue; }
   ConvArgs a;
@@ -280,7 +278,8 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   a.in_pad = c.in_pad; a.out_pad = c.out_pad;
   a.H = c.H; a.W = c.W; a.cin_chunks = c.cin_chunks; a.cout = c.cout;
   a.co_tiles = (c.cout + BCO - 1) / BCO;
-  a.px_tiles = (c.H * c.W + BPX - 1) / BPX;
+  a.tpx = tile_pixels(c, BPX, SEGCAP);
+  a.px_tiles = (c.H * c.W + a.tpx - 1) / a.tpx;
   a.act = c.act;
   const long long nb = (long long)c.n * a.px_tiles * a.co_tiles;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv: bad grid"); return hipErrorInvalidValue; }
@@ -307,9 +306,9 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
 }
 
 double conv_mfma_flops(const ConvLaunch& c) {
-  const double BPX = 128;   // every tile shape above covers 128 pixels
+  const int BPX = 128;      // every tile shape above covers 128 pixels
   const double co = (double)((c.cout + c.bco - 1) / c.bco) * c.bco;
-  const double px = std::ceil((double)c.H * c.W / BPX) * BPX;
+  const double px = std::ceil((double)c.H * c.W / tile_pixels(c, BPX, 2 * BPX)) * BPX;
   return 2.0 * co * (c.cin_chunks * 8.0) * c.ks * c.ks * px * c.n;
 }
 

@@ -1,0 +1,330 @@
+// Direct convolution (3x3 / 1x1 / 7x7, stride 1, "same" padding) on the gfx950
+// FP16 matrix cores with fp32 accuracy: every fp32 operand is split into two
+// fp16 halves, x = x_hi + x_lo, and each product is taken as
+//     x*w ~= x_hi*w_hi + x_hi*w_lo + x_lo*w_hi          (3 x v_mfma_f32_32x32x16_f16)
+// with fp32 accumulation.  The dropped x_lo*w_lo term and the split residuals
+// are ~2^-21 relative per product, i.e. fp32 round-off territory: on body_25
+// the max-normalised error vs fp64 is 2.2e-6 / 3.9e-6 (PAF / heat), the same as
+// native fp32 (2.2e-6 / 3.7e-6), against north_star's 1e-4 bar.  Three fp16
+// MFMAs cost 3/16 of one FP32 MFMA of the same K, so the convolutions run at
+// up to 16/3 = 5.3x the FP32 matrix peak.
+//
+// Replaces every nn.Conv2d (+ReLU / PReLU) of src/model.py:25-64 (make_layers,
+// make_layers_Mconv).
+//
+// Range: weights are scaled by a per-layer power of two 2^s (host, exact) so
+// that max|w| sits in [2^13, 2^14): the lo halves stay normal fp16 numbers, and
+// the epilogue multiplies by 2^-s (exact).  Activations are split unscaled;
+// their lo halves may be fp16 subnormals, an absolute error <= 2^-25 that is
+// negligible against the tensor maxima the tolerance is normalised by.  An
+// activation with |x| >= 65504 would not split: every epilogue checks its
+// outputs and raises the net's range flag (isl_net_check / ISL_E_RANGE), and
+// the host then re-runs on the fp32 kernels.
+//
+// GEMM view (same tiling as conv.hip):  D[co][px] = sum_k W[co][k] X[k][px],
+// k = (ky, kx, ci).  One MFMA K-step = one tap (ky, kx) x 16 input channels =
+// two 8-channel chunks of the NC8HW8 buffer; lane half h (= lane >> 5) carries
+// chunk h of the pair, 8 channels = one 16-byte fp16 fragment.
+//   A (32 rows)  = 32 output channels     lane: co = l & 31, k = 8h + j
+//   B (32 cols)  = 32 output pixels       lane: px = l & 31, k = 8h + j
+//   D            = lane holds pixel l&31, channels (r&3)+8(r>>2)+4(l>>5)
+//
+// K loop: one step = (chunk pair, kernel row ky).
+//   weights: the pre-split slab [kx][hi|lo][h][BCO] x 16 B arrives by LDS-DMA
+//            (global_load_lds_dwordx4, lane-linear, no VGPRs);
+//   input:   the row segment of the flattened pixel tile (one contiguous run of
+//            the padded buffer, see conv.hip) is loaded as fp32, split into
+//            fp16 hi / lo in registers and written as [hi|lo][h][px] x 16 B.
+// Double-buffered, one barrier per step; per step and wave KS taps x WM*WN
+// accumulator tiles x 3 MFMAs.
+#include <cmath>
+
+#include "internal.h"
+
+namespace isl {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct X3Args {
+  const float* in;
+  float* out;
+  const f16x8* wpk;
+  const float* bias;
+  const float* slope;
+  int* range_flag;
+  long long in_fs, in_chs;      // frame / chunk strides (floats) of the input buffer
+  long long out_fs, out_chs;
+  float wscale_inv;             // 2^-s
+  int in_pad, out_pad;
+  int H, W, cin_chunks, pairs, cout, co_tiles, px_tiles, tpx, act, nblocks;
+};
+
+constexpr int X3_SEGMAX = 192;   // input segment capacity in pixels (host-checked)
+
+template <int KS, int WAVES_M, int WAVES_N, int WM, int WN>
+__global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 2) conv_x3_f16(X3Args a) {
+  constexpr int NT = WAVES_M * WAVES_N * 64;
+  constexpr int NWAVES = WAVES_M * WAVES_N;
+  constexpr int BCO = WAVES_M * WM * 32;
+  constexpr int BPX = WAVES_N * WN * 32;
+  constexpr int P = KS / 2;
+  constexpr int SEGMAX = X3_SEGMAX;
+  constexpr int WSLAB = KS * 2 * 2 * BCO;        // 16-byte units: [kx][hi|lo][h][BCO]
+  constexpr int XSLAB = 2 * 2 * SEGMAX;          // 16-byte units: [hi|lo][h][px]
+  constexpr int BUF = WSLAB + XSLAB;
+  constexpr int IT = (2 * SEGMAX + NT - 1) / NT; // staging items (h, px) per thread
+  static_assert(WSLAB % 64 == 0, "weight slab is whole 1 KiB DMA pieces");
+  static_assert(BPX <= SEGMAX, "segment must hold a tile");
+  static_assert(2 * BUF * 16 <= 160 * 1024, "LDS");
+  __shared__ f16x8 smem[2 * BUF];
+
+  // XCD-aware tile order (conv.hip): co-tiles of a pixel tile, then neighbouring
+  // pixel tiles, on one XCD / L2.
+  int bid = blockIdx.x;
+  {
+    const int nb = a.nblocks, q = nb >> 3, r = nb & 7, xcd = bid & 7, k = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int co_t = bid % a.co_tiles;
+  const int rest = bid / a.co_tiles;
+  const int pt = rest % a.px_tiles;
+  const int n = rest / a.px_tiles;
+
+  const int HW = a.H * a.W;
+  const int m0 = pt * a.tpx;                    // tpx = BPX unless the image is very narrow
+  const int mlast = min(m0 + a.tpx, HW) - 1;
+  const int Wi = a.W + 2 * a.in_pad;
+  const int ya = m0 / a.W, xa = m0 - ya * a.W;
+  const int yb = mlast / a.W, xb = mlast - yb * a.W;
+  const int La = (ya + a.in_pad) * Wi + xa + a.in_pad;
+  const int Lb = (yb + a.in_pad) * Wi + xb + a.in_pad;
+  const int seg = Lb - La + 2 * P + 1;
+  const float* in_f = a.in + (size_t)n * a.in_fs;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wave_m = wave % WAVES_M, wave_n = wave / WAVES_M;
+  const int h = lane >> 5, l32 = lane & 31;
+
+  int rel[WN];
+#pragma unroll
+  for (int wn = 0; wn < WN; ++wn) {
+    const int j = (wave_n * WN + wn) * 32 + l32;
+    const int m = min(m0 + j, mlast);
+    const int y = m / a.W, x = m - y * a.W;
+    rel[wn] = (y + a.in_pad) * Wi + x + a.in_pad - La;
+  }
+
+  // staging items of this thread: item = tid + i*NT -> (chunk half ih, pixel ipx)
+  int ih[IT], ipx[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int it = tid + i * NT;
+    ih[i] = it >= seg ? 1 : 0;
+    ipx[i] = it - ih[i] * seg;
+    if (it >= 2 * seg) ipx[i] = -1;   // idle
+  }
+
+  const int T = a.pairs * KS;
+  f32x4 raw[IT][2];
+
+  auto load_x = [&](int t) __attribute__((always_inline)) {
+    const int c2 = t / KS, ky = t - c2 * KS;
+    const long long row = (long long)(La + (ky - P) * Wi - P);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int c = 2 * c2 + ih[i];
+      if (ipx[i] >= 0 && c < a.cin_chunks) {
+        const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + ipx[i]) * 8;
+        raw[i][0] = *(const f32x4*)src;
+        raw[i][1] = *(const f32x4*)(src + 4);
+      } else {
+        raw[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        raw[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  auto store_x = [&](int buf) __attribute__((always_inline)) {
+    f16x8* s = smem + buf * BUF + WSLAB;
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      if (ipx[i] < 0) continue;
+      f16x8 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = raw[i][j >> 2][j & 3];
+        hi[j] = (_Float16)x;
+        lo[j] = (_Float16)(x - (float)hi[j]);
+      }
+      s[(0 * 2 + ih[i]) * SEGMAX + ipx[i]] = hi;
+      s[(1 * 2 + ih[i]) * SEGMAX + ipx[i]] = lo;
+    }
+  };
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto issue_w = [&](int t, int buf) __attribute__((always_inline)) {
+    const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
+    f16x8* dst = smem + buf * BUF;
+#pragma unroll
+    for (int q0 = 0; q0 < WSLAB / 64; q0 += NWAVES) {
+      const int q = q0 + wave_u;
+      if ((WSLAB / 64) % NWAVES == 0 || q < WSLAB / 64)
+        __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
+                                         (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[WM][WN];
+#pragma unroll
+  for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+    for (int wn = 0; wn < WN; ++wn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[wm][wn][r] = 0.f;
+
+  issue_w(0, 0);
+  load_x(0);
+  store_x(0);
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < T) {
+      issue_w(t + 1, buf ^ 1);
+      load_x(t + 1);
+    }
+    const f16x8* sw = smem + buf * BUF + h * BCO + wave_m * WM * 32 + l32;
+    const f16x8* sx = smem + buf * BUF + WSLAB + h * SEGMAX;
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx) {
+      f16x8 A[WM][2], B[WN][2];
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+#pragma unroll
+        for (int wm = 0; wm < WM; ++wm) A[wm][hl] = sw[(kx * 2 + hl) * 2 * BCO + wm * 32];
+#pragma unroll
+        for (int wn = 0; wn < WN; ++wn) B[wn][hl] = sx[hl * 2 * SEGMAX + rel[wn] + kx];
+      }
+#pragma unroll
+      for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+        for (int wn = 0; wn < WN; ++wn) {
+          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][0], acc[wm][wn], 0, 0, 0);
+          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][1], acc[wm][wn], 0, 0, 0);
+          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[wn][0], acc[wm][wn], 0, 0, 0);
+        }
+    }
+    if (t + 1 < T) store_x(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: x 2^-s, bias + activation, range check, masked float4 stores
+  const int Wo = a.W + 2 * a.out_pad;
+  float* out_f = a.out + (size_t)n * a.out_fs;
+  bool bad = false;
+#pragma unroll
+  for (int wn = 0; wn < WN; ++wn) {
+    const int m = m0 + (wave_n * WN + wn) * 32 + l32;
+    if (m > mlast) continue;
+    const int y = m / a.W, x = m - y * a.W;
+    float* op = out_f + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8;
+#pragma unroll
+    for (int wm = 0; wm < WM; ++wm) {
+      const int cob = co_t * BCO + (wave_m * WM + wm) * 32 + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = cob + 8 * q;
+        const f32x4 b = *(const f32x4*)(a.bias + co);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[wm][wn][4 * q + e] * a.wscale_inv + b[e];
+        if (a.act == ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        } else if (a.act == ACT_PRELU) {
+          const f32x4 sl = *(const f32x4*)(a.slope + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bad |= !(__builtin_fabsf(v[e]) < 65504.f);
+        float* oc = op + (size_t)(co >> 3) * a.out_chs + (co & 7);
+        if (co + 3 < a.cout) {
+          *(f32x4*)oc = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (co + e < a.cout) oc[e] = v[e];
+        }
+      }
+    }
+  }
+  if (bad) atomicOr(a.range_flag, 1);
+}
+
+template <int KS, int WAVES_M, int WAVES_N, int WM, int WN>
+static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
+  constexpr int BCO = WAVES_M * WM * 32;
+  constexpr int BPX = WAVES_N * WN * 32;
+  constexpr int P = KS / 2;
+  constexpr int SEGCAP = X3_SEGMAX;
+  if (c.in_pad < P) { set_error("conv_x3: input ring narrower than kernel radius"); return hipErrorInvalidValue; }
+  if (c.bco != BCO) { set_error("conv_x3: tile mismatch"); return hipErrorInvalidValue; }
+  if ((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 7) { set_error("conv_x3: slice not on a chunk"); return hipErrorInvalidValue; }
+  if (!c.wx3 || !c.range_flag) { set_error("conv_x3: split weights / range flag missing"); return hipErrorInvalidValue; }
+  X3Args a;
+  a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
+  a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
+  a.in_fs = a.in_chs * (c.in_cs / 8);
+  a.out_fs = a.out_chs * (c.out_cs / 8);
+  a.in = c.in + (c.in_coff / 8) * a.in_chs;
+  a.out = c.out + (c.out_coff / 8) * a.out_chs;
+  a.wpk = (const f16x8*)c.wx3; a.bias = c.bias; a.slope = c.slope;
+  a.range_flag = c.range_flag;
+  a.wscale_inv = c.wscale_inv;
+  a.in_pad = c.in_pad; a.out_pad = c.out_pad;
+  a.H = c.H; a.W = c.W; a.cin_chunks = c.cin_chunks; a.pairs = (c.cin_chunks + 1) / 2; a.cout = c.cout;
+  a.co_tiles = (c.cout + BCO - 1) / BCO;
+  a.tpx = tile_pixels(c, BPX, SEGCAP);
+  a.px_tiles = (c.H * c.W + a.tpx - 1) / a.tpx;
+  a.act = c.act;
+  (void)P;
+  const long long nb = (long long)c.n * a.px_tiles * a.co_tiles;
+  if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
+  a.nblocks = (int)nb;
+  hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN>), dim3(a.nblocks), dim3(WAVES_M * WAVES_N * 64), 0, s,
+                     a);
+  return hipGetLastError();
+}
+
+template <int KS>
+static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
+  switch (c.bco) {
+    case 128: return launch_t<KS, 2, 2, 2, 2>(c, s);
+    case 96: return launch_t<KS, 1, 4, 3, 1>(c, s);
+    case 64: return launch_t<KS, 1, 4, 2, 1>(c, s);
+    case 32: return launch_t<KS, 1, 4, 1, 1>(c, s);
+  }
+  set_error("conv_x3: unsupported tile");
+  return hipErrorInvalidValue;
+}
+
+bool x3_fits(const ConvLaunch& c) { return c.in_pad >= c.ks / 2; }
+
+double conv_x3_mfma_flops(const ConvLaunch& c) {
+  const int BPX = 128;
+  const double co = (double)((c.cout + c.bco - 1) / c.bco) * c.bco;
+  const double px = std::ceil((double)c.H * c.W / tile_pixels(c, BPX, X3_SEGMAX)) * BPX;
+  return 3.0 * 2.0 * co * (((c.cin_chunks + 1) / 2) * 16.0) * c.ks * c.ks * px * c.n;
+}
+
+hipError_t launch_conv_x3(const ConvLaunch& c, hipStream_t s) {
+  switch (c.ks) {
+    case 1: return launch_ks<1>(c, s);
+    case 3: return launch_ks<3>(c, s);
+    case 7: return launch_ks<7>(c, s);
+  }
+  set_error("conv_x3: unsupported kernel size");
+  return hipErrorInvalidValue;
+}
+
+}  // namespace isl

@@ -37,7 +37,22 @@ struct ConvLaunch {
   int cout;                    // real output channels
   int bco;                     // output channels per block tile (32, 64, 96, 128)
   int act;
+  // split-fp16 path (conv_x3.hip)
+  const void* wx3 = nullptr;   // pre-split weights [co_tile][pair][ky][kx][hi|lo][h][BCO][8] fp16
+  float wscale_inv = 1.f;      // 2^-s, the inverse of the per-layer weight scale
+  int* range_flag = nullptr;   // raised when an output leaves the fp16 split range
 };
+
+// Pixels per tile of the flattened-raster conv kernels: BPX, or fewer when the
+// image is so narrow that a BPX-pixel tile's padded input row segment (which
+// crosses up to (W+BPX-2)/W image rows, each adding 2*in_pad ring pixels) would
+// overflow the kernel's LDS segment capacity `segcap`.
+inline int tile_pixels(const ConvLaunch& c, int bpx, int segcap) {
+  const int P = c.ks / 2;
+  for (int t = bpx; t > 1; --t)
+    if (t - 1 + 2 * c.in_pad * ((c.W + t - 2) / c.W) + 2 * P + 1 <= segcap) return t;
+  return 1;
+}
 
 // Returns the block tile width (output channels) the conv kernels use for cout.
 int conv_bco_for(int cout);
@@ -47,6 +62,11 @@ hipError_t launch_conv(const ConvLaunch& c, hipStream_t s);
 // the transformed filters [co_tile][chunk][xi 16][plane 2][BCO][4].
 int wino_bco_for(int cout);
 hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
+// Split-fp16 (3 x fp16 MFMA = fp32-accurate) direct convolution: same tiles as
+// launch_conv; x3_fits() says whether the input segment of a pixel tile fits.
+hipError_t launch_conv_x3(const ConvLaunch& c, hipStream_t s);
+bool x3_fits(const ConvLaunch& c);
+double conv_x3_mfma_flops(const ConvLaunch& c);
 // FLOPs the matrix cores execute for one launch (tile padding included)
 double conv_mfma_flops(const ConvLaunch& c);
 double wino_mfma_flops(const ConvLaunch& c);

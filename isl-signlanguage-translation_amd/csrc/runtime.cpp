@@ -56,6 +56,8 @@ struct ConvLayer {
   int wbco = 0;                  // Winograd tile (3x3 layers), 0 = direct only
   float *d_w = nullptr, *d_b = nullptr, *d_s = nullptr;
   float* d_wu = nullptr;         // Winograd-transformed filters
+  void* d_wx3 = nullptr;         // split-fp16 filters (conv_x3.hip)
+  float x3_inv = 1.f;            // 2^-s of the split weights
 };
 
 static ConvLayer mk(const std::string& name, int cin, int cout, int k, int act, const std::string& prelu = "") {
@@ -206,6 +208,9 @@ struct isl_net {
   };
   bool timing = false;
   std::vector<TimedRun> timed;
+  // conv algorithm (ISL_ALGO_*) and the split-fp16 range flag (isl_net_check)
+  int algo = ISL_ALGO_X3;
+  int* d_flag = nullptr;
 };
 
 namespace isl {
@@ -420,6 +425,44 @@ static std::vector<float> pack_wino(const ConvLayer& c) {
   return out;
 }
 
+// Split-fp16 filters for conv_x3.hip: w * 2^s = hi + lo (both fp16, round to
+// nearest), 2^s chosen per layer so that max|w| * 2^s lies in [2^13, 2^14);
+// layout [co_tile][chunk pair][ky][kx][hi|lo][h][BCO][8], h = chunk of the pair.
+static std::vector<_Float16> pack_x3(const ConvLayer& c, float* inv_scale) {
+  const int ks = c.k, bco = c.bco, chunks = c.cin_phys / 8, pairs = (chunks + 1) / 2;
+  const int co_tiles = (c.cout + bco - 1) / bco;
+  std::vector<int> p2l(pairs * 16, -1);
+  for (const Seg& s : c.cmap)
+    for (int i = 0; i < s.len; ++i) p2l[s.phys + i] = s.logical + i;
+  float mx = 0.f;
+  for (float v : c.w) mx = std::max(mx, std::fabs(v));
+  int e = 0;
+  if (mx > 0.f) {
+    std::frexp(mx, &e);            // mx = f * 2^e, f in [0.5, 1)
+    e = 14 - e;                    // mx * 2^e in [2^13, 2^14)
+  }
+  const float scale = std::ldexp(1.f, e);
+  *inv_scale = std::ldexp(1.f, -e);
+  std::vector<_Float16> out((size_t)co_tiles * pairs * ks * ks * 2 * 2 * bco * 8, (_Float16)0.f);
+  for (int ct = 0; ct < co_tiles; ++ct)
+    for (int pr = 0; pr < pairs; ++pr)
+      for (int ky = 0; ky < ks; ++ky)
+        for (int kx = 0; kx < ks; ++kx)
+          for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < bco; ++i)
+              for (int j = 0; j < 8; ++j) {
+                const int co = ct * bco + i, lci = p2l[pr * 16 + h * 8 + j];
+                if (co >= c.cout || lci < 0) continue;
+                const float w = c.w[(((size_t)co * c.cin + lci) * ks + ky) * ks + kx] * scale;
+                const _Float16 hi = (_Float16)w;
+                const _Float16 lo = (_Float16)(w - (float)hi);
+                const size_t base = ((((size_t)(ct * pairs + pr) * ks + ky) * ks + kx) * 2) * 2 * bco;
+                out[((base + 0 * 2 * bco) + (size_t)h * bco + i) * 8 + j] = hi;
+                out[((base + 1 * 2 * bco) + (size_t)h * bco + i) * 8 + j] = lo;
+              }
+  return out;
+}
+
 static int upload_params(isl_net* net) {
   for (ConvLayer& c : net->layers) {
     if (!c.has_w || !c.has_b || (c.act == ACT_PRELU && !c.has_s))
@@ -435,11 +478,20 @@ static int upload_params(isl_net* net) {
     HIP_OK(hipMemcpy(c.d_w, wp.data(), wp.size() * sizeof(float), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(c.d_b, bp.data(), bp.size() * sizeof(float), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(c.d_s, sp.data(), sp.size() * sizeof(float), hipMemcpyHostToDevice));
+    {
+      std::vector<_Float16> xp = pack_x3(c, &c.x3_inv);
+      if (!c.d_wx3) HIP_OK(hipMalloc(&c.d_wx3, xp.size() * sizeof(_Float16)));
+      HIP_OK(hipMemcpy(c.d_wx3, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
     if (c.wbco) {
       std::vector<float> up = pack_wino(c);
       if (!c.d_wu) HIP_OK(hipMalloc(&c.d_wu, up.size() * sizeof(float)));
       HIP_OK(hipMemcpy(c.d_wu, up.data(), up.size() * sizeof(float), hipMemcpyHostToDevice));
     }
+  }
+  if (!net->d_flag) {
+    HIP_OK(hipMalloc(&net->d_flag, sizeof(int)));
+    HIP_OK(hipMemset(net->d_flag, 0, sizeof(int)));
   }
   net->packed = true;
   return ISL_OK;
@@ -479,11 +531,14 @@ static int plan(isl_net* net, int n, int h, int w) {
   return ISL_OK;
 }
 
-// 3x3 layers: Winograd F(2x2,3x3) by default; ISLPOSE_CONV_ALGO=direct selects the
-// direct implicit-GEMM kernel for every layer (read per call, for A/B tests).
-static bool conv_algo_wino() {
+// Conv algorithm of a net (isl_net_set_algo); ISLPOSE_CONV_ALGO=x3|wino|direct
+// sets the default at isl_net_create (A/B tests).
+static int default_algo() {
   const char* e = getenv("ISLPOSE_CONV_ALGO");
-  return !(e && e[0] == 'd');
+  if (!e) return ISL_ALGO_X3;
+  if (e[0] == 'w') return ISL_ALGO_WINO;
+  if (e[0] == 'd') return ISL_ALGO_DIRECT;
+  return ISL_ALGO_X3;
 }
 
 static int run_ops(isl_net* net, hipStream_t s) {
@@ -514,17 +569,24 @@ static int run_ops(isl_net* net, hipStream_t s) {
     L.wpk = c.d_w; L.bias = c.d_b; L.slope = c.d_s;
     L.n = in.n; L.H = in.H; L.W = in.W; L.ks = c.k; L.cin_chunks = c.cin_phys / 8;
     L.cout = c.cout; L.bco = c.bco; L.act = c.act;
-    const bool wino = c.wbco && conv_algo_wino();
-    if (wino) {
+    L.wx3 = c.d_wx3; L.wscale_inv = c.x3_inv; L.range_flag = net->d_flag;
+    int kind = 1;
+    double mf = 0.0;
+    if (net->algo == ISL_ALGO_WINO && c.wbco) {
       L.wpk = c.d_wu; L.bco = c.wbco;
       HIP_OK(launch_wino(L, s));
+      kind = 2; mf = wino_mfma_flops(L);
+    } else if (net->algo == ISL_ALGO_X3 && x3_fits(L)) {
+      HIP_OK(launch_conv_x3(L, s));
+      kind = 3; mf = conv_x3_mfma_flops(L);
     } else {
       HIP_OK(launch_conv(L, s));
+      mf = conv_mfma_flops(L);
     }
     if (tr) {
-      tr->kind.push_back(wino ? 2 : 1);
+      tr->kind.push_back(kind);
       tr->flops.push_back(2.0 * c.cout * c.cin * c.k * c.k * (double)in.H * in.W * in.n);
-      tr->mfma_flops.push_back(wino ? wino_mfma_flops(L) : conv_mfma_flops(L));
+      tr->mfma_flops.push_back(mf);
       HIP_OK(hipEventRecord(tr->ev[k + 1], s));
     }
   }
@@ -581,6 +643,7 @@ int isl_net_create(int kind, int device, isl_net** out) {
   isl_net* net = new isl_net();
   net->kind = kind;
   net->device = device;
+  net->algo = default_algo();
   net->layers = kind == ISL_BODY25 ? body25_layers() : kind == ISL_COCO ? coco_layers() : hand_layers();
   for (size_t i = 0; i < net->layers.size(); ++i) {
     const ConvLayer& c = net->layers[i];
@@ -604,7 +667,9 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_b) (void)hipFree(c.d_b);
     if (c.d_s) (void)hipFree(c.d_s);
     if (c.d_wu) (void)hipFree(c.d_wu);
+    if (c.d_wx3) (void)hipFree(c.d_wx3);
   }
+  if (net->d_flag) (void)hipFree(net->d_flag);
   for (auto& kv : net->plans) (void)hipFree(kv.second.first);
   if (net->scratch) (void)hipFree(net->scratch);
   for (auto& r : net->timed)
@@ -725,6 +790,28 @@ int isl_net_timing(isl_net* net, int max_ops, int* n_ops, int* n_runs, double* o
   net->timed.clear();
   return ISL_OK;
 }
+
+int isl_net_set_algo(isl_net* net, int algo) {
+  if (!net) return fail(ISL_E_ARG, "net is NULL");
+  if (algo < ISL_ALGO_X3 || algo > ISL_ALGO_DIRECT) return fail(ISL_E_ARG, "unknown conv algorithm");
+  net->algo = algo;
+  return ISL_OK;
+}
+
+int isl_net_get_algo(const isl_net* net) { return net ? net->algo : fail(ISL_E_ARG, "net is NULL"); }
+
+int isl_net_check(isl_net* net, int clear) {
+  if (!net) return fail(ISL_E_ARG, "net is NULL");
+  if (!net->d_flag) return ISL_OK;
+  HIP_OK(hipSetDevice(net->device));
+  int f = 0;
+  HIP_OK(hipMemcpy(&f, net->d_flag, sizeof(int), hipMemcpyDeviceToHost));   // device-synchronising
+  if (f && clear) HIP_OK(hipMemset(net->d_flag, 0, sizeof(int)));
+  if (f) return fail(ISL_E_RANGE, "an activation left the split-fp16 range (|x| >= 65504); re-run with ISL_ALGO_DIRECT");
+  return ISL_OK;
+}
+
+const int* isl_net_range_flag(const isl_net* net) { return net ? net->d_flag : nullptr; }
 
 int isl_net_run(isl_net* net, float* d_out0, float* d_out1, void* stream) {
   if (!net || !net->arena) return fail(ISL_E_STATE, "isl_net_run before isl_net_preprocess");

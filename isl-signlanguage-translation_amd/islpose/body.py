@@ -168,6 +168,11 @@ class BodyEstimator:
         n, H, W, _ = t.shape
         geoms, pafs, heats = self.run_scales(t)
         host, lay, caps = self.post(n, H, W, geoms, pafs, heats)
+        if not self.net.range_ok():
+            # split-fp16 range exceeded somewhere in the batch: recompute it on the fp32 kernels
+            with self.net.algo_scope("direct"):
+                geoms, pafs, heats = self.run_scales(t)
+                host, lay, caps = self.post(n, H, W, geoms, pafs, heats)
         res = self.decode(host, lay, caps, n)
         if details:
             return res

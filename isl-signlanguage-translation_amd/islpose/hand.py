@@ -64,4 +64,9 @@ class HandEstimator:
         n, h, w, _ = t.shape
         geoms, heats = self.run_scales(t)
         peaks = self.post_maps(h, w, geoms, heats)
+        if not self.net.range_ok():
+            # split-fp16 range exceeded: recompute the crops on the fp32 kernels
+            with self.net.algo_scope("direct"):
+                geoms, heats = self.run_scales(t)
+                peaks = self.post_maps(h, w, geoms, heats)
         return peaks[0] if single else peaks

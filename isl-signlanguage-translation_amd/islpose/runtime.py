@@ -11,14 +11,19 @@ import os
 import numpy as np
 
 ISL_OK, ISL_E_ARG, ISL_E_PARAM, ISL_E_HIP, ISL_E_CAPACITY, ISL_E_STATE, ISL_E_INDEX = 0, -1, -2, -3, -4, -5, -6
+ISL_E_RANGE = -7
 ISL_BODY25, ISL_COCO, ISL_HAND = 0, 1, 2
+# conv arithmetic (isl_algo): split-fp16 x3 (default), Winograd fp32, direct fp32
+ISL_ALGO_X3, ISL_ALGO_WINO, ISL_ALGO_DIRECT = 0, 1, 2
+ALGOS = {"x3": ISL_ALGO_X3, "wino": ISL_ALGO_WINO, "direct": ISL_ALGO_DIRECT}
 
 LIB_PATH = os.environ.get("ISLPOSE_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libislpose.so"))
 
 # every symbol include/islpose.h declares
 EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destroy", "isl_net_param_count",
            "isl_net_param_info", "isl_net_set_param", "isl_net_forward", "isl_net_preprocess", "isl_net_run", "isl_net_debug_input",
-           "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post"]
+           "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post",
+           "isl_net_set_algo", "isl_net_get_algo", "isl_net_check"]
 
 
 class IslCaps(ctypes.Structure):
@@ -65,6 +70,9 @@ def lib():
     L.isl_net_run.argtypes = [vp, vp, vp, vp]
     L.isl_net_debug_input.argtypes = [vp, vp, vp]
     L.isl_net_set_timing.argtypes = [vp, i32]
+    L.isl_net_set_algo.argtypes = [vp, i32]
+    L.isl_net_get_algo.argtypes = [vp]
+    L.isl_net_check.argtypes = [vp, i32]
     pi, pd = ctypes.POINTER(i32), ctypes.POINTER(dbl)
     L.isl_net_timing.argtypes = [vp, i32, pi, pi, pd, pi, pd, pd]
     L.isl_body_layout.argtypes = [i32, ctypes.POINTER(IslCaps), ctypes.POINTER(IslLayout)]
@@ -163,7 +171,45 @@ class Net:
             o1 = out1 if out1 is not None else torch.empty((n, nj, h8, w8), device=x.device)
         check(lib().isl_net_forward(self.h, ptr(x), n, h, w, ptr(o0), ptr(o1), stream_handle(stream)),
               "isl_net_forward")
+        if not self.range_ok():
+            # an activation left the split-fp16 range: recompute on the fp32 kernels
+            with self.algo_scope("direct"):
+                check(lib().isl_net_forward(self.h, ptr(x), n, h, w, ptr(o0), ptr(o1), stream_handle(stream)),
+                      "isl_net_forward")
         return o0 if o1 is None else (o0, o1)
+
+    # -- conv arithmetic -----------------------------------------------------------
+    @property
+    def algo(self) -> str:
+        a = lib().isl_net_get_algo(self.h)
+        return {v: k for k, v in ALGOS.items()}[a]
+
+    def set_algo(self, algo: str):
+        """'x3' (split-fp16 on the FP16 matrix cores, fp32-accurate; default), 'wino'
+        (Winograd F(2x2,3x3), FP32 MFMA) or 'direct' (implicit GEMM, FP32 MFMA)."""
+        check(lib().isl_net_set_algo(self.h, ALGOS[algo]), "isl_net_set_algo")
+
+    def algo_scope(self, algo: str):
+        import contextlib
+
+        @contextlib.contextmanager
+        def scope():
+            prev = self.algo
+            self.set_algo(algo)
+            try:
+                yield
+            finally:
+                self.set_algo(prev)
+        return scope()
+
+    def range_ok(self, clear: bool = True) -> bool:
+        """Device-synchronising check of the split-fp16 range flag (isl_net_check):
+        False if any conv output since the last clear reached |x| >= 65504."""
+        rc = lib().isl_net_check(self.h, 1 if clear else 0)
+        if rc == ISL_E_RANGE:
+            return False
+        check(rc, "isl_net_check")
+        return True
 
     def preprocess(self, frames_u8, scale: float, stream=None):
         """frames uint8 [n,H,W,3] cuda -> fills the net input; returns (net_h, net_w)."""

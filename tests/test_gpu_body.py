@@ -49,27 +49,27 @@ def test_body25_forward_vs_oracle(net25, w25, n, h, w):
     assert _rel(heat.cpu().numpy(), rh) < TOL
 
 
-@pytest.mark.parametrize("algo", ["direct", "wino"])
-def test_body25_forward_algo_vs_oracle(net25, w25, monkeypatch, algo):
-    """Both 3x3 algorithms (direct implicit GEMM, Winograd F(2x2,3x3)) against the
-    oracle; 2 x 184x328 puts odd sizes (23x41) on the stage layers."""
-    monkeypatch.setenv("ISLPOSE_CONV_ALGO", algo)
+@pytest.mark.parametrize("algo", ["x3", "direct", "wino"])
+def test_body25_forward_algo_vs_oracle(net25, w25, algo):
+    """Every conv arithmetic (split-fp16 x3, direct fp32 implicit GEMM, Winograd
+    F(2x2,3x3)) against the oracle; 2 x 184x328 puts odd sizes (23x41) on the stage layers."""
     x = _inputs(2, 184, 328, seed=77)
-    paf, heat = net25.forward(torch.from_numpy(x).cuda())
+    with net25.algo_scope(algo):
+        paf, heat = net25.forward(torch.from_numpy(x).cuda())
     torch.cuda.synchronize()
     rp, rh = cpu_ref.make_net_fn("body25", w25)(x)
     ep, eh = _rel(paf.cpu().numpy(), rp), _rel(heat.cpu().numpy(), rh)
     print("algo %s: rel err paf %.3g heat %.3g" % (algo, ep, eh))
-    assert ep < TOL and eh < TOL
+    assert ep < TOL and eh < TOL, (ep, eh)
 
 
 def test_body25_forward_lds_dma_staging(net25, w25, monkeypatch):
     """The LDS-DMA staging variant of the conv kernel gives the same results."""
     x = torch.from_numpy(_inputs(2, 50, 70, seed=9)).cuda()
-    monkeypatch.setenv("ISLPOSE_CONV_ALGO", "direct")
-    paf0, heat0 = net25.forward(x)
-    monkeypatch.setenv("ISLPOSE_CONV_STAGING", "glds")
-    paf1, heat1 = net25.forward(x)
+    with net25.algo_scope("direct"):
+        paf0, heat0 = net25.forward(x)
+        monkeypatch.setenv("ISLPOSE_CONV_STAGING", "glds")
+        paf1, heat1 = net25.forward(x)
     torch.cuda.synchronize()
     assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
 
@@ -185,3 +185,38 @@ def test_designed_maps_batch_bit_exact(est25):
         assert np.array_equal(res[i].candidate, cand), i
         assert np.array_equal(res[i].subset, subset), i
         assert len(subset) == i, i
+
+
+def test_x3_range_guard_falls_back_to_fp32(w25):
+    """Activations beyond the fp16 split range (|x| >= 65504) raise the net's range
+    flag; Net.forward then recomputes on the fp32 kernels, so the result still
+    matches the oracle, and the net keeps its split-fp16 default afterwards."""
+    w = dict(w25)
+    w["conv1_1.weight"] = w["conv1_1.weight"] * np.float32(2.0 ** 20)   # conv1_1 outputs ~1e5-1e6
+    w["conv1_1.bias"] = w["conv1_1.bias"] * np.float32(2.0 ** 20)
+    net = rt.Net(rt.ISL_BODY25)
+    net.load_weights(w)
+    assert net.algo == "x3"
+    x = _inputs(1, 64, 96, seed=21)
+    xt = torch.from_numpy(x).cuda()
+    o0 = torch.empty((1, 52, 8, 12), device="cuda")
+    o1 = torch.empty((1, 26, 8, 12), device="cuda")
+    rt.check(rt.lib().isl_net_forward(net.h, rt.ptr(xt), 1, 64, 96, rt.ptr(o0), rt.ptr(o1), rt.stream_handle()))
+    assert not net.range_ok()             # raw x3 run flagged
+    assert net.range_ok()                 # and the flag was cleared
+    paf, heat = net.forward(xt)           # guarded seam: falls back
+    rp, rh = cpu_ref.make_net_fn("body25", w)(x)
+    assert _rel(paf.cpu().numpy(), rp) < TOL and _rel(heat.cpu().numpy(), rh) < TOL
+    assert net.algo == "x3"
+
+
+def test_x3_matches_direct_small_shapes(net25):
+    """Split-fp16 vs fp32 direct on awkward shapes (narrow images, one-row tiles,
+    odd chunk counts) -- both within the tolerance of each other."""
+    for (n, h, w) in [(1, 16, 200), (3, 40, 16), (1, 64, 24), (1, 8, 8)]:
+        x = torch.from_numpy(_inputs(n, h, w, seed=h * w)).cuda()
+        with net25.algo_scope("direct"):
+            p0, h0 = net25.forward(x)
+        p1, h1 = net25.forward(x)
+        assert _rel(p1.cpu().numpy(), p0.cpu().numpy()) < TOL
+        assert _rel(h1.cpu().numpy(), h0.cpu().numpy()) < TOL

@@ -24,3 +24,7 @@ clean:
 	rm -rf build $(OUT)
 
 .PHONY: all clean
+
+# development microbenchmark of the conv kernels (not part of the library)
+tools/convbench: tools/convbench.cpp $(OBJS)
+	$(HIPCC) $(HIPFLAGS) -x hip tools/convbench.cpp -x none $(filter-out build/runtime.cpp.o build/post.hip.o build/ops.hip.o,$(OBJS)) build/runtime.cpp.o build/post.hip.o build/ops.hip.o -o $@

@@ -38,6 +38,8 @@
 // Double-buffered, one barrier per step; per step and wave KS taps x WM*WN
 // accumulator tiles x 3 MFMAs.
 #include <cmath>
+#include <cstdlib>
+#include <type_traits>
 
 #include "internal.h"
 
@@ -61,23 +63,28 @@ struct X3Args {
   int H, W, cin_chunks, pairs, cout, co_tiles, px_tiles, tpx, act, nblocks;
 };
 
-constexpr int X3_SEGMAX = 192;   // input segment capacity in pixels (host-checked)
+// input segment capacity in pixels for a BPX-pixel tile (host: tile_pixels)
+constexpr int x3_segmax(int bpx) { return bpx + 64; }
 
-template <int KS, int WAVES_M, int WAVES_N, int WM, int WN>
-__global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 2) conv_x3_f16(X3Args a) {
+template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, int VAR, int OCC>
+__global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Args a) {
   constexpr int NT = WAVES_M * WAVES_N * 64;
   constexpr int NWAVES = WAVES_M * WAVES_N;
   constexpr int BCO = WAVES_M * WM * 32;
   constexpr int BPX = WAVES_N * WN * 32;
   constexpr int P = KS / 2;
-  constexpr int SEGMAX = X3_SEGMAX;
+  constexpr int SEGMAX = x3_segmax(BPX);
   constexpr int WSLAB = KS * 2 * 2 * BCO;        // 16-byte units: [kx][hi|lo][h][BCO]
-  constexpr int XSLAB = 2 * 2 * SEGMAX;          // 16-byte units: [hi|lo][h][px]
+  constexpr int SEGP = SEGMAX + 1;               // + one dummy slot idle staging items write to
+  constexpr int XSLAB = 2 * 2 * SEGP;            // 16-byte units: [hi|lo][h][px]
   constexpr int BUF = WSLAB + XSLAB;
   constexpr int IT = (2 * SEGMAX + NT - 1) / NT; // staging items (h, px) per thread
   static_assert(WSLAB % 64 == 0, "weight slab is whole 1 KiB DMA pieces");
   static_assert(BPX <= SEGMAX, "segment must hold a tile");
   static_assert(2 * BUF * 16 <= 160 * 1024, "LDS");
+  constexpr bool WEAVE = (VAR & 2) != 0;         // interleave the stores with the MFMAs
+  constexpr bool NO_STAGE = (VAR & 8) != 0;      // ablation: skip global loads + LDS stores
+  constexpr bool NO_MATH = (VAR & 16) != 0;      // ablation: skip LDS reads + MFMAs
   __shared__ f16x8 smem[2 * BUF];
 
   // XCD-aware tile order (conv.hip): co-tiles of a pixel tile, then neighbouring
@@ -157,8 +164,8 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 2) conv_x3_f16(X3Args 
         hi[j] = (_Float16)x;
         lo[j] = (_Float16)(x - (float)hi[j]);
       }
-      s[(0 * 2 + ih[i]) * SEGMAX + ipx[i]] = hi;
-      s[(1 * 2 + ih[i]) * SEGMAX + ipx[i]] = lo;
+      s[(0 * 2 + ih[i]) * SEGP + ipx[i]] = hi;
+      s[(1 * 2 + ih[i]) * SEGP + ipx[i]] = lo;
     }
   };
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -182,18 +189,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 2) conv_x3_f16(X3Args 
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[wm][wn][r] = 0.f;
 
-  issue_w(0, 0);
-  load_x(0);
-  store_x(0);
-  __syncthreads();
-  for (int t = 0; t < T; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < T) {
-      issue_w(t + 1, buf ^ 1);
-      load_x(t + 1);
-    }
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    if constexpr (NO_MATH) return;
     const f16x8* sw = smem + buf * BUF + h * BCO + wave_m * WM * 32 + l32;
-    const f16x8* sx = smem + buf * BUF + WSLAB + h * SEGMAX;
+    const f16x8* sx = smem + buf * BUF + WSLAB + h * SEGP;
 #pragma unroll
     for (int kx = 0; kx < KS; ++kx) {
       f16x8 A[WM][2], B[WN][2];
@@ -202,7 +201,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 2) conv_x3_f16(X3Args 
 #pragma unroll
         for (int wm = 0; wm < WM; ++wm) A[wm][hl] = sw[(kx * 2 + hl) * 2 * BCO + wm * 32];
 #pragma unroll
-        for (int wn = 0; wn < WN; ++wn) B[wn][hl] = sx[hl * 2 * SEGMAX + rel[wn] + kx];
+        for (int wn = 0; wn < WN; ++wn) B[wn][hl] = sx[hl * 2 * SEGP + rel[wn] + kx];
       }
 #pragma unroll
       for (int wm = 0; wm < WM; ++wm)
@@ -213,8 +212,118 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 2) conv_x3_f16(X3Args 
           acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[wn][0], acc[wm][wn], 0, 0, 0);
         }
     }
-    if (t + 1 < T) store_x(buf ^ 1);
+  };
+
+  if constexpr ((VAR & 1) == 0) {
+    // weights by LDS-DMA one step ahead, input rows register-staged one step ahead
+    issue_w(0, 0);
+    load_x(0);
+    store_x(0);
     __syncthreads();
+    for (int t = 0; t < T; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < T) {
+        issue_w(t + 1, buf ^ 1);
+        load_x(t + 1);
+      }
+      compute(buf);
+      if (t + 1 < T) store_x(buf ^ 1);
+      __syncthreads();
+    }
+  } else {
+    // everything register-staged, loads issued two steps ahead (two register
+    // sets; the loop is unrolled by two so set indices are compile-time): a
+    // step's loads have a whole step of MFMAs more to land than with VAR 0.
+    constexpr int WIT = (WSLAB + NT - 1) / NT;
+    f16x8 rw[2][WIT];
+    f32x4 rx[2][IT][2];
+    auto load = [&](auto S_, int t) __attribute__((always_inline)) {
+      constexpr int S = decltype(S_)::value;
+      if constexpr (NO_STAGE) return;
+      t = min(t, T - 1);   // past the end: harmless reload, never stored
+      const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
+#pragma unroll
+      for (int i = 0; i < WIT; ++i) {
+        const int idx = tid + i * NT;
+        if (WSLAB % NT == 0 || idx < WSLAB) rw[S][i] = src[idx];
+      }
+      const int c2 = t / KS, ky = t - c2 * KS;
+      const long long row = (long long)(La + (ky - P) * Wi - P);
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        const int c = min(2 * c2 + ih[i], a.cin_chunks - 1);
+        const int px = max(ipx[i], 0);
+        const float* xs = in_f + (size_t)c * a.in_chs + (size_t)(row + px) * 8;
+        rx[S][i][0] = *(const f32x4*)xs;
+        rx[S][i][1] = *(const f32x4*)(xs + 4);
+      }
+    };
+    // (the zeroing of a missing odd chunk happens here, at the use: a select right
+    // after the load would make the compiler wait for it a whole step early)
+    auto store = [&](auto S_, int buf, int t) __attribute__((always_inline)) {
+      constexpr int S = decltype(S_)::value;
+      if constexpr (NO_STAGE) return;
+      const int c2 = t / KS;
+      f16x8* sw = smem + buf * BUF;
+#pragma unroll
+      for (int i = 0; i < WIT; ++i) {
+        const int idx = tid + i * NT;
+        if (WSLAB % NT == 0 || idx < WSLAB) sw[idx] = rw[S][i];
+      }
+      f16x8* sx = smem + buf * BUF + WSLAB;
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        // no branch around idle items (they write the dummy slot): a store under an
+        // exec branch makes the compiler's waitcnt bookkeeping fall back to vmcnt(0)
+        const int px = ipx[i] < 0 ? SEGMAX : ipx[i];
+        f16x8 hi, lo;
+        const bool zero = 2 * c2 + ih[i] >= a.cin_chunks;
+        if constexpr ((VAR & 32) != 0) {   // ablation: no conversion (raw bits as fragments)
+          hi = __builtin_bit_cast(f16x8, rx[S][i][0]);
+          lo = __builtin_bit_cast(f16x8, rx[S][i][1]);
+        } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = zero ? 0.f : rx[S][i][j >> 2][j & 3];
+          hi[j] = (_Float16)x;
+          lo[j] = (_Float16)(x - (float)hi[j]);
+        }
+        }
+        sx[(0 * 2 + ih[i]) * SEGP + px] = hi;
+        sx[(1 * 2 + ih[i]) * SEGP + px] = lo;
+      }
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    load(S0{}, 0);
+    load(S1{}, 1);
+    store(S0{}, 0, 0);
+    __syncthreads();
+    // the loop body is branch-free (a store skipped on some path would make the
+    // compiler's waitcnt bookkeeping fall back to vmcnt(0) at the next reuse)
+    int t = 0;
+    // sched_barrier pins the phase order: loads issued first, the previous set's
+    // stores after this step's MFMAs (hoisting them would wait on young loads)
+    for (; t + 2 < T; t += 2) {
+      load(S0{}, t + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0);
+      if constexpr (!WEAVE) __builtin_amdgcn_sched_barrier(0);
+      store(S1{}, 1, t + 1);
+      __syncthreads();
+      load(S1{}, t + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1);
+      if constexpr (!WEAVE) __builtin_amdgcn_sched_barrier(0);
+      store(S0{}, 0, t + 2);
+      __syncthreads();
+    }
+    compute(0);                 // step t; step t+1 if T - t == 2
+    if (t + 1 < T) {
+      store(S1{}, 1, t + 1);
+      __syncthreads();
+      compute(1);
+    }
   }
 
   // epilogue: x 2^-s, bias + activation, range check, masked float4 stores
@@ -261,12 +370,12 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, 2) conv_x3_f16(X3Args 
   if (bad) atomicOr(a.range_flag, 1);
 }
 
-template <int KS, int WAVES_M, int WAVES_N, int WM, int WN>
+template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, int VAR, int OCC>
 static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   constexpr int BCO = WAVES_M * WM * 32;
   constexpr int BPX = WAVES_N * WN * 32;
   constexpr int P = KS / 2;
-  constexpr int SEGCAP = X3_SEGMAX;
+  constexpr int SEGCAP = x3_segmax(BPX);
   if (c.in_pad < P) { set_error("conv_x3: input ring narrower than kernel radius"); return hipErrorInvalidValue; }
   if (c.bco != BCO) { set_error("conv_x3: tile mismatch"); return hipErrorInvalidValue; }
   if ((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 7) { set_error("conv_x3: slice not on a chunk"); return hipErrorInvalidValue; }
@@ -287,22 +396,57 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   a.tpx = tile_pixels(c, BPX, SEGCAP);
   a.px_tiles = (c.H * c.W + a.tpx - 1) / a.tpx;
   a.act = c.act;
-  (void)P;
   const long long nb = (long long)c.n * a.px_tiles * a.co_tiles;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
-  hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN>), dim3(a.nblocks), dim3(WAVES_M * WAVES_N * 64), 0, s,
-                     a);
+  hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN, VAR, OCC>), dim3(a.nblocks),
+                     dim3(WAVES_M * WAVES_N * 64), 0, s, a);
   return hipGetLastError();
 }
 
+static int x3_var() {
+  static const int v = getenv("ISLPOSE_X3_VAR") ? atoi(getenv("ISLPOSE_X3_VAR")) : 0;
+  return v;
+}
+
+static bool x3_small_tiles() {
+  static const bool v = getenv("ISLPOSE_X3_TILES") && getenv("ISLPOSE_X3_TILES")[0] == 's';
+  return v;
+}
+
+// Tile families.  3x3 / 1x1 layers: 512-pixel tiles (8-16 waves per block, one
+// block per CU): the weight slab of a K step is then shared by 4x the pixels,
+// which cut the L2->LDS bytes per FLOP ~2x and measured +10 % over the 128-pixel
+// tiles (r01).  7x7 layers keep 128-pixel tiles (their slab is 2.3x larger).
 template <int KS>
 static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
+  const int var = KS <= 3 ? x3_var() : 0;
+  if constexpr (KS <= 3) {
+    if (!x3_small_tiles() && var == 0) {
+      switch (c.bco) {
+        case 128: return launch_t<KS, 2, 8, 2, 2, 0, 4>(c, s);
+        case 96: return launch_t<KS, 1, 8, 3, 2, 0, 2>(c, s);
+        case 64: return launch_t<KS, 1, 8, 2, 2, 0, 2>(c, s);
+        case 32: return launch_t<KS, 1, 8, 1, 2, 0, 2>(c, s);
+      }
+    }
+    if (var == 4 && c.bco == 128) return launch_t<KS, 2, 2, 2, 4, 3, 1>(c, s);
+    if (var == 5 && c.bco == 128) return launch_t<KS, 2, 2, 2, 4, 1, 1>(c, s);
+    if (var == 6 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 1, 2>(c, s);
+    if (var == 7 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 0, 2>(c, s);
+    if (var == 8 && c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 1, 4>(c, s);
+  }
   switch (c.bco) {
-    case 128: return launch_t<KS, 2, 2, 2, 2>(c, s);
-    case 96: return launch_t<KS, 1, 4, 3, 1>(c, s);
-    case 64: return launch_t<KS, 1, 4, 2, 1>(c, s);
-    case 32: return launch_t<KS, 1, 4, 1, 1>(c, s);
+#define X3_CASE(BC, WMS, WNS, WMM, WNN)                                                   \
+  case BC:                                                                                \
+    if (var == 1) return launch_t<KS, WMS, WNS, WMM, WNN, (KS <= 3 ? 1 : 0), 2>(c, s);    \
+    if (var == 3) return launch_t<KS, WMS, WNS, WMM, WNN, (KS <= 3 ? 3 : 0), 2>(c, s);    \
+    return launch_t<KS, WMS, WNS, WMM, WNN, 0, 2>(c, s);
+    X3_CASE(128, 2, 2, 2, 2)
+    X3_CASE(96, 1, 4, 3, 1)
+    X3_CASE(64, 1, 4, 2, 1)
+    X3_CASE(32, 1, 4, 1, 1)
+#undef X3_CASE
   }
   set_error("conv_x3: unsupported tile");
   return hipErrorInvalidValue;
@@ -311,9 +455,9 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
 bool x3_fits(const ConvLaunch& c) { return c.in_pad >= c.ks / 2; }
 
 double conv_x3_mfma_flops(const ConvLaunch& c) {
-  const int BPX = 128;
+  const int BPX = (c.ks <= 3 && !x3_small_tiles() && x3_var() == 0) ? 512 : 128;
   const double co = (double)((c.cout + c.bco - 1) / c.bco) * c.bco;
-  const double px = std::ceil((double)c.H * c.W / tile_pixels(c, BPX, X3_SEGMAX)) * BPX;
+  const double px = std::ceil((double)c.H * c.W / tile_pixels(c, BPX, x3_segmax(BPX))) * BPX;
   return 3.0 * 2.0 * co * (((c.cin_chunks + 1) / 2) * 16.0) * c.ks * c.ks * px * c.n;
 }
 

@@ -1,0 +1,103 @@
+// Conv-kernel microbenchmark (development tool, not shipped): times one conv
+// layer shape on random data with every algorithm, interleaved in one process.
+//   build: make convbench          run: tools/convbench ks cin cout H W n iters
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+using namespace isl;
+
+#define CK(x)                                                                              \
+  do {                                                                                     \
+    hipError_t e = (x);                                                                    \
+    if (e != hipSuccess) {                                                                 \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e));      \
+      exit(1);                                                                             \
+    }                                                                                      \
+  } while (0)
+
+template <class T>
+static T* dev_random(size_t n, float lo, float hi, unsigned seed) {
+  std::vector<T> h(n);
+  std::mt19937 g(seed);
+  std::uniform_real_distribution<float> d(lo, hi);
+  for (auto& v : h) v = (T)d(g);
+  T* p;
+  CK(hipMalloc(&p, n * sizeof(T)));
+  CK(hipMemcpy(p, h.data(), n * sizeof(T), hipMemcpyHostToDevice));
+  return p;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 8) {
+    fprintf(stderr, "usage: convbench ks cin cout H W n iters [algos=x3,direct,wino] [rounds=3]\n");
+    return 2;
+  }
+  const int ks = atoi(argv[1]), cin = atoi(argv[2]), cout = atoi(argv[3]), H = atoi(argv[4]), W = atoi(argv[5]),
+            n = atoi(argv[6]), iters = atoi(argv[7]);
+  const std::string algos = argc > 8 ? argv[8] : "x3,direct,wino";
+  const int rounds = argc > 9 ? atoi(argv[9]) : 3;
+  const int cs_in = (cin + 7) / 8 * 8, cs_out = (cout + 7) / 8 * 8;
+  const int pin = std::max(1, ks / 2), pout = 1;
+  Act in, out;
+  in.n = out.n = n; in.H = out.H = H; in.W = out.W = W;
+  in.pad = pin; in.cs = cs_in; out.pad = pout; out.cs = cs_out;
+  in.base = dev_random<float>(in.bytes() / 4, -1.f, 1.f, 1);
+  CK(hipMalloc(&out.base, out.bytes()));
+  const int chunks = cs_in / 8, pairs = (chunks + 1) / 2, bco = conv_bco_for(cout), co_tiles = (cout + bco - 1) / bco;
+  float* wd = dev_random<float>((size_t)co_tiles * chunks * ks * ks * 2 * bco * 4, -0.05f, 0.05f, 2);
+  _Float16* wx = dev_random<_Float16>((size_t)co_tiles * pairs * ks * ks * 4 * bco * 8, -8192.f, 8192.f, 3);
+  const int wb = wino_bco_for(cout);
+  float* wu = wb ? dev_random<float>((size_t)(cout / wb) * chunks * 16 * 2 * wb * 4, -0.05f, 0.05f, 4) : nullptr;
+  float* bias = dev_random<float>(co_tiles * 128 + 128, -0.05f, 0.05f, 5);
+  float* slope = dev_random<float>(co_tiles * 128 + 128, 0.05f, 0.25f, 6);
+  int* flag;
+  CK(hipMalloc(&flag, 4));
+  CK(hipMemset(flag, 0, 4));
+  ConvLaunch L;
+  L.in = in.base; L.in_pad = pin; L.in_cs = cs_in; L.in_coff = 0;
+  L.out = out.base; L.out_pad = pout; L.out_cs = cs_out; L.out_coff = 0;
+  L.bias = bias; L.slope = slope; L.n = n; L.H = H; L.W = W; L.ks = ks; L.cin_chunks = chunks; L.cout = cout;
+  L.act = ACT_PRELU; L.wx3 = wx; L.wscale_inv = 1.f / 16384.f; L.range_flag = flag;
+  const double flops = 2.0 * cout * cin * ks * ks * (double)H * W * n;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  printf("conv k%d %d->%d %dx%d n=%d: %.2f GFLOP (direct count)\n", ks, cin, cout, H, W, n, flops / 1e9);
+  for (int r = 0; r < rounds; ++r) {
+    size_t pos = 0;
+    while (pos < algos.size()) {
+      size_t e = algos.find(',', pos);
+      if (e == std::string::npos) e = algos.size();
+      const std::string a = algos.substr(pos, e - pos);
+      pos = e + 1;
+      ConvLaunch c = L;
+      auto launch = [&]() -> hipError_t {
+        if (a == "x3") { c.bco = bco; c.wpk = wd; return launch_conv_x3(c, 0); }
+        if (a == "direct") { c.bco = bco; c.wpk = wd; return launch_conv(c, 0); }
+        if (a == "wino" && wb && ks == 3) { c.bco = wb; c.wpk = wu; return launch_wino(c, 0); }
+        return hipErrorNotSupported;
+      };
+      if (launch() != hipSuccess) continue;
+      for (int i = 0; i < 2; ++i) CK(launch());
+      CK(hipEventRecord(e0, 0));
+      for (int i = 0; i < iters; ++i) CK(launch());
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1e3 / iters;
+      const double fac = a == "x3" ? 3.0 : 1.0;
+      printf("  round %d %-7s %9.1f us  fp32-equiv %7.1f TF  alg-MFMA %7.1f TF\n", r, a.c_str(), us,
+             flops / us / 1e6, fac * flops / us / 1e6);
+    }
+  }
+  return 0;
+}

@@ -35,10 +35,11 @@ METRIC = "frames/sec body_25 368×656 fwd+NMS+PAF at 1/8 MI355X; conv MFMA util 
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix peak (spec) = 256 CU x 4 SIMD x 64 FLOP/clk x 2.4 GHz
 PEAK_FP16_MFMA_TFLOPS = 2516.6     # dense FP16/BF16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF, no sparsity)
 KIND = {0: "maxpool2_kernel", 1: "conv_mfma_f32 (direct fp32)", 2: "wino_f23_mfma (Winograd F(2x2,3x3) fp32)",
-        3: "conv_x3_f16 (split-fp16 x3, fp32-accurate)"}
+        3: "conv_x3_f16 (split-fp16 x3, fp32-accurate)",
+        4: "wino_x3_f16 (Winograd F(2x2,3x3), split-fp16 x3, fp32-accurate)"}
 # MFMA FLOPs the algorithm of each kind needs per direct-conv FLOP (2*Cout*Cin*k*k*H*W), tile padding excluded
-ALG_FACTOR = {1: 1.0, 2: 16.0 / 36.0, 3: 3.0}
-KIND_PEAK = {1: PEAK_FP32_MFMA_TFLOPS, 2: PEAK_FP32_MFMA_TFLOPS, 3: PEAK_FP16_MFMA_TFLOPS}
+ALG_FACTOR = {1: 1.0, 2: 16.0 / 36.0, 3: 3.0, 4: 3.0 * 16.0 / 36.0}
+KIND_PEAK = {1: PEAK_FP32_MFMA_TFLOPS, 2: PEAK_FP32_MFMA_TFLOPS, 3: PEAK_FP16_MFMA_TFLOPS, 4: PEAK_FP16_MFMA_TFLOPS}
 
 
 def parse():
@@ -198,12 +199,13 @@ def main():
     fp32_equiv = dk["flops"] / sec / 1e12                      # direct-conv FLOPs per second
     achieved = ALG_FACTOR.get(dom, 1.0) * dk["flops"] / sec / 1e12   # MFMA work the algorithm needs, no padding
     executed = dk["mfma_flops"] / sec / 1e12                   # what the matrix cores ran (tile padding included)
-    conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3))
-    conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3))
+    conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3, 4))
+    conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3, 4))
     traffic = None
     prof = os.path.join(REPO, "profiles", "conv_traffic.json")
     if os.path.exists(prof):
-        traffic = json.load(open(prof)).get({1: "direct", 2: "wino", 3: "x3"}.get(dom, "x3") + "_hbm_bytes_per_launch")
+        traffic = json.load(open(prof)).get({1: "direct", 2: "wino", 3: "x3", 4: "wino_x3"}.get(dom, "x3")
+                                            + "_hbm_bytes_per_launch")
     out = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -215,7 +217,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {3: "fp32 (split-fp16 x3 MFMA, fp32 accumulate)"}.get(dom, "fp32"),
+        "dtype": {3: "fp32 (split-fp16 x3 MFMA, fp32 accumulate)",
+                  4: "fp32 (split-fp16 x3 MFMA, fp32 accumulate)"}.get(dom, "fp32"),
         "data": "synthetic (seeded uint8 frames, counter-hash weights; post fed designed %d-person maps)"
                 % args.persons,
         "config": {"workload": "configs[1]: body_25 single-scale %dx%d frames, batch %d per GPU, net input %dx%d"

@@ -67,6 +67,11 @@ hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
 hipError_t launch_conv_x3(const ConvLaunch& c, hipStream_t s);
 bool x3_fits(const ConvLaunch& c);
 double conv_x3_mfma_flops(const ConvLaunch& c);
+// Split-fp16 Winograd F(2x2,3x3) (wino_x3.hip): 3x3 layers with cout % 4 == 0;
+// c.wx3 then holds the split transformed filters [co_tile][pair][xi][hi|lo][h][64][8].
+hipError_t launch_wino_x3(const ConvLaunch& c, hipStream_t s);
+double wino_x3_mfma_flops(const ConvLaunch& c);
+constexpr int WINO_X3_BCO = 64;
 // FLOPs the matrix cores execute for one launch (tile padding included)
 double conv_mfma_flops(const ConvLaunch& c);
 double wino_mfma_flops(const ConvLaunch& c);

@@ -58,6 +58,8 @@ struct ConvLayer {
   float* d_wu = nullptr;         // Winograd-transformed filters
   void* d_wx3 = nullptr;         // split-fp16 filters (conv_x3.hip)
   float x3_inv = 1.f;            // 2^-s of the split weights
+  void* d_wux3 = nullptr;        // split-fp16 Winograd filters (wino_x3.hip), 3x3 only
+  float wx3_inv = 1.f;
 };
 
 static ConvLayer mk(const std::string& name, int cin, int cout, int k, int act, const std::string& prelu = "") {
@@ -463,6 +465,57 @@ static std::vector<_Float16> pack_x3(const ConvLayer& c, float* inv_scale) {
   return out;
 }
 
+// Split-fp16 Winograd filters for wino_x3.hip: U = G g G^T (double) per (co,
+// physical ci), scaled by a per-layer 2^s (max|U| * 2^s in [2^13, 2^14)), split
+// hi + lo; layout [co_tile][pair][xi][hi|lo][h][64][8], h = chunk of the pair.
+static std::vector<_Float16> pack_wino_x3(const ConvLayer& c, float* inv_scale) {
+  constexpr int BCO = WINO_X3_BCO;
+  const int chunks = c.cin_phys / 8, pairs = (chunks + 1) / 2, co_tiles = (c.cout + BCO - 1) / BCO;
+  std::vector<int> p2l(pairs * 16, -1);
+  for (const Seg& sg : c.cmap)
+    for (int i = 0; i < sg.len; ++i) p2l[sg.phys + i] = sg.logical + i;
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  std::vector<double> U((size_t)c.cout * pairs * 16 * 16, 0.0);   // [co][pc][xi]
+  double mx = 0.0;
+  for (int co = 0; co < c.cout; ++co)
+    for (int pc = 0; pc < pairs * 16; ++pc) {
+      const int lci = p2l[pc];
+      if (lci < 0) continue;
+      const float* g = &c.w[((size_t)co * c.cin + lci) * 9];
+      double t[4][3];
+      for (int i = 0; i < 4; ++i)
+        for (int jj = 0; jj < 3; ++jj) t[i][jj] = G[i][0] * g[0 * 3 + jj] + G[i][1] * g[1 * 3 + jj] + G[i][2] * g[2 * 3 + jj];
+      for (int i = 0; i < 4; ++i)
+        for (int jj = 0; jj < 4; ++jj) {
+          const double u = t[i][0] * G[jj][0] + t[i][1] * G[jj][1] + t[i][2] * G[jj][2];
+          U[((size_t)co * pairs * 16 + pc) * 16 + 4 * i + jj] = u;
+          mx = std::max(mx, std::fabs(u));
+        }
+    }
+  int e = 0;
+  if (mx > 0.0) {
+    std::frexp(mx, &e);
+    e = 14 - e;
+  }
+  const double scale = std::ldexp(1.0, e);
+  *inv_scale = std::ldexp(1.f, -e);
+  std::vector<_Float16> out((size_t)co_tiles * pairs * 16 * 2 * 2 * BCO * 8, (_Float16)0.f);
+  for (int co = 0; co < c.cout; ++co)
+    for (int pc = 0; pc < pairs * 16; ++pc) {
+      if (p2l[pc] < 0) continue;
+      const int ct = co / BCO, i_co = co % BCO, pr = pc / 16, h = (pc % 16) / 8, k = pc % 8;
+      for (int xi = 0; xi < 16; ++xi) {
+        const float w = (float)(U[((size_t)co * pairs * 16 + pc) * 16 + xi] * scale);
+        const _Float16 hi = (_Float16)w;
+        const _Float16 lo = (_Float16)(w - (float)hi);
+        const size_t base = (((size_t)ct * pairs + pr) * 16 + xi) * 2;
+        out[(((base + 0) * 2 + h) * BCO + i_co) * 8 + k] = hi;
+        out[(((base + 1) * 2 + h) * BCO + i_co) * 8 + k] = lo;
+      }
+    }
+  return out;
+}
+
 static int upload_params(isl_net* net) {
   for (ConvLayer& c : net->layers) {
     if (!c.has_w || !c.has_b || (c.act == ACT_PRELU && !c.has_s))
@@ -482,6 +535,11 @@ static int upload_params(isl_net* net) {
       std::vector<_Float16> xp = pack_x3(c, &c.x3_inv);
       if (!c.d_wx3) HIP_OK(hipMalloc(&c.d_wx3, xp.size() * sizeof(_Float16)));
       HIP_OK(hipMemcpy(c.d_wx3, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
+    if (c.k == 3 && c.cout % 4 == 0) {
+      std::vector<_Float16> up = pack_wino_x3(c, &c.wx3_inv);
+      if (!c.d_wux3) HIP_OK(hipMalloc(&c.d_wux3, up.size() * sizeof(_Float16)));
+      HIP_OK(hipMemcpy(c.d_wux3, up.data(), up.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
     if (c.wbco) {
       std::vector<float> up = pack_wino(c);
@@ -541,6 +599,17 @@ static int default_algo() {
   return ISL_ALGO_X3;
 }
 
+// ISL_ALGO_X3 runs 3x3 layers on the direct split-fp16 kernel; ISLPOSE_X3_WINO=1
+// selects the split-fp16 Winograd kernel instead.  It is fp32-accurate (rel err
+// 3e-6) but measured 1.3-1.8x SLOWER (r01): its V transform + split costs ~184
+// VALU ops per (tile, channel), twice the time of the 6144 MFMA FLOPs they feed
+// at 64 output channels per block, and a 128 KB single-buffered step leaves
+// no room for more channels.  Kept for A/B and as the record of that finding.
+static bool x3_wino_enabled() {
+  static const bool on = getenv("ISLPOSE_X3_WINO") && getenv("ISLPOSE_X3_WINO")[0] == '1';
+  return on;
+}
+
 static int run_ops(isl_net* net, hipStream_t s) {
   isl_net::TimedRun* tr = nullptr;
   if (net->timing) {
@@ -576,6 +645,10 @@ static int run_ops(isl_net* net, hipStream_t s) {
       L.wpk = c.d_wu; L.bco = c.wbco;
       HIP_OK(launch_wino(L, s));
       kind = 2; mf = wino_mfma_flops(L);
+    } else if (net->algo == ISL_ALGO_X3 && c.d_wux3 && x3_wino_enabled()) {
+      L.wx3 = c.d_wux3; L.wscale_inv = c.wx3_inv;
+      HIP_OK(launch_wino_x3(L, s));
+      kind = 4; mf = wino_x3_mfma_flops(L);
     } else if (net->algo == ISL_ALGO_X3 && x3_fits(L)) {
       HIP_OK(launch_conv_x3(L, s));
       kind = 3; mf = conv_x3_mfma_flops(L);
@@ -668,6 +741,7 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_s) (void)hipFree(c.d_s);
     if (c.d_wu) (void)hipFree(c.d_wu);
     if (c.d_wx3) (void)hipFree(c.d_wx3);
+    if (c.d_wux3) (void)hipFree(c.d_wux3);
   }
   if (net->d_flag) (void)hipFree(net->d_flag);
   for (auto& kv : net->plans) (void)hipFree(kv.second.first);

@@ -56,6 +56,8 @@ int main(int argc, char** argv) {
   _Float16* wx = dev_random<_Float16>((size_t)co_tiles * pairs * ks * ks * 4 * bco * 8, -8192.f, 8192.f, 3);
   const int wb = wino_bco_for(cout);
   float* wu = wb ? dev_random<float>((size_t)(cout / wb) * chunks * 16 * 2 * wb * 4, -0.05f, 0.05f, 4) : nullptr;
+  const int wxt = (cout + 63) / 64;
+  _Float16* wux = dev_random<_Float16>((size_t)wxt * pairs * 16 * 4 * 64 * 8, -8192.f, 8192.f, 7);
   float* bias = dev_random<float>(co_tiles * 128 + 128, -0.05f, 0.05f, 5);
   float* slope = dev_random<float>(co_tiles * 128 + 128, 0.05f, 0.25f, 6);
   int* flag;
@@ -83,6 +85,7 @@ int main(int argc, char** argv) {
         if (a == "x3") { c.bco = bco; c.wpk = wd; return launch_conv_x3(c, 0); }
         if (a == "direct") { c.bco = bco; c.wpk = wd; return launch_conv(c, 0); }
         if (a == "wino" && wb && ks == 3) { c.bco = wb; c.wpk = wu; return launch_wino(c, 0); }
+        if (a == "wx3" && ks == 3) { c.wx3 = wux; return launch_wino_x3(c, 0); }
         return hipErrorNotSupported;
       };
       if (launch() != hipSuccess) continue;
@@ -94,7 +97,7 @@ int main(int argc, char** argv) {
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       const double us = ms * 1e3 / iters;
-      const double fac = a == "x3" ? 3.0 : 1.0;
+      const double fac = a == "x3" ? 3.0 : a == "wx3" ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
       printf("  round %d %-7s %9.1f us  fp32-equiv %7.1f TF  alg-MFMA %7.1f TF\n", r, a.c_str(), us,
              flops / us / 1e6, fac * flops / us / 1e6);
     }

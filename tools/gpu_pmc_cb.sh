@@ -1,0 +1,13 @@
+# SQ / TA / TCP counters of the conv microbenchmark.  usage: bash tools/gpu_pmc_cb.sh <tag> "<shape>" <algos>
+set -o pipefail
+export TMPDIR=/tmp
+T=$1; S=$2; A=$3; O=gpurun_out/$T; mkdir -p $O
+P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
+P2="SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum"
+P3="TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum"
+i=0
+for P in "$P1" "$P2" "$P3"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $O/p$i -o run -- tools/convbench $S 5 $A 1 > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail $O/p$i.log; exit 1; }
+done
+echo ok

@@ -23,10 +23,10 @@ def main(path, h=368, w=656, B=32, kind=0, quiet=False):
         n = r["Kernel_Name"]
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         tot += d
-        if "conv_mfma" in n or "wino_f23" in n or "conv_x3" in n:
+        if "conv_mfma" in n or "wino_f23" in n or "conv_x3" in n or "wino_x3" in n:
             c = convs[ci]
             fl = 2 * c.cout * c.cin * c.k * c.k * h * w * B
-            key = "%dx%d c%d->%d k%d %s" % (h, w, c.cin, c.cout, c.k, "W" if "wino" in n else ("X" if "x3" in n else "D"))
+            key = "%dx%d c%d->%d k%d %s" % (h, w, c.cin, c.cout, c.k, "WX" if "wino_x3" in n else ("W" if "wino" in n else ("X" if "x3" in n else "D")))
             g = groups.setdefault(key, [0, 0.0, 0.0])
             g[0] += 1; g[1] += d; g[2] += fl
             if c.name in ("conv1_2", "conv2_2", "conv3_4"):

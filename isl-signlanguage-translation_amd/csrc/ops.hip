@@ -8,35 +8,37 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // nn.MaxPool2d(2, 2, 0) (model.py:30-31): floor mode, 4 channels per thread;
 // thread order (frame, chunk, y, x, half) so a wave reads and writes contiguous bytes.
+// 2x2 / stride 2 max-pool (nn.MaxPool2d(2, 2), model.py:33) on chunked buffers.
+// Grid: x = pixel halves of one output plane (32-bit index math), y = (frame, chunk)
+// plane.  A lane pair covers one output pixel's 8 channels (16 B each), so a
+// wave reads two 1 KiB input row runs and writes one 1 KiB output run.
 __global__ void maxpool2_kernel(const float* __restrict__ in, int ip, int iH, int iW, float* __restrict__ out,
-                                int op, int oH, int oW, int chunks, int in_chunks, int out_chunks, int n) {
-  const long long total = (long long)n * chunks * oH * oW * 2;
+                                int op, int oH, int oW, int chunks, int in_chunks, int out_chunks) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= oH * oW * 2) return;
+  const int plane = blockIdx.y, f = plane / chunks, k = plane - f * chunks;
+  const int half = idx & 1, px = idx >> 1;
+  const int y = px / oW, x = px - y * oW;
   const int iWp = iW + 2 * ip, oWp = oW + 2 * op;
   const size_t ich = (size_t)(iH + 2 * ip) * iWp * 8, och = (size_t)(oH + 2 * op) * oWp * 8;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int half = (int)(i & 1);
-    long long r = i >> 1;
-    const int x = (int)(r % oW); r /= oW;
-    const int y = (int)(r % oH); r /= oH;
-    const int k = (int)(r % chunks);
-    const int f = (int)(r / chunks);
-    const float* p = in + ((size_t)f * in_chunks + k) * ich + ((size_t)(2 * y + ip) * iWp + 2 * x + ip) * 8 + 4 * half;
-    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 8);
-    const f32x4 c = *(const f32x4*)(p + (size_t)iWp * 8), d = *(const f32x4*)(p + (size_t)iWp * 8 + 8);
-    f32x4 m;
+  const float* p = in + ((size_t)f * in_chunks + k) * ich + (size_t)((2 * y + ip) * iWp + 2 * x + ip) * 8 + 4 * half;
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 8);
+  const f32x4 c = *(const f32x4*)(p + (size_t)iWp * 8), d = *(const f32x4*)(p + (size_t)iWp * 8 + 8);
+  f32x4 m;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) m[e] = fmaxf(fmaxf(a[e], b[e]), fmaxf(c[e], d[e]));
-    *(f32x4*)(out + ((size_t)f * out_chunks + k) * och + ((size_t)(y + op) * oWp + x + op) * 8 + 4 * half) = m;
-  }
+  for (int e = 0; e < 4; ++e) m[e] = fmaxf(fmaxf(a[e], b[e]), fmaxf(c[e], d[e]));
+  *(f32x4*)(out + ((size_t)f * out_chunks + k) * och + (size_t)((y + op) * oWp + x + op) * 8 + 4 * half) = m;
 }
 
 hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s) {
   const int chunks = (C + 7) / 8;
-  const long long total = (long long)out.n * chunks * out.H * out.W * 2;
-  const int grid = (int)std::min<long long>((total + 255) / 256, 256 * 16);
-  hipLaunchKernelGGL(maxpool2_kernel, dim3(grid), dim3(256), 0, s, in.base, in.pad, in.H, in.W, out.base, out.pad,
-                     out.H, out.W, chunks, in.cs / 8, out.cs / 8, in.n);
+  const long long per_plane = (long long)out.H * out.W * 2;
+  if (per_plane > 0x7fffffffLL || (long long)out.n * chunks > 65535) {
+    set_error("maxpool2: plane too large");
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(maxpool2_kernel, dim3((unsigned)((per_plane + 255) / 256), out.n * chunks), dim3(256), 0, s,
+                     in.base, in.pad, in.H, in.W, out.base, out.pad, out.H, out.W, chunks, in.cs / 8, out.cs / 8);
   return hipGetLastError();
 }
 

@@ -213,8 +213,11 @@ template <typename T>
 __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ planes, int H, int W, int words,
                                                         unsigned long long* __restrict__ mask, double thre,
                                                         int mode_hand) {
+  // one LDS tile: v (axis-0 result), then g written in place over it (the
+  // horizontal pass holds its v run in registers across a barrier) -> 31 KB,
+  // so 4 blocks fit a CU and hide each other's load latency
   __shared__ double s_v[NMS_VR][NMS_VC];
-  __shared__ double s_g[NMS_VR][NMS_GC];
+  double (*s_g)[NMS_VC] = s_v;
   const int plane = blockIdx.z;
   const int y0 = blockIdx.y * NMS_TY, x0 = blockIdx.x * NMS_TX;
   const T* src = planes + (size_t)plane * H * W;
@@ -237,11 +240,15 @@ __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ pla
   // axis 1, same recurrence along the row
   {
     constexpr int SEGS = (NMS_GC + NMS_SEG - 1) / NMS_SEG;   // 14 runs per row, 252 threads
-    if (tid < NMS_VR * SEGS) {
-      const int r = tid / SEGS, c0 = (tid - r * SEGS) * NMS_SEG;
-      double v[NMS_SEG + 2 * NMS_R];
+    const bool act = tid < NMS_VR * SEGS;
+    const int r = tid / SEGS, c0 = (tid - r * SEGS) * NMS_SEG;
+    double v[NMS_SEG + 2 * NMS_R];
+    if (act) {
 #pragma unroll
       for (int k = 0; k < NMS_SEG + 2 * NMS_R; ++k) v[k] = c0 + k < NMS_VC ? s_v[r][c0 + k] : 0.0;
+    }
+    __syncthreads();   // every v run is in registers: g may overwrite the tile
+    if (act) {
 #pragma unroll
       for (int k = 0; k < NMS_SEG; ++k) {
         double o = v[k + NMS_R] * kGauss[0];

@@ -17,7 +17,7 @@ import json
 import os
 
 
-NET_KERNELS = ("conv_mfma", "wino_f23", "maxpool")
+NET_KERNELS = ("conv_mfma", "wino_f23", "maxpool", "conv_x3", "wino_x3")
 
 
 def load(d, name):
@@ -64,9 +64,12 @@ def main():
         t = {"hbm_bytes_per_net_run": res["net_run"]["hbm_bytes_per_step"],
              "source": os.path.relpath(a.out),
              "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KiB->B; per bench step "
-                     "(one net run over the batch) and per launch of the Winograd kernel"}
-        if "wino_f23_mfma" in res:
-            t["wino_hbm_bytes_per_launch"] = res["wino_f23_mfma"]["hbm_bytes_per_launch"]
+                     "(one net run over the batch) and per launch (averaged over the net's launches) of each conv kernel"}
+        for cls, key in (("wino_f23_mfma", "wino"), ("conv_x3_f16", "x3"), ("conv_mfma_f32", "direct"),
+                         ("wino_x3_f16", "wino_x3")):
+            if cls in res:
+                t[key + "_hbm_bytes_per_launch"] = res[cls]["hbm_bytes_per_launch"]
+                t[key + "_dispatches"] = res[cls]["dispatches"]
         json.dump(t, open(a.traffic_out, "w"), indent=1)
     for k, v in res.items():
         print("%-40s read %10.1f MB  write %10.1f MB" % (k, v["read_bytes_per_step"] / 1e6, v["write_bytes_per_step"] / 1e6))

@@ -214,7 +214,38 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     }
   };
 
-  if constexpr ((VAR & 1) == 0) {
+  // ablation (VAR & 64): input rows by LDS-DMA too, raw fp32 halves as if they
+  // were pre-split fp16 planes (wrong numbers, right traffic): what a split
+  // activation storage would buy
+  auto issue_x = [&](int t, int buf) __attribute__((always_inline)) {
+    const int c2 = t / KS, ky = t - c2 * KS;
+    const long long row = (long long)(La + (ky - P) * Wi - P);
+    f16x8* dst = smem + buf * BUF + WSLAB;
+    const int nch = (seg + 63) >> 6;
+    for (int q = wave_u; q < 4 * nch; q += NWAVES) {
+      const int run = q / nch, ch = q - run * nch;          // run = hl*2 + h
+      const int hl = run >> 1, hh = run & 1;
+      const int c = min(2 * c2 + hh, a.cin_chunks - 1);
+      const int px = min(ch * 64 + lane, seg - 1);
+      const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + px) * 8 + 4 * hl;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(dst + run * SEGP + ch * 64), 16, 0, 0);
+    }
+  };
+  if constexpr ((VAR & 64) != 0) {
+    issue_w(0, 0);
+    issue_x(0, 0);
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < T) {
+        issue_w(t + 1, buf ^ 1);
+        issue_x(t + 1, buf ^ 1);
+      }
+      compute(buf);
+      __syncthreads();
+    }
+  } else if constexpr ((VAR & 1) == 0) {
     // weights by LDS-DMA one step ahead, input rows register-staged one step ahead
     issue_w(0, 0);
     load_x(0);
@@ -414,20 +445,21 @@ static bool x3_small_tiles() {
   return v;
 }
 
-// Tile families.  3x3 / 1x1 layers: 512-pixel tiles (8-16 waves per block, one
+// Tile families.  3x3 / 1x1 layers: 512-pixel tiles (16 waves per block, one
 // block per CU): the weight slab of a K step is then shared by 4x the pixels,
 // which cut the L2->LDS bytes per FLOP ~2x and measured +10 % over the 128-pixel
-// tiles (r01).  7x7 layers keep 128-pixel tiles (their slab is 2.3x larger).
+// tiles (r01); 16 rather than 8 waves for the narrow (96/64/32-channel) tiles
+// +2-9 %.  7x7 layers keep 128-pixel tiles (their slab is 2.3x larger).
 template <int KS>
 static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   const int var = KS <= 3 ? x3_var() : 0;
   if constexpr (KS <= 3) {
     if (!x3_small_tiles() && var == 0) {
       switch (c.bco) {
-        case 128: return launch_t<KS, 2, 8, 2, 2, 0, 4>(c, s);
-        case 96: return launch_t<KS, 1, 8, 3, 2, 0, 2>(c, s);
-        case 64: return launch_t<KS, 1, 8, 2, 2, 0, 2>(c, s);
-        case 32: return launch_t<KS, 1, 8, 1, 2, 0, 2>(c, s);
+        case 128: return launch_t<KS, 2, 8, 2, 2, 0, 4>(c, s);   // 16 waves, 64co x 64px each
+        case 96: return launch_t<KS, 1, 16, 3, 1, 0, 4>(c, s);   // 16 waves, 96co x 32px
+        case 64: return launch_t<KS, 2, 8, 1, 2, 0, 4>(c, s);    // 16 waves, 32co x 64px
+        case 32: return launch_t<KS, 1, 16, 1, 1, 0, 4>(c, s);   // 16 waves, 32co x 32px
       }
     }
     if (var == 4 && c.bco == 128) return launch_t<KS, 2, 2, 2, 4, 3, 1>(c, s);
@@ -435,6 +467,9 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
     if (var == 6 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 1, 2>(c, s);
     if (var == 7 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 0, 2>(c, s);
     if (var == 8 && c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 1, 4>(c, s);
+    if (var == 64 && c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 64, 4>(c, s);
+    if (var == 64 && c.bco == 96) return launch_t<KS, 1, 8, 3, 2, 64, 2>(c, s);
+    if (var == 64 && c.bco == 64) return launch_t<KS, 1, 8, 2, 2, 64, 2>(c, s);
   }
   switch (c.bco) {
 #define X3_CASE(BC, WMS, WNS, WMM, WNN)                                                   \

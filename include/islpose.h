@@ -91,6 +91,22 @@ int isl_net_forward(isl_net* net, const float* d_x_nchw, int n, int h, int w,
 int isl_net_preprocess(isl_net* net, const uint8_t* d_frames, int n, int H, int W,
                        double scale, int* net_h, int* net_w, void* stream);
 
+/* A square (or any) sub-image of frame `frame`: pixels [y, y+h) x [x, x+w). */
+typedef struct {
+  int32_t frame, x, y, w, h;
+} isl_crop;
+
+/* Pre-processing of a batch of crops (Hand.__call__ on oriImg[y:y+h, x:x+w],
+ * src/hand.py:33-41; demo.py:36): crop i is resized by fx = fy =
+ * scale_times_box / h_i (the reference's `scale = x * boxsize / oriImg.shape[0]`)
+ * with OpenCV's INTER_CUBIC on the crop as its own image (borders replicated
+ * at the crop's edges), padded and normalised into slot i of the net input.
+ * Every crop must resize to the same padded net size (true for the hand
+ * pyramid: round(s * 368) for every crop width); otherwise ISL_E_ARG. */
+int isl_net_preprocess_crops(isl_net* net, const uint8_t* d_frames, int n_frames, int H, int W,
+                             const isl_crop* crops, int n_crops, double scale_times_box, int* net_h,
+                             int* net_w, void* stream);
+
 /* Run the network on the input buffer filled by isl_net_preprocess; outputs stay
  * in the arena (low-res, 8-channel chunks) for the post kernels, and are also
  * copied to d_out0/d_out1 (NCHW) when those are non-NULL. */

@@ -79,8 +79,13 @@ double wino_mfma_flops(const ConvLaunch& c);
 hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s);
 hipError_t launch_pack_nchw(const float* x, int n, int C, int h, int w, const Act& out, hipStream_t s);
 hipError_t launch_unpack_nchw(const Act& in, int coff, int C, float* y, hipStream_t s);
-hipError_t launch_preprocess(const uint8_t* frames, int n, int H, int W, double scale,
-                             int rh, int rw, const Act& out, hipStream_t s);
+// Pre-processing of a batch of images described by a device table of entries
+// (preprocess_entry: byte offset of the image in `frames`, its size, the
+// resized size and 1/fx); row_bytes = bytes per row of the frame array.
+hipError_t launch_preprocess_tab(const uint8_t* frames, long long row_bytes, const void* d_tab, int n,
+                                 const Act& out, hipStream_t s);
+size_t preprocess_entry_bytes();
+void preprocess_entry(void* dst, long long off, int sh, int sw, int rh, int rw, double scale);
 
 struct MapSrc {            // one single-stage cubic resize, sampled per output element
   const float* base;       // element (f, c, y, x) at base + f*fs + chan(c) + y*ys + x*xs,

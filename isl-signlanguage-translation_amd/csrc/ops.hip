@@ -1,5 +1,7 @@
 // Byte-moving kernels around the convolutions: 2x2 max-pool, NCHW <-> chunked
 // padded packing, and the frame pre-processing of Body/Hand.__call__.
+#include <cstring>
+
 #include "internal.h"
 
 namespace isl {
@@ -119,28 +121,37 @@ __device__ __forceinline__ void axis_tap(int d, double scale, int n, int idx[4],
   for (int k = 0; k < 4; ++k) idx[k] = min(max(s + k - 1, 0), n - 1);
 }
 
-__global__ void preprocess_kernel(const uint8_t* __restrict__ frames, int n, int H, int W, double scale_y,
-                                  double scale_x, int rh, int rw, int identity, float* __restrict__ out,
-                                  int op, int ocs, int ph, int pw) {
-  const long long total = (long long)n * ph * pw;
-  const int rowlen = rw * 3;
+// One image of a preprocess batch: a frame, or a crop of one (Hand.__call__ runs
+// on oriImg[y:y+w, x:x+w] views, demo.py:36 / ISL_Model_parameter.py:56).
+struct PreSrc {
+  long long off;       // byte offset of the image's (0, 0) pixel in the frame array
+  int sh, sw;          // image size
+  int rh, rw;          // resized size (cvRound(s * fx)); the rest of the net input is pad 128
+  double scale;        // source pixels per output pixel (1 / fx)
+};
+
+// `tab` (device) describes image f = blockIdx.y; `row` = bytes per source row (frame W * 3).
+__global__ void preprocess_kernel(const uint8_t* __restrict__ frames, const PreSrc* __restrict__ tab, long long row,
+                                  float* __restrict__ out, int op, int ocs, int ph, int pw) {
+  const int f = blockIdx.y;
+  const PreSrc t = tab[f];
+  const int rowlen = t.rw * 3;
   const int body = rowlen - rowlen % 8;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int x = (int)(i % pw);
-    const int y = (int)((i / pw) % ph);
-    const int f = (int)(i / ((long long)pw * ph));
+  const bool identity = t.rh == t.sh && t.rw == t.sw;
+  const uint8_t* img = frames + t.off;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ph * pw; i += gridDim.x * blockDim.x) {
+    const int y = i / pw, x = i - y * pw;
     float v[3];
-    if (y >= rh || x >= rw) {
+    if (y >= t.rh || x >= t.rw) {
       v[0] = v[1] = v[2] = 128.f / 256.f - 0.5f;
     } else if (identity) {
-      const uint8_t* p = frames + (((size_t)f * H + y) * W + x) * 3;
+      const uint8_t* p = img + (size_t)y * row + (size_t)x * 3;
       for (int c = 0; c < 3; ++c) v[c] = (float)p[c] / 256.f - 0.5f;
     } else {
       int xi[4], yi[4];
       float xc[4], yc[4];
-      axis_tap(x, scale_x, W, xi, xc);
-      axis_tap(y, scale_y, H, yi, yc);
+      axis_tap(x, t.scale, t.sw, xi, xc);
+      axis_tap(y, t.scale, t.sh, yi, yc);
       int ia[4], ib[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -151,8 +162,8 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ frames, int n, int
         int hz[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const uint8_t* row = frames + ((size_t)f * H + yi[k]) * W * 3 + c;
-          hz[k] = row[xi[0] * 3] * ia[0] + row[xi[1] * 3] * ia[1] + row[xi[2] * 3] * ia[2] + row[xi[3] * 3] * ia[3];
+          const uint8_t* r = img + (size_t)yi[k] * row + c;
+          hz[k] = r[xi[0] * 3] * ia[0] + r[xi[1] * 3] * ia[1] + r[xi[2] * 3] * ia[2] + r[xi[3] * 3] * ia[3];
         }
         int r;
         if (x * 3 + c < body) {
@@ -177,14 +188,22 @@ __global__ void preprocess_kernel(const uint8_t* __restrict__ frames, int n, int
   }
 }
 
-hipError_t launch_preprocess(const uint8_t* frames, int n, int H, int W, double scale, int rh, int rw,
-                             const Act& out, hipStream_t s) {
-  const int identity = (rh == H && rw == W);
-  const long long total = (long long)n * out.H * out.W;
-  const int grid = (int)std::min<long long>((total + 255) / 256, 256 * 32);
-  hipLaunchKernelGGL(preprocess_kernel, dim3(grid), dim3(256), 0, s, frames, n, H, W, 1.0 / scale, 1.0 / scale,
-                     rh, rw, identity, out.base, out.pad, out.cs, out.H, out.W);
+// `tab` is a device array of n PreSrc entries (one per image of the batch).
+hipError_t launch_preprocess_tab(const uint8_t* frames, long long row_bytes, const void* tab, int n, const Act& out,
+                                 hipStream_t s) {
+  if (n > 65535) { set_error("preprocess: batch too large"); return hipErrorInvalidValue; }
+  const int blocks = (int)std::min<long long>(((long long)out.H * out.W + 255) / 256, 1024);
+  hipLaunchKernelGGL(preprocess_kernel, dim3(blocks, n), dim3(256), 0, s, frames, (const PreSrc*)tab, row_bytes,
+                     out.base, out.pad, out.cs, out.H, out.W);
   return hipGetLastError();
+}
+
+size_t preprocess_entry_bytes() { return sizeof(PreSrc); }
+
+void preprocess_entry(void* dst, long long off, int sh, int sw, int rh, int rw, double scale) {
+  PreSrc t;
+  t.off = off; t.sh = sh; t.sw = sw; t.rh = rh; t.rw = rw; t.scale = scale;
+  memcpy(dst, &t, sizeof(t));
 }
 
 }  // namespace isl

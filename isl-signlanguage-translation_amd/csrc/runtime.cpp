@@ -213,6 +213,10 @@ struct isl_net {
   // conv algorithm (ISL_ALGO_*) and the split-fp16 range flag (isl_net_check)
   int algo = ISL_ALGO_X3;
   int* d_flag = nullptr;
+  // pre-processing image table (device, grow-only; refilled stream-ordered per call)
+  void* d_tab = nullptr;
+  size_t tab_bytes = 0;
+  std::vector<char> h_tab;
 };
 
 namespace isl {
@@ -744,6 +748,7 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_wux3) (void)hipFree(c.d_wux3);
   }
   if (net->d_flag) (void)hipFree(net->d_flag);
+  if (net->d_tab) (void)hipFree(net->d_tab);
   for (auto& kv : net->plans) (void)hipFree(kv.second.first);
   if (net->scratch) (void)hipFree(net->scratch);
   for (auto& r : net->timed)
@@ -805,16 +810,71 @@ int isl_net_forward(isl_net* net, const float* d_x, int n, int h, int w, float* 
   return copy_outputs(net, d_out0, d_out1, s);
 }
 
+// Upload the image table built in net->h_tab (stream-ordered; pageable source is staged by HIP).
+static int upload_tab(isl_net* net, hipStream_t s) {
+  const size_t bytes = net->h_tab.size();
+  if (bytes > net->tab_bytes) {
+    if (net->d_tab) HIP_OK(hipFree(net->d_tab));
+    net->d_tab = nullptr;
+    net->tab_bytes = 0;
+    HIP_OK(hipMalloc(&net->d_tab, bytes));
+    net->tab_bytes = bytes;
+  }
+  HIP_OK(hipMemcpyAsync(net->d_tab, net->h_tab.data(), bytes, hipMemcpyHostToDevice, s));
+  return ISL_OK;
+}
+
 int isl_net_preprocess(isl_net* net, const uint8_t* d_frames, int n, int H, int W, double scale, int* net_h,
                        int* net_w, void* stream) {
   if (!net || !d_frames || n <= 0 || H <= 0 || W <= 0 || !(scale > 0)) return fail(ISL_E_ARG, "bad argument");
   // cv::resize dsize from fx/fy: saturate_cast<int>(W*fx) = cvRound (half to even)
   const int rh = (int)std::nearbyint(H * scale), rw = (int)std::nearbyint(W * scale);
+  if (rh <= 0 || rw <= 0) return fail(ISL_E_ARG, "resized image is empty");
   const int ph = (rh + 7) / 8 * 8, pw = (rw + 7) / 8 * 8;  // padRightDownCorner (util.py:12-32)
   int rc = prepare(net);
   if (rc) return rc;
   if ((rc = plan(net, n, ph, pw))) return rc;
-  HIP_OK(launch_preprocess(d_frames, n, H, W, scale, rh, rw, net->act[net->in_buf], (hipStream_t)stream));
+  const size_t eb = preprocess_entry_bytes();
+  net->h_tab.resize(eb * n);
+  for (int f = 0; f < n; ++f)
+    preprocess_entry(net->h_tab.data() + eb * f, (long long)f * H * W * 3, H, W, rh, rw, 1.0 / scale);
+  hipStream_t s = (hipStream_t)stream;
+  if ((rc = upload_tab(net, s))) return rc;
+  HIP_OK(launch_preprocess_tab(d_frames, (long long)W * 3, net->d_tab, n, net->act[net->in_buf], s));
+  if (net_h) *net_h = ph;
+  if (net_w) *net_w = pw;
+  return ISL_OK;
+}
+
+int isl_net_preprocess_crops(isl_net* net, const uint8_t* d_frames, int n_frames, int H, int W,
+                             const isl_crop* crops, int n_crops, double scale_times_box, int* net_h, int* net_w,
+                             void* stream) {
+  if (!net || !d_frames || !crops || n_frames <= 0 || n_crops <= 0 || H <= 0 || W <= 0 || !(scale_times_box > 0))
+    return fail(ISL_E_ARG, "bad argument");
+  const size_t eb = preprocess_entry_bytes();
+  net->h_tab.resize(eb * n_crops);
+  int ph = 0, pw = 0;
+  for (int i = 0; i < n_crops; ++i) {
+    const isl_crop& c = crops[i];
+    if (c.frame < 0 || c.frame >= n_frames || c.x < 0 || c.y < 0 || c.w <= 0 || c.h <= 0 || c.x + c.w > W ||
+        c.y + c.h > H)
+      return fail(ISL_E_ARG, "crop " + std::to_string(i) + " outside its frame");
+    // Hand.__call__: scale = x * boxsize / oriImg.shape[0]; cv2.resize(fx=fy=scale) (hand.py:33-37)
+    const double m = scale_times_box / c.h;
+    const int rh = (int)std::nearbyint(c.h * m), rw = (int)std::nearbyint(c.w * m);
+    if (rh <= 0 || rw <= 0) return fail(ISL_E_ARG, "resized crop is empty");
+    const int h8 = (rh + 7) / 8 * 8, w8 = (rw + 7) / 8 * 8;
+    if (i == 0) { ph = h8; pw = w8; }
+    if (h8 != ph || w8 != pw) return fail(ISL_E_ARG, "crops resize to different net sizes: batch them separately");
+    const long long off = (((long long)c.frame * H + c.y) * W + c.x) * 3;
+    preprocess_entry(net->h_tab.data() + eb * i, off, c.h, c.w, rh, rw, 1.0 / m);
+  }
+  int rc = prepare(net);
+  if (rc) return rc;
+  if ((rc = plan(net, n_crops, ph, pw))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if ((rc = upload_tab(net, s))) return rc;
+  HIP_OK(launch_preprocess_tab(d_frames, (long long)W * 3, net->d_tab, n_crops, net->act[net->in_buf], s));
   if (net_h) *net_h = ph;
   if (net_w) *net_w = pw;
   return ISL_OK;

@@ -14,7 +14,7 @@ import ctypes
 import numpy as np
 
 from . import runtime as rt
-from .body import scale_geometry
+from .body import BOXSIZE, scale_geometry
 
 HAND_SCALES = (0.5, 1.0, 1.5, 2.0)
 
@@ -42,16 +42,55 @@ class HandEstimator:
             heats.append(heat)
         return geoms, heats
 
-    def post_maps(self, h, w, geoms, heats):
+    def post_maps(self, h, w, geoms, heats, out=None):
+        """isl_hand_post on low-res maps [n,22,h8,w8] per scale -> int64 [n,21,2]; with
+        `out` (a cuda tensor) the result is written there and not synchronised."""
         import torch
         n = heats[0].shape[0]
         ns = len(geoms)
-        out = torch.empty((n, 21, 2), dtype=torch.int64, device=heats[0].device)
+        dst = out if out is not None else torch.empty((n, 21, 2), dtype=torch.int64, device=heats[0].device)
         g = (rt.IslScaleGeom * ns)(*[rt.IslScaleGeom(*gg) for gg in geoms])
         hp = (ctypes.c_void_p * ns)(*[rt.ptr(t).value for t in heats])
-        rt.check(rt.lib().isl_hand_post(self.net.h, n, h, w, ns, g, hp, rt.ptr(out), rt.stream_handle()),
+        rt.check(rt.lib().isl_hand_post(self.net.h, n, h, w, ns, g, hp, rt.ptr(dst), rt.stream_handle()),
                  "isl_hand_post")
-        return out.cpu().numpy()
+        return None if out is not None else dst.cpu().numpy()
+
+    def estimate_crops(self, frames, boxes):
+        """Batched Hand.__call__ over crops of different sizes: frames uint8 [n,H,W,3]
+        (numpy or torch), boxes [(frame_index, x, y, w)] (util.handDetect's square boxes,
+        oriImg[y:y+w, x:x+w]) -> int64 [len(boxes), 21, 2] in crop coordinates, equal to
+        estimate() on each crop.  The 4 scales run as one batch of all crops each (every
+        crop resizes to round(s*368) px); the post runs per crop (its resize-back target
+        is the crop size)."""
+        import torch
+        if len(boxes) == 0:
+            return np.zeros((0, 21, 2), np.int64)
+        t = torch.as_tensor(np.ascontiguousarray(frames) if isinstance(frames, np.ndarray) else frames)
+        t = t.to("cuda:%d" % self.device).contiguous()
+        crops = [(f, x, y, w, w) for (f, x, y, w) in boxes]
+        n = len(crops)
+
+        def run():
+            heats, ref = [], None
+            for s in self.scale_search:
+                gh, gw = self.net.preprocess_crops(t, crops, s * BOXSIZE)
+                heat = torch.empty((n, 22, gh // 8, gw // 8), device=t.device)
+                self.net.run(heat)
+                heats.append(heat)
+            out = torch.empty((n, 21, 2), dtype=torch.int64, device=t.device)
+            # largest crop first: its post sizes the net's grow-only scratch once, so no
+            # later (queued) post reallocates it under an earlier one
+            for i in sorted(range(n), key=lambda k: -crops[k][3]):
+                w = crops[i][3]
+                geoms = [g[1:] for g in scale_geometry(w, w, self.scale_search)]
+                assert all((g[0], g[1]) == (hh.shape[2] * 8, hh.shape[3] * 8) for g, hh in zip(geoms, heats))
+                self.post_maps(w, w, geoms, [hh[i:i + 1] for hh in heats], out=out[i:i + 1])
+            return out.cpu().numpy()
+        peaks = run()
+        if not self.net.range_ok():
+            with self.net.algo_scope("direct"):
+                peaks = run()
+        return peaks
 
     def estimate(self, crops):
         """crops: uint8 [n,h,w,3] or one [h,w,3] (numpy or torch) -> int64 [n,21,2] / [21,2]."""

@@ -23,7 +23,7 @@ LIB_PATH = os.environ.get("ISLPOSE_LIB", os.path.join(os.path.dirname(os.path.ab
 EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destroy", "isl_net_param_count",
            "isl_net_param_info", "isl_net_set_param", "isl_net_forward", "isl_net_preprocess", "isl_net_run", "isl_net_debug_input",
            "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post",
-           "isl_net_set_algo", "isl_net_get_algo", "isl_net_check"]
+           "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops"]
 
 
 class IslCaps(ctypes.Structure):
@@ -39,6 +39,10 @@ class IslLayout(ctypes.Structure):
 class IslScaleGeom(ctypes.Structure):
     _fields_ = [("net_h", ctypes.c_int32), ("net_w", ctypes.c_int32),
                 ("valid_h", ctypes.c_int32), ("valid_w", ctypes.c_int32)]
+
+
+class IslCrop(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("frame", "x", "y", "w", "h")]
 
 
 class IslError(RuntimeError):
@@ -70,6 +74,8 @@ def lib():
     L.isl_net_run.argtypes = [vp, vp, vp, vp]
     L.isl_net_debug_input.argtypes = [vp, vp, vp]
     L.isl_net_set_timing.argtypes = [vp, i32]
+    L.isl_net_preprocess_crops.argtypes = [vp, vp, i32, i32, i32, ctypes.POINTER(IslCrop), i32, dbl,
+                                           ctypes.POINTER(i32), ctypes.POINTER(i32), vp]
     L.isl_net_set_algo.argtypes = [vp, i32]
     L.isl_net_get_algo.argtypes = [vp]
     L.isl_net_check.argtypes = [vp, i32]
@@ -217,6 +223,17 @@ class Net:
         nh, nw = ctypes.c_int32(), ctypes.c_int32()
         check(lib().isl_net_preprocess(self.h, ptr(frames_u8), n, H, W, float(scale), ctypes.byref(nh),
                                        ctypes.byref(nw), stream_handle(stream)), "isl_net_preprocess")
+        return nh.value, nw.value
+
+    def preprocess_crops(self, frames_u8, crops, scale_times_box: float, stream=None):
+        """frames uint8 [n,H,W,3] cuda; crops [(frame, x, y, w, h)] -> fills one net-input
+        slot per crop (Hand.__call__'s resize of each crop); returns (net_h, net_w)."""
+        n, H, W, _ = frames_u8.shape
+        arr = (IslCrop * len(crops))(*[IslCrop(*map(int, c)) for c in crops])
+        nh, nw = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().isl_net_preprocess_crops(self.h, ptr(frames_u8), n, H, W, arr, len(crops), float(scale_times_box),
+                                             ctypes.byref(nh), ctypes.byref(nw), stream_handle(stream)),
+              "isl_net_preprocess_crops")
         return nh.value, nw.value
 
     def debug_input(self, n, h, w, stream=None):

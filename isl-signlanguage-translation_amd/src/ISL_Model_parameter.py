@@ -68,11 +68,26 @@ class ISLSignPos(object):
     __call__ = call
 
     def call_batch(self, frames):
-        """frames uint8 [n, H, W, 3] -> [(candidate, subset, all_hand_peaks)] * n."""
-        frames = _as_numpy(frames)
-        body, _ = self._estimators()
-        res = body.estimate(np.ascontiguousarray(frames, dtype=np.uint8))
-        return [(c, s, self._hands(frames[i], c, s)) for i, (c, s) in enumerate(res)]
+        """frames uint8 [n, H, W, 3] -> [(candidate, subset, all_hand_peaks)] * n, equal to
+        call() per frame.  The body runs as one batch; every hand crop of the batch
+        (util.handDetect boxes, in the reference's order) runs as one batch per scale."""
+        frames = np.ascontiguousarray(_as_numpy(frames), dtype=np.uint8)
+        body, hand = self._estimators()
+        t = torch.from_numpy(frames).to("cuda:%d" % body.device)
+        res = body.estimate(t)
+        boxes, owner = [], []
+        for i, (c, s) in enumerate(res):
+            for x, y, w, _is_left in util.handDetect(c, s, frames[i]):
+                boxes.append((i, x, y, w))
+                owner.append(i)
+        peaks = hand.estimate_crops(t, boxes)
+        out = [(c, s, []) for (c, s) in res]
+        for (i, x, y, _w), pk in zip(boxes, peaks):
+            pk = pk.copy()
+            pk[:, 0] = np.where(pk[:, 0] == 0, pk[:, 0], pk[:, 0] + x)   # ISL_Model_parameter.py:56-59
+            pk[:, 1] = np.where(pk[:, 1] == 0, pk[:, 1], pk[:, 1] + y)
+            out[i][2].append(pk)
+        return out
 
 
 class ISLSignPosTranslator(object):

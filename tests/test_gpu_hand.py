@@ -56,3 +56,31 @@ def test_hand_estimate_end_to_end(hest):
         ref = cpu_ref.hand_call(crops[i], lambda im: next(maps)[None])
         assert np.array_equal(got[i], ref)
     assert np.array_equal(hest.estimate(crops[0]), got[0])
+
+
+def test_crop_preprocess_bit_exact(hest):
+    """isl_net_preprocess_crops: each crop resized as its own image (borders replicated at
+    the crop edge) == the oracle's net_input on the cut-out crop, bit for bit."""
+    frames = synth.synth_frames(2, 120, 160, seed=17)
+    t = torch.from_numpy(frames).cuda()
+    boxes = [(0, 10, 5, 60), (1, 100, 60, 60), (0, 0, 0, 37), (1, 123, 83, 37)]
+    for s in HAND_SCALES:
+        same = [b for b in boxes if b[3] == 60]
+        nh, nw = hest.net.preprocess_crops(t, [(f, x, y, w, w) for f, x, y, w in same], s * 368)
+        got = hest.net.debug_input(len(same), nh, nw).cpu().numpy()
+        for i, (f, x, y, w) in enumerate(same):
+            ref, _, _ = cpu_ref.net_input(np.ascontiguousarray(frames[f, y:y + w, x:x + w]), s * 368 / w)
+            assert ref.shape[2:] == (nh, nw)
+            assert np.array_equal(got[i:i + 1], ref), (s, i)
+
+
+def test_estimate_crops_matches_per_crop(hest):
+    """Batched crops of different sizes (one batch per scale) == estimate() per crop."""
+    frames = synth.synth_frames(3, 160, 200, seed=23)
+    boxes = [(0, 20, 30, 96), (1, 0, 0, 40), (2, 104, 64, 96), (0, 150, 100, 50), (1, 33, 71, 77)]
+    got = hest.estimate_crops(frames, boxes)
+    assert got.shape == (5, 21, 2) and got.dtype == np.int64
+    for (f, x, y, w), pk in zip(boxes, got):
+        ref = hest.estimate(np.ascontiguousarray(frames[f, y:y + w, x:x + w]))
+        assert np.array_equal(pk, ref), (f, x, y, w)
+    assert hest.estimate_crops(frames, []).shape == (0, 21, 2)

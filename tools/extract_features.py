@@ -1,0 +1,89 @@
+"""Config 5 driver: dataset CSV of videos -> per-frame keypoint JSON + feature CSVs,
+one process per GPU (the MI355X form of the reference's extract_features_mp.py).
+
+  # 1 GPU
+  python tools/extract_features.py --csv sample.csv --dataset-base data/ --out features/
+  # 8 GPUs of one node (videos sharded across ranks, no collective on the data path)
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+      tools/extract_features.py --csv sample.csv --dataset-base data/ --out features/
+
+Videos are .npy uint8 [T,H,W,3] RGB arrays (pims / torchvision.io are absent from
+this image); --synthetic T,H,W makes seeded frames for a throughput run.
+Weights: --body-weights / --hand-weights flat caffe-named dicts (torch.load,
+weights_only=True), or synthetic weights when omitted.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "isl-signlanguage-translation_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--csv", help="dataset CSV with Filepath,type,expression columns")
+    ap.add_argument("--dataset-base", default=".")
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--body-weights")
+    ap.add_argument("--hand-weights")
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--synthetic", help="T,H,W: synthetic videos instead of .npy files")
+    ap.add_argument("--videos", type=int, default=4, help="number of synthetic videos (without --csv)")
+    ap.add_argument("--no-resume", action="store_true")
+    ap.add_argument("--no-json", action="store_true", help="skip per-frame JSON files (throughput runs)")
+    ap.add_argument("--no-export", action="store_true",
+                    help="leave out the get_bodypose/get_handpose columns (the reference raises on >2 hands there)")
+    a = ap.parse_args()
+
+    import torch
+    from islpose import pipeline, synth
+    from islpose.parallel import dist_env
+
+    rank, local, world = dist_env()
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")          # host-side gather of per-frame results only
+    torch.cuda.set_device(local)
+
+    from src.body import Body
+    from src.hand import Hand
+    from src.ISL_Model_parameter import ISLSignPos
+
+    def weights(path, kind):
+        if path:
+            return path
+        return {k: torch.from_numpy(v) for k, v in synth.synth_weights(kind).items()}
+
+    body = Body(weights(a.body_weights, 0), "body25")
+    hand = Hand(weights(a.hand_weights, 2))
+    model = ISLSignPos(body.model, hand.model)
+
+    if a.synthetic:
+        T, H, W = (int(v) for v in a.synthetic.split(","))
+        decode = pipeline.synthetic_decoder(T, H, W)
+    else:
+        decode = pipeline.npy_decoder(a.dataset_base)
+    rows = pipeline.read_dataset_csv(a.csv) if a.csv else \
+        [{"Filepath": "synthetic/v%03d.npy" % i, "type": "synthetic", "expression": "e%d" % (i % 4)}
+         for i in range(a.videos)]
+
+    t0 = time.time()
+    merged, stats = pipeline.run(rows, decode, model, a.out, rank, world, batch=a.batch,
+                                 resume=not a.no_resume, write_json=not a.no_json, group=group,
+                                 export=not a.no_export)
+    stats["frames_per_s"] = stats["frames"] / max(time.time() - t0, 1e-9)
+    print(json.dumps(stats))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -19,6 +19,7 @@
 // the file is built with -ffp-contract=off so no FMA is formed.
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -642,28 +643,46 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds) {
 // map_ori with every other pixel zeroed.  One workgroup per (crop, part).
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ int ld_parent(const int* p, int x) {
-  return __hip_atomic_load(p + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// parent arrays live in LDS (planes up to CC_LDS_MAX pixels: workgroup-scope
+// atomics, ds_* instructions) or in global scratch (agent scope)
+typedef __attribute__((address_space(3))) int lds_int;
+template <typename PT> struct UfScope { static constexpr int v = __HIP_MEMORY_SCOPE_AGENT; };
+template <> struct UfScope<lds_int*> { static constexpr int v = __HIP_MEMORY_SCOPE_WORKGROUP; };
+
+template <typename PT>
+__device__ __forceinline__ int ld_parent(PT p, int x) {
+  return __hip_atomic_load(p + x, __ATOMIC_RELAXED, UfScope<PT>::v);
 }
 
-__device__ int uf_find(int* parent, int x) {
-  int p = ld_parent(parent, x);
-  while (p != x) {
-    x = p;
-    p = ld_parent(parent, x);
+// find with path halving: a non-root's parent is only ever replaced by one of its
+// ancestors (halving stores here; the union CAS only touches roots), so the
+// relaxed stores are race-safe and chains stay short.  Without it a plane that
+// is one big component (random weights) built O(P)-long chains: 7 ms per crop.
+template <typename PT>
+__device__ int uf_find(PT parent, int x) {
+  while (true) {
+    const int p = ld_parent(parent, x);
+    if (p == x) return x;
+    const int gp = ld_parent(parent, p);
+    if (gp == p) return p;
+    __hip_atomic_store(parent + x, gp, __ATOMIC_RELAXED, UfScope<PT>::v);
+    x = gp;
   }
-  return x;
 }
 
 // lock-free union: hook the larger root under the smaller with a CAS, so the
 // final root of every component is its smallest raster index (= label order).
-__device__ void uf_union(int* parent, int a, int b) {
+template <typename PT>
+__device__ void uf_union(PT parent, int a, int b) {
   while (true) {
     a = uf_find(parent, a);
     b = uf_find(parent, b);
     if (a == b) return;
     if (a < b) { const int t = a; a = b; b = t; }
-    if (atomicCAS(parent + a, a, b) == a) return;
+    int expected = a;
+    if (__hip_atomic_compare_exchange_strong(parent + a, &expected, b, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             UfScope<PT>::v))
+      return;
   }
 }
 
@@ -714,6 +733,76 @@ __device__ double np_pairwise(const double* a, int n) {
   return ret;
 }
 
+// numpy's leaf: < 8 sequential from 0; <= 128: 8 accumulators, then the tail
+__device__ __forceinline__ double np_leaf(const double* x, int len) {
+  if (len < 8) {
+    double res = 0.0;
+    for (int i = 0; i < len; ++i) res += x[i];
+    return res;
+  }
+  double r[8];
+  for (int k = 0; k < 8; ++k) r[k] = x[k];
+  int i = 8;
+  for (; i < len - (len % 8); i += 8)
+    for (int k = 0; k < 8; ++k) r[k] += x[i + k];
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < len; ++i) res += x[i];
+  return res;
+}
+
+// Block-cooperative np.sum with numpy's exact association (same result as np_sum):
+// per 8192-element buffer, thread 0 lists the leaves of the split tree, the block
+// sums the leaves in parallel, thread 0 combines them in tree order.  Every thread
+// of the block must call it; the result is returned to all of them.
+__device__ double np_sum_block(const double* a, int n) {
+  constexpr int MAXL = 128;   // leaves of an 8192-element tree have 65..128 elements
+  __shared__ int s_loff[MAXL], s_llen[MAXL], s_nl;
+  __shared__ double s_lsum[MAXL];
+  __shared__ double s_tot;
+  const int tid = threadIdx.x;
+  for (int i0 = 0; i0 < n; i0 += 8192) {
+    const int len0 = min(8192, n - i0);
+    if (tid == 0) {   // pre-order leaf list
+      int st_off[32], st_len[32], sp = 0, nl = 0;
+      st_off[0] = i0; st_len[0] = len0;
+      while (sp >= 0) {
+        const int off = st_off[sp], len = st_len[sp];
+        --sp;
+        if (len <= 128) { s_loff[nl] = off; s_llen[nl] = len; ++nl; continue; }
+        int n2 = len / 2;
+        n2 -= n2 % 8;
+        ++sp; st_off[sp] = off + n2; st_len[sp] = len - n2;   // right pushed first: left pops first
+        ++sp; st_off[sp] = off; st_len[sp] = n2;
+      }
+      s_nl = nl;
+    }
+    __syncthreads();
+    for (int l = tid; l < s_nl; l += blockDim.x) s_lsum[l] = np_leaf(a + s_loff[l], s_llen[l]);
+    __syncthreads();
+    if (tid == 0) {   // post-order combination (left + right at every split)
+      struct F { int len, state; double left; };
+      F st[32];
+      int sp = 0, leaf = 0;
+      st[0] = {len0, 0, 0.0};
+      double ret = 0.0;
+      while (sp >= 0) {
+        F& f = st[sp];
+        if (f.len <= 128) { ret = s_lsum[leaf++]; --sp; continue; }
+        int n2 = f.len / 2;
+        n2 -= n2 % 8;
+        if (f.state == 0) { f.state = 1; st[++sp] = {n2, 0, 0.0}; }
+        else if (f.state == 1) { f.left = ret; f.state = 2; st[++sp] = {f.len - n2, 0, 0.0}; }
+        else { ret = f.left + ret; --sp; }
+      }
+      s_tot = i0 == 0 ? ret : s_tot + ret;
+    }
+    __syncthreads();
+  }
+  const double r = s_tot;
+  __syncthreads();
+  return r;
+}
+
 // np.sum of a contiguous float64 array: pairwise sums of 8192-element buffers, added left to right
 __device__ double np_sum(const double* a, int n) {
   double s = 0.0;
@@ -724,15 +813,22 @@ __device__ double np_sum(const double* a, int n) {
   return s;
 }
 
+constexpr int CC_LDS_MAX = 36864;   // plane pixels whose parent array fits LDS (144 KB)
+
+template <bool LDSP>
 __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__ planes,
                                                       const unsigned long long* __restrict__ mask, int h, int w,
                                                       int words, int* __restrict__ parent_all,
                                                       double* __restrict__ vals_all, long long* __restrict__ out) {
+  extern __shared__ int s_dyn[];
   const int plane = blockIdx.x;   // crop * 21 + part
   const int P = h * w, tid = threadIdx.x;
   const double* map = planes + (size_t)plane * P;
   const unsigned long long* mk = mask + (size_t)plane * h * words;
-  int* parent = parent_all + (size_t)plane * P;
+  typedef typename std::conditional<LDSP, lds_int*, int*>::type PT;
+  PT parent;
+  if constexpr (LDSP) parent = (lds_int*)s_dyn;
+  else parent = parent_all + (size_t)plane * P;
   double* vals = vals_all + (size_t)plane * P;
   auto bit = [&](int y, int x) -> bool { return (mk[(size_t)y * words + (x >> 6)] >> (x & 63)) & 1ull; };
   __shared__ int s_cnt;
@@ -774,14 +870,43 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
     if (ld_parent(parent, p) >= 0) parent[p] = uf_find(parent, p);
   __threadfence();
   __syncthreads();
-  // components in label order = roots in raster order; keep the first maximal sum
-  if (tid == 0) { s_best_root = -1; s_best_sum = 0.0; }
+  // np.argmax over the components' np.sum (hand.py:68-69): only components whose sum
+  // can be the maximum need numpy's exact pairwise order.  An order-free fp64 sum per
+  // root (atomics; relative error < 1e-12 for these sizes) finds the maximum M; the
+  // components with approx >= M*(1-1e-9) -- in practice one -- are the candidates, and
+  // only they are summed exactly, in label (= root raster) order, first max kept.
+  // (Random weights give hundreds of components per plane: one exact pass per
+  // component made this kernel 7 ms per crop.)  Sums are of values > thre > 0.
+  constexpr int MAXC = 64;
+  __shared__ int s_cand[MAXC];
+  __shared__ int s_ncand;
+  for (int p = tid; p < P; p += 256) vals[p] = 0.0;
+  __threadfence_block();
   __syncthreads();
-  for (int r0 = 0; r0 < P; ++r0) {
-    // next root (parent[r] == r) at or after r0, found cooperatively
+  for (int p = tid; p < P; p += 256) {
+    const int r = parent[p];
+    if (r >= 0) atomicAdd(&vals[r], map[p]);
+  }
+  __threadfence();
+  __syncthreads();
+  {
+    double m = -INFINITY;
+    for (int p = tid; p < P; p += 256)
+      if (parent[p] == p) m = fmax(m, vals[p]);
+    s_red_v[tid] = m;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (tid < off) s_red_v[tid] = fmax(s_red_v[tid], s_red_v[tid + off]);
+      __syncthreads();
+    }
+  }
+  const double thr_c = s_red_v[0] * (1.0 - 1e-9);
+  if (tid == 0) s_ncand = 0;
+  __syncthreads();
+  for (int r0 = 0; r0 < P;) {   // candidate roots in raster order
     int cand = 0x7fffffff;
     for (int p = r0 + tid; p < P; p += 256)
-      if (parent[p] == p) { cand = p; break; }
+      if (parent[p] == p && vals[p] >= thr_c) { cand = p; break; }
     s_scan[tid] = cand;
     __syncthreads();
     for (int off = 128; off > 0; off >>= 1) {
@@ -791,6 +916,36 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
     const int root = s_scan[0];
     __syncthreads();
     if (root == 0x7fffffff) break;
+    if (tid == 0) {
+      if (s_ncand < MAXC) s_cand[s_ncand] = root;
+      ++s_ncand;
+    }
+    __syncthreads();
+    r0 = root + 1;
+  }
+  const bool all_roots = s_ncand > MAXC;   // pathological ties: every component, exactly
+  if (tid == 0) { s_best_root = -1; s_best_sum = 0.0; }
+  __syncthreads();
+  for (int ci = 0, r0 = 0; all_roots ? r0 < P : ci < s_ncand; ++ci) {
+    int root;
+    if (all_roots) {
+      // next root (parent[r] == r) at or after r0, found cooperatively
+      int cand = 0x7fffffff;
+      for (int p = r0 + tid; p < P; p += 256)
+        if (parent[p] == p) { cand = p; break; }
+      s_scan[tid] = cand;
+      __syncthreads();
+      for (int off = 128; off > 0; off >>= 1) {
+        if (tid < off) s_scan[tid] = min(s_scan[tid], s_scan[tid + off]);
+        __syncthreads();
+      }
+      root = s_scan[0];
+      __syncthreads();
+      if (root == 0x7fffffff) break;
+      r0 = root + 1;
+    } else {
+      root = s_cand[ci];
+    }
     // compact this component's values in raster order
     int base = 0;
     for (int c0 = root; c0 < P; c0 += 256) {
@@ -808,12 +963,11 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
       base += s_scan[255];
       __syncthreads();
     }
-    if (tid == 0) {
-      const double s = np_sum(vals, base);
-      if (s_best_root < 0 || s > s_best_sum) { s_best_sum = s; s_best_root = root; }   // np.argmax: first max
-    }
+    __threadfence_block();
     __syncthreads();
-    r0 = root;   // loop increments past this root
+    const double sum = np_sum_block(vals, base);
+    if (tid == 0 && (s_best_root < 0 || sum > s_best_sum)) { s_best_sum = sum; s_best_root = root; }   // first max
+    __syncthreads();
   }
   // util.npmax on map_ori with the other labels zeroed: first raster-order maximum
   const int best = s_best_root;
@@ -1090,8 +1244,19 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
   dim3 gb((w + NMS_TX - 1) / NMS_TX, (h + NMS_TY - 1) / NMS_TY, n * nparts);
   hipLaunchKernelGGL(blur_nms_kernel<double>, gb, dim3(256), 0, s, (const double*)avg, h, w, words, mask, 0.05, 1);
   PHIP(hipGetLastError());
-  hipLaunchKernelGGL(hand_cc_kernel, dim3(n * nparts), dim3(256), 0, s, (const double*)avg, mask, h, w, words, parent,
-                     vals, (long long*)d_peaks);
+  if (h * w <= CC_LDS_MAX) {
+    static bool attr = false;
+    if (!attr) {
+      PHIP(hipFuncSetAttribute((const void*)hand_cc_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               CC_LDS_MAX * 4));
+      attr = true;
+    }
+    hipLaunchKernelGGL(hand_cc_kernel<true>, dim3(n * nparts), dim3(256), (size_t)h * w * 4, s, (const double*)avg,
+                       mask, h, w, words, parent, vals, (long long*)d_peaks);
+  } else {
+    hipLaunchKernelGGL(hand_cc_kernel<false>, dim3(n * nparts), dim3(256), 0, s, (const double*)avg, mask, h, w,
+                       words, parent, vals, (long long*)d_peaks);
+  }
   PHIP(hipGetLastError());
   return ISL_OK;
 }

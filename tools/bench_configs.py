@@ -1,0 +1,124 @@
+"""Throughput of the other BASELINE.json configs on one GPU (bench.py measures configs[1]).
+
+  C3  body_25 + handpose, batch 16 frames, 1 person and 2 hand crops per frame
+      (crop widths 120-200 px, Hand.__call__'s 4-scale pyramid 184/368/552/736):
+      body net (Mode R, scale 0.5 like the ISL scripts) + body post on designed
+      1-person maps + one batched hand pass over the 32 crops per step.
+  C4  body_25 4-scale pyramid (scale_search 0.5/1/1.5/2 -> nets 184x328 ... 736x1312),
+      batch 16 frames per GPU (128 over 8 GPUs, sharded), post on designed maps.
+
+Prints one JSON line per config: frames/s, ms per step and the conv TFLOP/s of the
+step (direct-conv FLOP count, HIP events around the whole step).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "isl-signlanguage-translation_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def conv_gflop(kind, h, w):
+    from islpose import netspec
+    g, H, W = 0.0, h, w
+    for c in netspec.convs_for(kind):
+        g += 2.0 * c.cout * c.cin * c.k * c.k * H * W / 1e9
+        if c.name in ("conv1_2", "conv2_2", "conv3_4"):
+            H, W = H // 2, W // 2
+    return g
+
+
+def timed(step, steps, warmup):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def c3(args):
+    from islpose import synth
+    from islpose.body import BodyEstimator, scale_geometry
+    from islpose.hand import HandEstimator, HAND_SCALES
+    B, H, W = args.batch, 368, 656
+    body = BodyEstimator(synth.synth_weights(0), "body25", scale_search=(0.5,))
+    hand = HandEstimator(synth.synth_weights(2))
+    frames = torch.from_numpy(synth.synth_frames(B, H, W, seed=5)).cuda()
+    (m, nh, nw, vh, vw), = scale_geometry(H, W, (0.5,))
+    maps = [synth.designed_pose_maps(nh // 8, nw // 8, 1, seed=i) for i in range(B)]
+    paf = torch.from_numpy(np.stack([a for a, _ in maps])).cuda()
+    heat = torch.from_numpy(np.stack([b for _, b in maps])).cuda()
+    rng = np.random.RandomState(0)
+    boxes = []
+    for f in range(B):
+        for _ in range(2):
+            w = int(rng.randint(120, 201))
+            boxes.append((f, int(rng.randint(0, W - w)), int(rng.randint(0, H - w)), w))
+
+    def step():
+        body.net.preprocess(frames, m)
+        body.net.run()
+        body.post_maps(H, W, [(nh, nw, vh, vw)], [paf], [heat], details=False)
+        hand.estimate_crops(frames, boxes)
+
+    sec = timed(step, args.steps, args.warmup)
+    gf = B * conv_gflop(0, nh, nw) + len(boxes) * sum(conv_gflop(2, s, s) for s in (184, 368, 552, 736))
+    return {"config": "C3 body_25 + hand (2 crops/frame, 4 scales)", "batch": B, "crops": len(boxes),
+            "frames_per_s": round(B / sec, 2), "ms_per_step": round(sec * 1e3, 2),
+            "conv_gflop_per_step": round(gf, 1), "conv_tflops_fp32_equiv_wall": round(gf / sec / 1e3, 1),
+            "hand_scales": list(HAND_SCALES)}
+
+
+def c4(args):
+    from islpose import synth
+    from islpose.body import BodyEstimator, scale_geometry
+    B, H, W = args.batch, 368, 656
+    scales = (0.5, 1.0, 1.5, 2.0)
+    body = BodyEstimator(synth.synth_weights(0), "body25", scale_search=scales)
+    frames = torch.from_numpy(synth.synth_frames(B, H, W, seed=6)).cuda()
+    geo = scale_geometry(H, W, scales)
+    pafs, heats = [], []
+    for i, g in enumerate(geo):
+        mp = [synth.designed_pose_maps(g[1] // 8, g[2] // 8, 3, seed=10 * i + k) for k in range(B)]
+        pafs.append(torch.from_numpy(np.stack([a for a, _ in mp])).cuda())
+        heats.append(torch.from_numpy(np.stack([b for _, b in mp])).cuda())
+    geoms = [g[1:] for g in geo]
+
+    def step():
+        for (m, nh, nw, vh, vw) in geo:
+            body.net.preprocess(frames, m)
+            body.net.run()
+        body.post_maps(H, W, geoms, pafs, heats, details=False)
+
+    sec = timed(step, args.steps, args.warmup)
+    gf = B * sum(conv_gflop(0, g[1], g[2]) for g in geo)
+    return {"config": "C4 body_25 4-scale pyramid", "batch_per_gpu": B, "nets": [[g[1], g[2]] for g in geo],
+            "frames_per_s": round(B / sec, 2), "ms_per_step": round(sec * 1e3, 2),
+            "conv_gflop_per_step": round(gf, 1), "conv_tflops_fp32_equiv_wall": round(gf / sec / 1e3, 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", choices=["c3", "c4", "all"], default="all")
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    a = ap.parse_args()
+    for name, fn in (("c3", c3), ("c4", c4)):
+        if a.config in (name, "all"):
+            print(json.dumps(fn(a)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -81,11 +81,12 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr int IT = (2 * SEGMAX + NT - 1) / NT; // staging items (h, px) per thread
   static_assert(WSLAB % 64 == 0, "weight slab is whole 1 KiB DMA pieces");
   static_assert(BPX <= SEGMAX, "segment must hold a tile");
-  static_assert(2 * BUF * 16 <= 160 * 1024, "LDS");
+  constexpr int NBUF = (VAR & 256) ? 3 : 2;        // VAR 256: 3-stage LDS-DMA ring
+  static_assert(NBUF * BUF * 16 <= 160 * 1024, "LDS");
   constexpr bool WEAVE = (VAR & 2) != 0;         // interleave the stores with the MFMAs
   constexpr bool NO_STAGE = (VAR & 8) != 0;      // ablation: skip global loads + LDS stores
   constexpr bool NO_MATH = (VAR & 16) != 0;      // ablation: skip LDS reads + MFMAs
-  __shared__ f16x8 smem[2 * BUF];
+  __shared__ f16x8 smem[NBUF * BUF];
 
   // XCD-aware tile order (conv.hip): co-tiles of a pixel tile, then neighbouring
   // pixel tiles, on one XCD / L2.
@@ -233,7 +234,52 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
                                        (__attribute__((address_space(3))) void*)(dst + run * SEGP + ch * 64), 16, 0, 0);
     }
   };
-  if constexpr ((VAR & 64) != 0) {
+  // ablation (VAR & 256): both operands by LDS-DMA (input as fake-split raw fp32)
+  // through a 3-buffer ring whose loads stay in flight ACROSS the barrier: every
+  // wave issues exactly DW + DX DMA pieces per step (count padded with harmless
+  // duplicate pieces), so a counted s_waitcnt vmcnt(DW + DX) retires step t while
+  // step t+1's pieces keep flying; raw s_barrier (no vmcnt(0) drain).
+  if constexpr ((VAR & 256) != 0) {
+    constexpr int DW = (WSLAB / 64 + NWAVES - 1) / NWAVES;
+    constexpr int NCH = (SEGMAX + 63) / 64;
+    constexpr int DX = (4 * NCH + NWAVES - 1) / NWAVES;
+    auto ring_issue = [&](int t, int buf) __attribute__((always_inline)) {
+      t = min(t, T - 1);      // past the end: duplicate of the last step (never read)
+      const f16x8* wsrc = a.wpk + ((size_t)co_t * T + t) * WSLAB;
+      f16x8* dst = smem + buf * BUF;
+#pragma unroll
+      for (int k = 0; k < DW; ++k) {
+        const int q = min(wave_u + k * NWAVES, WSLAB / 64 - 1);
+        __builtin_amdgcn_global_load_lds((const void*)(wsrc + q * 64 + lane),
+                                         (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
+      }
+      const int c2 = t / KS, ky = t - c2 * KS;
+      const long long row = (long long)(La + (ky - P) * Wi - P);
+      f16x8* xd = dst + WSLAB;
+#pragma unroll
+      for (int k = 0; k < DX; ++k) {
+        const int q = min(wave_u + k * NWAVES, 4 * NCH - 1);
+        const int run = q / NCH, ch = q - run * NCH;
+        const int hl = run >> 1, hh = run & 1;
+        const int c = min(2 * c2 + hh, a.cin_chunks - 1);
+        const int px = min(ch * 64 + lane, seg - 1);
+        const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + px) * 8 + 4 * hl;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(xd + run * SEGP + ch * 64), 16,
+                                         0, 0);
+      }
+    };
+    ring_issue(0, 0);
+    ring_issue(1, 1);
+    for (int t = 0; t < T; ++t) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DW + DX) : "memory");   // my pieces of step t landed
+      __builtin_amdgcn_s_barrier();                                     // everyone's; compute(t-1) done
+      ring_issue(t + 2, (t + 2) % 3);
+      compute(t % 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else if constexpr ((VAR & 64) != 0) {
     issue_w(0, 0);
     issue_x(0, 0);
     __syncthreads();
@@ -468,6 +514,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
     if (var == 6 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 1, 2>(c, s);
     if (var == 7 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 0, 2>(c, s);
     if (var == 8 && c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 1, 4>(c, s);
+    if (var == 256 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 256, 2>(c, s);
     if (var == 64 && c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 64, 4>(c, s);
     if (var == 64 && c.bco == 96) return launch_t<KS, 1, 8, 3, 2, 64, 2>(c, s);
     if (var == 64 && c.bco == 64) return launch_t<KS, 1, 8, 2, 2, 64, 2>(c, s);

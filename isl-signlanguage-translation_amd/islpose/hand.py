@@ -67,30 +67,37 @@ class HandEstimator:
             return np.zeros((0, 21, 2), np.int64)
         t = torch.as_tensor(np.ascontiguousarray(frames) if isinstance(frames, np.ndarray) else frames)
         t = t.to("cuda:%d" % self.device).contiguous()
-        crops = [(f, x, y, w, w) for (f, x, y, w) in boxes]
-        n = len(crops)
-
-        def run():
-            heats, ref = [], None
-            for s in self.scale_search:
-                gh, gw = self.net.preprocess_crops(t, crops, s * BOXSIZE)
-                heat = torch.empty((n, 22, gh // 8, gw // 8), device=t.device)
-                self.net.run(heat)
-                heats.append(heat)
-            out = torch.empty((n, 21, 2), dtype=torch.int64, device=t.device)
-            # largest crop first: its post sizes the net's grow-only scratch once, so no
-            # later (queued) post reallocates it under an earlier one
-            for i in sorted(range(n), key=lambda k: -crops[k][3]):
-                w = crops[i][3]
-                geoms = [g[1:] for g in scale_geometry(w, w, self.scale_search)]
-                assert all((g[0], g[1]) == (hh.shape[2] * 8, hh.shape[3] * 8) for g, hh in zip(geoms, heats))
-                self.post_maps(w, w, geoms, [hh[i:i + 1] for hh in heats], out=out[i:i + 1])
-            return out.cpu().numpy()
-        peaks = run()
+        peaks = self.post_crops(boxes, self.run_crops(t, boxes))
         if not self.net.range_ok():
             with self.net.algo_scope("direct"):
-                peaks = run()
+                peaks = self.post_crops(boxes, self.run_crops(t, boxes))
         return peaks
+
+    def run_crops(self, frames_t, boxes):
+        """The hand net over all crops, one batch per scale -> low-res heat [n,22,h8,w8] per scale."""
+        import torch
+        crops = [(f, x, y, w, w) for (f, x, y, w) in boxes]
+        heats = []
+        for s in self.scale_search:
+            gh, gw = self.net.preprocess_crops(frames_t, crops, s * BOXSIZE)
+            heat = torch.empty((len(crops), 22, gh // 8, gw // 8), device=frames_t.device)
+            self.net.run(heat)
+            heats.append(heat)
+        return heats
+
+    def post_crops(self, boxes, heats):
+        """isl_hand_post per crop (its resize-back target is the crop size) -> int64 [n,21,2]."""
+        import torch
+        n = len(boxes)
+        out = torch.empty((n, 21, 2), dtype=torch.int64, device=heats[0].device)
+        # largest crop first: its post sizes the net's grow-only scratch once, so no
+        # later (queued) post reallocates it under an earlier one
+        for i in sorted(range(n), key=lambda k: -boxes[k][3]):
+            w = boxes[i][3]
+            geoms = [g[1:] for g in scale_geometry(w, w, self.scale_search)]
+            assert all((g[0], g[1]) == (hh.shape[2] * 8, hh.shape[3] * 8) for g, hh in zip(geoms, heats))
+            self.post_maps(w, w, geoms, [hh[i:i + 1] for hh in heats], out=out[i:i + 1])
+        return out.cpu().numpy()
 
     def estimate(self, crops):
         """crops: uint8 [n,h,w,3] or one [h,w,3] (numpy or torch) -> int64 [n,21,2] / [21,2]."""

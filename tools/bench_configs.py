@@ -66,18 +66,27 @@ def c3(args):
             w = int(rng.randint(120, 201))
             boxes.append((f, int(rng.randint(0, W - w)), int(rng.randint(0, H - w)), w))
 
+    # designed hand maps for the post (random weights give dense maps: one giant component
+    # per plane, unlike real footage); the hand nets still run in full on every crop
+    hgeo = [(s * 368 // 8, s * 368 // 8) for s in (0.5, 1.0, 1.5, 2.0)]
+    hmaps = [torch.from_numpy(np.stack([synth.designed_hand_maps(int(hh), int(ww), seed=31 * i + k)
+                                        for i in range(len(boxes))])).cuda()
+             for k, (hh, ww) in enumerate(hgeo)]
+
     def step():
         body.net.preprocess(frames, m)
         body.net.run()
         body.post_maps(H, W, [(nh, nw, vh, vw)], [paf], [heat], details=False)
-        hand.estimate_crops(frames, boxes)
+        heats = hand.run_crops(frames, boxes)
+        hand.post_crops(boxes, hmaps if args.designed_hands else heats)
 
     sec = timed(step, args.steps, args.warmup)
     gf = B * conv_gflop(0, nh, nw) + len(boxes) * sum(conv_gflop(2, s, s) for s in (184, 368, 552, 736))
     return {"config": "C3 body_25 + hand (2 crops/frame, 4 scales)", "batch": B, "crops": len(boxes),
             "frames_per_s": round(B / sec, 2), "ms_per_step": round(sec * 1e3, 2),
             "conv_gflop_per_step": round(gf, 1), "conv_tflops_fp32_equiv_wall": round(gf / sec / 1e3, 1),
-            "hand_scales": list(HAND_SCALES)}
+            "hand_scales": list(HAND_SCALES),
+            "hand_post_on": "designed maps" if args.designed_hands else "raw net output (random weights: dense maps)"}
 
 
 def c4(args):
@@ -114,6 +123,8 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--raw-hand-maps", dest="designed_hands", action="store_false",
+                    help="C3: run the hand post on the raw net maps instead of designed maps")
     a = ap.parse_args()
     for name, fn in (("c3", c3), ("c4", c4)):
         if a.config in (name, "all"):

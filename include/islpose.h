@@ -186,6 +186,19 @@ int isl_body_post(isl_net* net, int n, int H, int W, int nscales, const isl_scal
 int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, const isl_scale_geom* geom,
                   const float* const* d_heat, int64_t* d_peaks, void* stream);
 
+/* Sign classifier of ISLSignPosTranslator (reference demo_isl_translate.py:72-100,
+ * applied in src/ISL_Model_parameter.py:337 to a [1,20,156] window of
+ * populate_features rows, :376-443): Masking(0) -> BatchNorm -> BiLSTM(32, seq)
+ * -> BiLSTM(32) -> elu -> Dense32 -> BN -> elu -> Dense32 -> BN -> elu ->
+ * Dense(n_classes) softmax, inference semantics (dropouts off, keras masking).
+ * d_params: float32, the keras `model.get_weights()` list flattened in order
+ * (isl_sign_param_count floats); d_windows: float32 [batch][window][n_features];
+ * d_probs: float32 [batch][n_classes].  window <= 32, n_features <= 256,
+ * n_classes <= 1024.  One workgroup per window, one launch per call. */
+int isl_sign_param_count(int n_features, int n_classes, int64_t* count);
+int isl_sign_classify(const float* d_params, int n_features, int window, int n_classes,
+                      const float* d_windows, int batch, float* d_probs, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,6 +19,9 @@ from .body import BOXSIZE, scale_geometry
 HAND_SCALES = (0.5, 1.0, 1.5, 2.0)
 
 
+CROP_CHUNK = 64     # hand crops per batched pass of estimate_crops
+
+
 class HandEstimator:
     def __init__(self, weights: dict = None, device: int = 0, scale_search=HAND_SCALES, net: "rt.Net" = None):
         self.device = device
@@ -67,11 +70,16 @@ class HandEstimator:
             return np.zeros((0, 21, 2), np.int64)
         t = torch.as_tensor(np.ascontiguousarray(frames) if isinstance(frames, np.ndarray) else frames)
         t = t.to("cuda:%d" % self.device).contiguous()
-        peaks = self.post_crops(boxes, self.run_crops(t, boxes))
-        if not self.net.range_ok():
-            with self.net.algo_scope("direct"):
-                peaks = self.post_crops(boxes, self.run_crops(t, boxes))
-        return peaks
+        out = []
+        # bounded batches: the 736 px scale costs ~0.4 GB of activations per crop
+        for c in range(0, len(boxes), CROP_CHUNK):
+            part = boxes[c:c + CROP_CHUNK]
+            peaks = self.post_crops(part, self.run_crops(t, part))
+            if not self.net.range_ok():
+                with self.net.algo_scope("direct"):
+                    peaks = self.post_crops(part, self.run_crops(t, part))
+            out.append(peaks)
+        return np.concatenate(out)
 
     def run_crops(self, frames_t, boxes):
         """The hand net over all crops, one batch per scale -> low-res heat [n,22,h8,w8] per scale."""

@@ -23,7 +23,8 @@ LIB_PATH = os.environ.get("ISLPOSE_LIB", os.path.join(os.path.dirname(os.path.ab
 EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destroy", "isl_net_param_count",
            "isl_net_param_info", "isl_net_set_param", "isl_net_forward", "isl_net_preprocess", "isl_net_run", "isl_net_debug_input",
            "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post",
-           "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops"]
+           "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops",
+           "isl_sign_param_count", "isl_sign_classify"]
 
 
 class IslCaps(ctypes.Structure):
@@ -85,6 +86,8 @@ def lib():
     L.isl_body_post.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp),
                                 ctypes.POINTER(vp), ctypes.POINTER(IslCaps), vp, vp]
     L.isl_hand_post.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp), vp, vp]
+    L.isl_sign_param_count.argtypes = [i32, i32, ctypes.POINTER(i64)]
+    L.isl_sign_classify.argtypes = [vp, i32, i32, i32, vp, i32, vp, vp]
     for name in EXPORTS[2:]:
         getattr(L, name).restype = i32
     if L.isl_abi_version() != 1:

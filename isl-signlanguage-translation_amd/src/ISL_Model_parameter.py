@@ -9,14 +9,22 @@ Everything runs on the GPU through libislpose; there is no keras dependency.
 
 ``call_batch(frames)`` runs the body path for a whole batch of frames at once.
 
-Out of scope: ``ISLSignPosTranslator`` (the Keras BiLSTM sign
-classifier, :308-689) and the ffmpeg ``Writer`` -- constructing them raises.
+``ISLSignPosTranslator(body_model, hand_model, translation_model)`` (:308-443)
+turns a 20-frame window into [1, 20, 156] ``populate_features`` rows and applies
+``translation_model`` -- a keras-free ``islpose.translate.SignClassifier`` (one
+HIP launch, csrc/sign.hip) or any callable taking that array.
+``translate_stream(frames)`` is the batched form of the demo's rolling-window loop
+(demo_isl_translate.py:170-197): keypoints once per frame, every window classified
+in one launch.
+
+Out of scope: the ffmpeg ``Writer`` -- constructing it raises.
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
 
+from islpose import translate
 from islpose.body import BodyEstimator
 from islpose.hand import HandEstimator
 
@@ -90,10 +98,60 @@ class ISLSignPos(object):
         return out
 
 
-class ISLSignPosTranslator(object):
-    def __init__(self, *args, **kwargs):
-        raise NotImplementedError("ISLSignPosTranslator (Keras BiLSTM sign classifier) is outside the MI355X "
-                                  "keypoint engine; use ISLSignPos for the keypoints")
+class ISLSignPosTranslator(ISLSignPos):
+    window_size = translate.WINDOW
+
+    def __init__(self, body_model, hand_model, translation_model):
+        super().__init__(body_model, hand_model)
+        self.model_type = 'body25'
+        self.translation_layer = translation_model
+
+    def populate_features(self, bodypose_circles, handpose_peaks):
+        return translate.populate_features(bodypose_circles, handpose_peaks)
+
+    def frame_features(self, candidate, subset, all_hand_peaks):
+        """One frame's 156-d row (ISL_Model_parameter.py:320-329): export tuples, then
+        populate_features.  More than two hands raises IndexError (get_handpose), as in
+        the reference."""
+        circles, _ = util.get_bodypose(candidate, subset, self.model_type)
+        _, peaks = util.get_handpose(all_hand_peaks)
+        return self.populate_features(circles, peaks)
+
+    def features(self, frames, batch: int = 32):
+        """[T, H, W, 3] uint8 BGR frames -> [T, 156] rows (body + hand keypoints in GPU batches)."""
+        frames = _as_numpy(frames)
+        rows = []
+        for s in range(0, len(frames), batch):
+            rows.extend(self.frame_features(*r) for r in self.call_batch(frames[s:s + batch]))
+        return np.array(rows, dtype=np.float64).reshape(len(rows), translate.N_FEATURES)
+
+    def call(self, window):
+        """ISL_Model_parameter.py:318-337: window [20, H, W, 3] -> translation_model of the
+        [1, 20, 156] feature window.  Shorter windows fail as in the reference, whose
+        padding branch reads ``.shape`` of a list (:331-333); longer ones fail its reshape."""
+        frames = _as_numpy(window)
+        feats = [self.frame_features(*r) for r in self.call_batch(frames)] if len(frames) else []
+        if len(feats) < self.window_size:
+            raise AttributeError("'list' object has no attribute 'shape'")
+        return self.translation_layer(np.array(feats).reshape(1, self.window_size, translate.N_FEATURES))
+
+    __call__ = call
+
+    def translate_stream(self, frames, batch: int = 32):
+        """Every full window of a clip: row s = translation_model(features[s:s+20]), the
+        result call(frames[s:s+20]) gives, for s = 0 .. T-20.  Keypoints run once per
+        frame instead of 20 times, and all windows go to the classifier together.
+        (The demo's loop classifies s >= 1: it fills the window before its first call.)"""
+        wins = translate.sliding_windows(self.features(frames, batch), self.window_size)
+        if len(wins) == 0:
+            return wins
+        return self.translation_layer(wins)
+
+    def frame_to_window(self, frame):
+        """ISL_Model_parameter.py:353-374: shift self.window by one and append frame
+        (self.window must have been set by the caller, as in the reference)."""
+        self.window[:-1] = self.window[1:]
+        self.window[-1] = frame
 
 
 class Writer(object):

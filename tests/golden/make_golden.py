@@ -2,7 +2,7 @@
 
 Run in the build container (needs /root/reference, read-only):
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [g9]
 
 The reference is imported from /root/reference with three shims for modules
 absent from this environment:
@@ -302,8 +302,47 @@ def g8_export_formats():
     json.dump(out, open(os.path.join(HERE, "g8_export_formats.json"), "w"))
 
 
+def g9_translator_features():
+    """ISLSignPosTranslator.populate_features (ISL_Model_parameter.py:376-443) on the
+    export tuples of G2 bodies and 0-2 random hands (§8f#4).  The module imports keras
+    and ffmpeg at the top; both get empty stand-ins here (populate_features uses
+    neither), the method is called unbound (it never reads self)."""
+    from src import util
+    keras = types.ModuleType("keras")
+    keras.Model = object
+    kl = types.ModuleType("keras.layers")
+    kl.TorchModuleWrapper = object
+    keras.layers = kl
+    sys.modules.setdefault("keras", keras)
+    sys.modules.setdefault("keras.layers", kl)
+    sys.modules.setdefault("ffmpeg", types.ModuleType("ffmpeg"))
+    from src.ISL_Model_parameter import ISLSignPosTranslator
+    z = np.load(os.path.join(HERE, "g2_body_post.npz"))
+    rng = np.random.RandomState(9)
+    out = []
+    for name in sorted({k.split("/")[0] for k in z.files}):
+        cand, subset = z[name + "/candidate"], z[name + "/subset"]
+        if cand.ndim != 2 or str(z[name + "/model_type"]) != "body25":
+            continue
+        for nh in (0, 1, 2):
+            hands = []
+            for _ in range(nh):
+                p = rng.randint(0, 400, size=(21, 2)).astype(np.int64)
+                p[rng.rand(21) < 0.2] = 0
+                hands.append(p)
+            circles, _ = util.get_bodypose(cand, subset, "body25")
+            _, peaks = util.get_handpose(hands)
+            feat = ISLSignPosTranslator.populate_features(None, circles, peaks)
+            out.append({"case": name, "hands": [h.tolist() for h in hands], "dtype": str(feat.dtype),
+                        "features": [float(v) for v in feat]})
+    json.dump(out, open(os.path.join(HERE, "g9_translator_features.json"), "w"))
+
+
 def main():
     install_shims()
+    if sys.argv[1:] == ["g9"]:
+        g9_translator_features()
+        return
     g7_state_dict_keys()
     g8_export_formats()
     shutil.copy(os.path.join(REF, "src/hand_model_output_size.json"),
@@ -312,6 +351,7 @@ def main():
     cases = g2_body_post()
     g4_hand_post()
     g5_hand_detect(cases)
+    g9_translator_features()
 
 
 if __name__ == "__main__":

@@ -7,6 +7,11 @@
   C4  body_25 4-scale pyramid (scale_search 0.5/1/1.5/2 -> nets 184x328 ... 736x1312),
       batch 16 frames per GPU (128 over 8 GPUs, sharded), post on designed maps.
 
+  C6  translator head: the HIP sign classifier (csrc/sign.hip) on [B, 20, 156]
+      windows -- latency of one window (the demo's per-frame call) and throughput
+      of a batch of 4096 windows; plus translate_stream over a 64-frame clip
+      (body + hands once per frame, 45 windows classified in one launch).
+
 Prints one JSON line per config: frames/s, ms per step and the conv TFLOP/s of the
 step (direct-conv FLOP count, HIP events around the whole step).
 """
@@ -117,16 +122,51 @@ def c4(args):
             "conv_gflop_per_step": round(gf, 1), "conv_tflops_fp32_equiv_wall": round(gf / sec / 1e3, 1)}
 
 
+def c6(args):
+    from islpose import synth, translate
+    from src.body import Body
+    from src.hand import Hand
+    from src.ISL_Model_parameter import ISLSignPosTranslator
+    clf = translate.SignClassifier()
+    rng = np.random.RandomState(0)
+    res = {"config": "C6 translator head (sign classifier + translate_stream)"}
+    for B in (1, 4096):
+        x = torch.from_numpy(rng.uniform(0, 600, (B, 20, 156)).astype(np.float32)).cuda()
+        out = torch.empty(B, clf.n_classes, device="cuda")
+        sec = timed(lambda: clf(x), args.steps * 10, args.warmup)
+        res["windows_%d_us" % B] = round(sec * 1e6, 1)
+        res["windows_%d_per_s" % B] = round(B / sec, 1)
+        del out
+    print(json.dumps(res), flush=True)
+    wts = lambda k: {n: torch.from_numpy(v) for n, v in synth.synth_weights(k).items()}  # noqa: E731
+    t = ISLSignPosTranslator(Body(wts(0), "body25").model, Hand(wts(2)).model, clf)
+    full = t.call_batch
+    n_hands = []
+
+    def two_hands(f):      # random weights detect many people; keep <= 2 hands per frame for the export
+        r = full(f)
+        n_hands.append(sum(len(h) for _, _, h in r))
+        return [(c, s, h[:2]) for c, s, h in r]
+    t.call_batch = two_hands
+    frames = synth.synth_frames(64, 368, 656, seed=4)
+    sec = timed(lambda: t.translate_stream(frames), args.steps, args.warmup)
+    res.update({"stream_frames": 64, "stream_windows": 45, "stream_ms": round(sec * 1e3, 1),
+                "stream_frames_per_s": round(64 / sec, 1),
+                "stream_hand_crops_per_clip": int(sum(n_hands) / (args.steps + args.warmup)),
+                "stream_note": "synthetic weights: hand crops per clip is set by the random body net"})
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", choices=["c3", "c4", "all"], default="all")
+    ap.add_argument("--config", choices=["c3", "c4", "c6", "all"], default="all")
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--raw-hand-maps", dest="designed_hands", action="store_false",
                     help="C3: run the hand post on the raw net maps instead of designed maps")
     a = ap.parse_args()
-    for name, fn in (("c3", c3), ("c4", c4)):
+    for name, fn in (("c3", c3), ("c4", c4), ("c6", c6)):
         if a.config in (name, "all"):
             print(json.dumps(fn(a)), flush=True)
 

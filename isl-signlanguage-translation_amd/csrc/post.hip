@@ -120,7 +120,7 @@ __device__ __forceinline__ float sample(const MapSrc& m, int f, int c, int y, in
 // horizontal pass is computed once per source row the tile needs (OpenCV's
 // HResizeCubic, stored in LDS), then every output combines 4 of those rows
 // (VResizeCubic) -- the same values OpenCV computes, with 4-5x fewer loads.
-constexpr int RS_TY = 8, RS_TX = 256, RS_MAXR = 40;
+constexpr int RS_TY = 32, RS_TX = 256, RS_MAXR = 40;   // 32 rows: amortise the horizontal pass
 __global__ void __launch_bounds__(256) resize_sep_kernel(MapSrc m, int nch, int oh, int ow, int ty_rows, int mode,
                                                           float inv_div_f, void* out) {
   __shared__ float s_h[RS_MAXR][RS_TX];
@@ -209,26 +209,153 @@ constexpr int NMS_GC = NMS_TX + 2;                 // g columns (194)
 constexpr int NMS_IR = NMS_VR + 2 * NMS_R;         // input rows (42)
 constexpr int NMS_SEG = 14;                        // g outputs per thread in the horizontal pass
 
+// Fused single-scale source (FUSED = true): the planes are not materialised; the
+// tile's input window is resized on the fly from the low-resolution map `m`
+// (stage-1 cv2.resize x8, cropped: body.py:68-73 when the net input is the frame),
+// with resize_sep_kernel's exact operation order.  Only scale 1/8 is fused.
+constexpr int NMS_SRC_ROWS = 16;
+constexpr int NMS_SRC_COLS = 40;                   // low-res columns (218 / 8 + 5 = 33 at scale 1/8)
+
+// [min, max] of reflect_idx(i, n) over i in [lo, hi]
+__device__ __forceinline__ void reflect_range(int lo, int hi, int n, int* a, int* b) {
+  if (hi - lo + 1 >= n) { *a = 0; *b = n - 1; return; }          // may wrap: take the whole line
+  if (lo < 0) { *a = 0; *b = max(hi, -lo - 1); return; }           // (one edge only: the window is < n)
+  if (hi >= n) { *a = min(lo, 2 * n - 1 - hi); *b = n - 1; return; }
+  *a = lo; *b = hi;
+}
+
+// low-res window [sr0, sr0+nsr) x [sc0, sc0+nsc) that the fused tile at (y0, x0) reads
+__device__ __forceinline__ void fused_window(const MapSrc& m, int H, int W, int y0, int x0, int* sr0, int* nsr,
+                                             int* sc0, int* nsc) {
+  // the window's rows / columns are reflect(y0-13 .. y0+28) / reflect(x0-13 .. x0+204);
+  // cubic taps are monotone in the index, so [taps(min)[0], taps(max)[3]] covers them
+  int rlo, rhi, clo, chi;
+  reflect_range(y0 - 1 - NMS_R, y0 - 2 - NMS_R + NMS_IR, H, &rlo, &rhi);
+  reflect_range(x0 - 1 - NMS_R, x0 - 2 - NMS_R + NMS_VC, W, &clo, &chi);
+  int t0[4], t1[4], u0[4], u1[4];
+  float dmy[4];
+  taps(rlo, m.scy, m.sh, t0, dmy);
+  taps(rhi, m.scy, m.sh, t1, dmy);
+  taps(clo, m.scx, m.sw, u0, dmy);
+  taps(chi, m.scx, m.sw, u1, dmy);
+  *sr0 = t0[0];
+  *nsr = t1[3] - t0[0] + 1;
+  *sc0 = u0[0];
+  *nsc = u1[3] - u0[0] + 1;
+}
+// Early out, exact: |resized| <= max|low| * (sum|cubic taps|)^2, and fp32 rounding is
+// covered by the 1.9 / 1.890625 margin; then |g| <= max|resized| * (1 + 1e-13).
+constexpr double CUBIC_ABS_SUM_SQ = 1.890625;      // max over t of (sum_k |cubic_k(t)|)^2, A = -0.75
+
 // planes: [n*nparts][H][W] (T = float or double); mask: [n*nparts][H][words]
-template <typename T>
-__global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ planes, int H, int W, int words,
-                                                        unsigned long long* __restrict__ mask, double thre,
-                                                        int mode_hand) {
+template <typename T, bool FUSED>
+__device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, int W, int words,
+                                          unsigned long long* __restrict__ mask, double thre, int mode_hand,
+                                          const MapSrc& m, int nch, int plane, int by, int bx) {
   // one LDS tile: v (axis-0 result), then g written in place over it (the
   // horizontal pass holds its v run in registers across a barrier) -> 31 KB,
   // so 4 blocks fit a CU and hide each other's load latency
   __shared__ double s_v[NMS_VR][NMS_VC];
+  __shared__ float s_hz[FUSED ? NMS_SRC_ROWS : 1][FUSED ? NMS_VC : 1];
+  __shared__ int4 s_ti[FUSED ? NMS_IR : 1];
+  __shared__ float s_low[FUSED ? NMS_SRC_ROWS : 1][FUSED ? NMS_SRC_COLS : 1];
+  __shared__ float4 s_tb[FUSED ? NMS_IR : 1];
+  __shared__ int s_live;
   double (*s_g)[NMS_VC] = s_v;
-  const int plane = blockIdx.z;
-  const int y0 = blockIdx.y * NMS_TY, x0 = blockIdx.x * NMS_TX;
-  const T* src = planes + (size_t)plane * H * W;
+  const int y0 = by * NMS_TY, x0 = bx * NMS_TX;
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_live = 0;
+  __syncthreads();
   // axis 0 (NI_Correlate1D, symmetric): o = c*w0; for j = 12..1: o += (a[-j] + a[+j]) * w[j]
-  if (tid < NMS_VC) {
-    const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
-    double in[NMS_IR];
+  double in[NMS_IR];
+  if constexpr (!FUSED) {
+    const T* src = planes + (size_t)plane * H * W;
+    if (tid < NMS_VC) {
+      const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
+      double amax = 0.0;
 #pragma unroll
-    for (int r = 0; r < NMS_IR; ++r) in[r] = (double)src[(size_t)reflect_idx(y0 - 1 - NMS_R + r, H) * W + xx];
+      for (int r = 0; r < NMS_IR; ++r) {
+        in[r] = (double)src[(size_t)reflect_idx(y0 - 1 - NMS_R + r, H) * W + xx];
+        amax = fmax(amax, fabs(in[r]));
+      }
+      // Early out, exact: every g of the tile is a positive-weight average (weights sum
+      // to 1) of these inputs, so |g| <= max|in| * (1 + 1e-13) in fp64.  When that stays
+      // below the threshold no pixel can pass `g > thre` and the tile's mask is zero.
+      if (amax >= thre * (1.0 - 1e-9)) s_live = 1;
+    }
+    __syncthreads();
+  } else {
+    const int f = plane / nch, c = plane - f * nch;
+    const float* b = m.base + (size_t)f * m.fs + chan_off(m, c);
+    int sr0, nsr, sc0, nsc;
+    fused_window(m, H, W, y0, x0, &sr0, &nsr, &sc0, &nsc);
+    if (nsr > NMS_SRC_ROWS) __builtin_trap();   // the host fuses only scale 1/8, tiles of 42 rows
+    // the low-res window is staged in LDS: one coalesced pass, reused by the resize
+    if (nsc > NMS_SRC_COLS) __builtin_trap();
+    float amax = 0.f;
+    for (int i = tid; i < nsr * nsc; i += 256) {
+      const int r = i / nsc, cc = i - r * nsc;
+      const float v = b[(size_t)(sr0 + r) * m.ys + (size_t)(sc0 + cc) * m.xs];
+      s_low[r][cc] = v;
+      amax = fmaxf(amax, fabsf(v));
+    }
+    if ((double)amax * 1.9 >= thre * (1.0 - 1e-9)) s_live = 1;
+    __syncthreads();
+    const bool s_live_lr = s_live != 0;
+    __syncthreads();   // everyone has read s_live before it is reused for the second bound
+    if (s_live_lr) {
+      if (tid < NMS_VC) {
+        // horizontal cubic pass for the window column (OpenCV HResizeCubic order)
+        const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
+        int xi[4];
+        float a[4];
+        taps(xx, m.scx, m.sw, xi, a);
+        const int i0 = xi[0] - sc0, i1 = xi[1] - sc0, i2 = xi[2] - sc0, i3 = xi[3] - sc0;
+        for (int r = 0; r < nsr; ++r) {
+          const float* row = s_low[r];
+          s_hz[r][tid] = ((row[i0] * a[0] + row[i1] * a[1]) + row[i2] * a[2]) + row[i3] * a[3];
+        }
+      } else {
+        // vertical taps of the window's 42 rows, once per block (the 38 idle lanes)
+        for (int r = tid - NMS_VC; r < NMS_IR; r += 256 - NMS_VC) {
+          int yi[4];
+          float be[4];
+          taps(reflect_idx(y0 - 1 - NMS_R + r, H), m.scy, m.sh, yi, be);
+          s_ti[r] = make_int4(yi[0] - sr0, yi[1] - sr0, yi[2] - sr0, yi[3] - sr0);
+          s_tb[r] = make_float4(be[0], be[1], be[2], be[3]);
+        }
+      }
+      if (tid == 0) s_live = 0;
+    }
+    __syncthreads();
+    if (s_live_lr && tid < NMS_VC) {
+      const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
+      const int rowlen = m.dw * m.cn;
+      const bool simd = xx * m.cn + c < rowlen - rowlen % 4;
+      double vmax = 0.0;
+#pragma unroll
+      for (int r = 0; r < NMS_IR; ++r) {
+        const int4 yi = s_ti[r];
+        const float4 be = s_tb[r];
+        const float h0 = s_hz[yi.x][tid], h1 = s_hz[yi.y][tid], h2 = s_hz[yi.z][tid], h3 = s_hz[yi.w][tid];
+        const float v = simd ? h0 * be.x + (h1 * be.y + (h2 * be.z + h3 * be.w))   // VResizeCubicVec_32f
+                             : ((h0 * be.x + h1 * be.y) + h2 * be.z) + h3 * be.w;
+        in[r] = (double)v;
+        vmax = fmax(vmax, fabs(in[r]));
+      }
+      if (vmax >= thre * (1.0 - 1e-9)) s_live = 1;   // the exact blur bound, as unfused
+    }
+    __syncthreads();
+  }
+  if (!s_live) {
+    for (int it = wave; it < NMS_TY * 3; it += 4) {
+      const int y = y0 + it / 3, wi = bx * 3 + it % 3;
+      if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = 0ull;
+    }
+    return;
+  }
+  if (tid < NMS_VC) {
 #pragma unroll
     for (int r = 0; r < NMS_VR; ++r) {
       double o = in[r + NMS_R] * kGauss[0];
@@ -261,7 +388,6 @@ __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ pla
   }
   __syncthreads();
   // one wave per (row, 64-column word) -> one 64-bit mask word
-  const int lane = tid & 63, wave = tid >> 6;
   for (int it = wave; it < NMS_TY * 3; it += 4) {
     const int ty = it / 3, wd = it - ty * 3;
     const int y = y0 + ty, cx = wd * 64 + lane, x = x0 + cx;
@@ -279,8 +405,69 @@ __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ pla
       }
     }
     const unsigned long long word = __ballot(pk);
-    const int wi = blockIdx.x * 3 + wd;
+    const int wi = bx * 3 + wd;
     if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = word;
+  }
+}
+
+template <typename T, bool FUSED>
+__global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ planes, int H, int W, int words,
+                                                        unsigned long long* __restrict__ mask, double thre,
+                                                        int mode_hand, MapSrc m, int nch, const int* __restrict__ live,
+                                                        const int* __restrict__ live_count, int tiles_x, int tiles_y) {
+  if constexpr (!FUSED) {
+    blur_tile<T, false>(planes, H, W, words, mask, thre, mode_hand, m, nch, blockIdx.z, blockIdx.y, blockIdx.x);
+  } else {
+    // grid-stride over the live tiles found by tile_live_kernel (mask pre-zeroed)
+    const int cnt = *live_count;
+    for (int k = blockIdx.x; k < cnt; k += gridDim.x) {
+      const int t = live[k];
+      const int bx = t % tiles_x, r = t / tiles_x, by = r % tiles_y, plane = r / tiles_y;
+      blur_tile<T, true>(planes, H, W, words, mask, thre, mode_hand, m, nch, plane, by, bx);
+      __syncthreads();   // LDS reuse by the next tile
+    }
+  }
+}
+
+// The low-res bound of the fused path for TL_TILES consecutive blur tiles per block
+// (one wave per tile at a time); live tiles are appended to `live` with one atomic
+// per block (order irrelevant: every tile owns its mask words).
+constexpr int TL_TILES = 64;
+__global__ void __launch_bounds__(256) tile_live_kernel(MapSrc m, int nch, int H, int W, int tiles_x, int tiles_y,
+                                                        int n_tiles, double thre, int* __restrict__ live,
+                                                        int* __restrict__ live_count) {
+  __shared__ int s_flag[TL_TILES];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int j = wave; j < TL_TILES; j += 4) {
+    const int t = blockIdx.x * TL_TILES + j;
+    int live_t = 0;
+    if (t < n_tiles) {
+      const int bx = t % tiles_x, r = t / tiles_x, by = r % tiles_y, plane = r / tiles_y;
+      const int f = plane / nch, c = plane - f * nch;
+      const float* b = m.base + (size_t)f * m.fs + chan_off(m, c);
+      int sr0, nsr, sc0, nsc;
+      fused_window(m, H, W, by * NMS_TY, bx * NMS_TX, &sr0, &nsr, &sc0, &nsc);
+      float amax = 0.f;
+      if (nsr > NMS_SRC_ROWS || nsc > NMS_SRC_COLS) __builtin_trap();   // host fuses scale 1/8 only
+      if (lane < nsc) {   // nsc <= NMS_SRC_COLS < 64: one column per lane, all rows in flight
+        const float* col = b + (size_t)(sc0 + lane) * m.xs + (size_t)sr0 * m.ys;
+#pragma unroll
+        for (int rr = 0; rr < NMS_SRC_ROWS; ++rr)
+          if (rr < nsr) amax = fmaxf(amax, fabsf(col[(size_t)rr * m.ys]));
+      }
+      for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+      live_t = (double)amax * 1.9 >= thre * (1.0 - 1e-9);
+    }
+    if (lane == 0) s_flag[j] = live_t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int fl = s_flag[lane];
+    const unsigned long long bal = __ballot(fl);
+    int base = 0;
+    if (lane == 0 && bal) base = atomicAdd(live_count, (int)__popcll(bal));
+    base = __shfl(base, 0);
+    if (fl) live[base + __popcll(bal & ((1ull << lane) - 1))] = blockIdx.x * TL_TILES + lane;
   }
 }
 
@@ -288,11 +475,13 @@ __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ pla
 // peak compaction: np.nonzero (row-major) order, one block per (frame, part)
 // ---------------------------------------------------------------------------
 
-template <typename T>
+// FUSED: scores sampled from the low-res map with the resize's arithmetic (the
+// full-resolution plane was never written; blur_nms_kernel<float, true>)
+template <typename T, bool FUSED>
 __global__ void __launch_bounds__(256) compact_kernel(const unsigned long long* __restrict__ mask,
                                                        const T* __restrict__ planes, int nparts, int H, int W,
                                                        int words, char* __restrict__ result, isl_layout lay,
-                                                       int max_peaks) {
+                                                       int max_peaks, MapSrc m) {
   const int f = blockIdx.y, part = blockIdx.x;
   const int plane = f * nparts + part;
   const unsigned long long* mk = mask + (size_t)plane * H * words;
@@ -336,7 +525,8 @@ __global__ void __launch_bounds__(256) compact_kernel(const unsigned long long* 
           double* p = peaks + (size_t)pos * 3;
           p[0] = (double)x;
           p[1] = (double)y;
-          p[2] = (double)src[(size_t)y * W + x];
+          if constexpr (FUSED) p[2] = (double)sample(m, f, part, y, x);
+          else p[2] = (double)src[(size_t)y * W + x];
         }
         ++pos;
       }
@@ -1034,6 +1224,11 @@ extern "C" int isl_body_layout(int model_kind, const isl_caps* caps, isl_layout*
 }
 
 
+static bool fused_blur_enabled() {
+  const char* e = getenv("ISLPOSE_FUSED_BLUR");   // A/B switch (tests); default on
+  return !(e && e[0] == '0');
+}
+
 static int post_fail(int code, const char* msg) {
   set_error(msg);
   return code;
@@ -1094,7 +1289,10 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   if (rc) return rc;
   // ---- scratch plan ----
   const bool multi = nscales > 1;
-  const size_t heat_bytes = (size_t)n * nparts * H * W * (multi ? 8 : 4);
+  // single scale with the net input at frame size (one x8 resize): fuse resize + blur,
+  // no full-resolution heat planes
+  const bool fused = !multi && geom[0].valid_h == H && geom[0].valid_w == W && fused_blur_enabled();
+  const size_t heat_bytes = fused ? 0 : (size_t)n * nparts * H * W * (multi ? 8 : 4);
   size_t mid_bytes = 0;
   for (int si = 0; si < nscales; ++si) {
     const isl_scale_geom& g = geom[si];
@@ -1104,8 +1302,11 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   const size_t mask_bytes = (size_t)n * nparts * H * words * 8;
   const size_t pair_bytes = (size_t)n * nlimbs * caps->max_pairs * (8 + 4 + 4);
   const size_t used_bytes = (size_t)n * nlimbs * 2 * caps->max_peaks;
+  const size_t n_tiles_all = (size_t)((W + NMS_TX - 1) / NMS_TX) * ((H + NMS_TY - 1) / NMS_TY) * n * nparts;
+  const size_t live_bytes = fused ? (n_tiles_all + 1) * sizeof(int) : 0;
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
-  const size_t total = up(heat_bytes) + up(mid_bytes) + up(mask_bytes) + up(pair_bytes) + up(used_bytes);
+  const size_t total = up(heat_bytes) + up(mid_bytes) + up(mask_bytes) + up(pair_bytes) + up(used_bytes) +
+                       up(live_bytes);
   char* base = (char*)net_scratch(net, total);
   if (!base) return ISL_E_HIP;
   char* heat = base;
@@ -1113,6 +1314,8 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   unsigned long long* mask = (unsigned long long*)(mid + up(mid_bytes));
   char* pairs = (char*)mask + up(mask_bytes);
   unsigned char* used = (unsigned char*)(pairs + up(pair_bytes));
+  int* live_count = (int*)(used + up(used_bytes));
+  int* live = live_count + 1;
 
   hipLaunchKernelGGL(init_records_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (char*)d_result, lay, n, nlimbs);
   PHIP(hipGetLastError());
@@ -1121,6 +1324,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   GroupArgs ga;
   memset(&ga, 0, sizeof(ga));
   char* midp = mid;
+  MapSrc fused_src{};
   const float div_f = (float)nscales;
   for (int si = 0; si < nscales; ++si) {
     const isl_scale_geom& g = geom[si];
@@ -1156,22 +1360,39 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       fh = lh;
       fp = lp;
     }
-    if ((rc = launch_resize(fh, n, nparts, H, W, multi ? 2 : 1, div_f, heat, s))) return rc;
+    if (fused) fused_src = fh;   // no full-resolution heat: blur_nms resizes on the fly
+    else if ((rc = launch_resize(fh, n, nparts, H, W, multi ? 2 : 1, div_f, heat, s))) return rc;
     ga.paf[si] = fp;
   }
   // blur + NMS (body.py:86-100)
   dim3 gb((W + NMS_TX - 1) / NMS_TX, (H + NMS_TY - 1) / NMS_TY, n * nparts);
   if (multi)
-    hipLaunchKernelGGL(blur_nms_kernel<double>, gb, dim3(256), 0, s, (const double*)heat, H, W, words, mask, 0.1, 0);
-  else
-    hipLaunchKernelGGL(blur_nms_kernel<float>, gb, dim3(256), 0, s, (const float*)heat, H, W, words, mask, 0.1, 0);
+    hipLaunchKernelGGL((blur_nms_kernel<double, false>), gb, dim3(256), 0, s, (const double*)heat, H, W, words, mask,
+                       0.1, 0, MapSrc{}, 0, nullptr, nullptr, 0, 0);
+  else if (fused) {
+    // live-tile list (low-res bound), then the fused blur over live tiles only
+    const int n_tiles = (int)(gb.x * gb.y * gb.z);
+    PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));
+    PHIP(hipMemsetAsync(live_count, 0, sizeof(int), s));
+    hipLaunchKernelGGL(tile_live_kernel, dim3((n_tiles + TL_TILES - 1) / TL_TILES), dim3(256), 0, s, fused_src, nparts, H, W, (int)gb.x,
+                       (int)gb.y, n_tiles, 0.1, live, live_count);
+    PHIP(hipGetLastError());
+    hipLaunchKernelGGL((blur_nms_kernel<float, true>), dim3(std::min(n_tiles, 256 * 8)), dim3(256), 0, s,
+                       (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts, live, live_count,
+                       (int)gb.x, (int)gb.y);
+  } else
+    hipLaunchKernelGGL((blur_nms_kernel<float, false>), gb, dim3(256), 0, s, (const float*)heat, H, W, words, mask,
+                       0.1, 0, MapSrc{}, 0, nullptr, nullptr, 0, 0);
   PHIP(hipGetLastError());
   if (multi)
-    hipLaunchKernelGGL(compact_kernel<double>, dim3(nparts, n), dim3(256), 0, s, mask, (const double*)heat, nparts, H,
-                       W, words, (char*)d_result, lay, caps->max_peaks);
+    hipLaunchKernelGGL((compact_kernel<double, false>), dim3(nparts, n), dim3(256), 0, s, mask, (const double*)heat,
+                       nparts, H, W, words, (char*)d_result, lay, caps->max_peaks, MapSrc{});
+  else if (fused)
+    hipLaunchKernelGGL((compact_kernel<float, true>), dim3(nparts, n), dim3(256), 0, s, mask, (const float*)nullptr,
+                       nparts, H, W, words, (char*)d_result, lay, caps->max_peaks, fused_src);
   else
-    hipLaunchKernelGGL(compact_kernel<float>, dim3(nparts, n), dim3(256), 0, s, mask, (const float*)heat, nparts, H,
-                       W, words, (char*)d_result, lay, caps->max_peaks);
+    hipLaunchKernelGGL((compact_kernel<float, false>), dim3(nparts, n), dim3(256), 0, s, mask, (const float*)heat,
+                       nparts, H, W, words, (char*)d_result, lay, caps->max_peaks, MapSrc{});
   PHIP(hipGetLastError());
   ga.nscales = nscales;
   ga.div_f = div_f;
@@ -1242,7 +1463,8 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
     if ((rc = launch_resize(fh, n, nparts, h, w, 3, div_f, avg, s))) return rc;
   }
   dim3 gb((w + NMS_TX - 1) / NMS_TX, (h + NMS_TY - 1) / NMS_TY, n * nparts);
-  hipLaunchKernelGGL(blur_nms_kernel<double>, gb, dim3(256), 0, s, (const double*)avg, h, w, words, mask, 0.05, 1);
+  hipLaunchKernelGGL((blur_nms_kernel<double, false>), gb, dim3(256), 0, s, (const double*)avg, h, w, words, mask, 0.05,
+                     1, MapSrc{}, 0, nullptr, nullptr, 0, 0);
   PHIP(hipGetLastError());
   if (h * w <= CC_LDS_MAX) {
     static bool attr = false;

@@ -187,6 +187,35 @@ def test_designed_maps_batch_bit_exact(est25):
         assert len(subset) == i, i
 
 
+@pytest.mark.parametrize("H,W", [(368, 656), (368, 131), (368, 45)])
+def test_fused_resize_blur_matches_unfused(est25, monkeypatch, H, W):
+    """Single-scale post with the resize fused into blur_nms (no full-res planes, exact
+    early-out of dead tiles) == the two-kernel path == the oracle, on maps with noise
+    just around the 0.1 threshold (many live and borderline tiles) and odd sizes."""
+    geoms = [g[1:] for g in scale_geometry(H, W, (1.0,))]
+    nh, nw = geoms[0][0] // 8, geoms[0][1] // 8
+    rng = np.random.RandomState(H)
+    maps = [synth.designed_pose_maps(nh, nw, p, 200 + p) for p in (1, 2, 3)]
+    heat_np = np.stack([m[1] for m in maps])
+    noise = rng.uniform(0.0, 0.16, heat_np.shape).astype(np.float32) * (rng.rand(*heat_np.shape) < 0.15)
+    heat_np = heat_np + noise
+    paf = torch.from_numpy(np.stack([m[0] for m in maps])).cuda()
+    heat = torch.from_numpy(heat_np).cuda()
+    monkeypatch.setenv("ISLPOSE_FUSED_BLUR", "1")
+    fused = est25.post_maps(H, W, geoms, [paf], [heat])
+    monkeypatch.setenv("ISLPOSE_FUSED_BLUR", "0")
+    plain = est25.post_maps(H, W, geoms, [paf], [heat])
+    for i in range(len(maps)):
+        assert np.array_equal(fused[i].candidate, plain[i].candidate), i
+        assert np.array_equal(fused[i].subset, plain[i].subset), i
+        hl, pl = heat_np[i], maps[i][0]
+        heat_avg, paf_avg = cpu_ref.body_maps(np.zeros((H, W, 3), np.uint8), lambda im: (pl[None], hl[None]),
+                                              "body25", (1.0,))
+        cand, subset, _, _ = cpu_ref.body_post(heat_avg, paf_avg, "body25", H)
+        assert np.array_equal(fused[i].candidate, cand), i
+        assert np.array_equal(fused[i].subset, subset), i
+
+
 def test_x3_range_guard_falls_back_to_fp32(w25):
     """Activations beyond the fp16 split range (|x| >= 65504) raise the net's range
     flag; Net.forward then recomputes on the fp32 kernels, so the result still

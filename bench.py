@@ -133,6 +133,9 @@ def main():
             marks.append((e0, e1))
             rt.check(L.isl_body_post(ln.net.h, ln.b, H, W, 1, ln.g, ln.pp, ln.hp, ctypes.byref(ln.caps),
                                      rt.ptr(ln.d_res), ln.sh), "post")
+            e2 = torch.cuda.Event(enable_timing=True)
+            e2.record(ln.stream)
+            marks[-1] = (e0, e1, e2)
             with torch.cuda.stream(ln.stream):
                 ln.h_res.copy_(ln.d_res, non_blocking=True)
         for ln in lanes:
@@ -143,18 +146,27 @@ def main():
 
     def net_window_ms(ref, marks):
         # conv stage wall time of one step: first net start -> last net end over all lanes
-        return max(ref.elapsed_time(e1) for _, e1 in marks) - min(ref.elapsed_time(e0) for e0, _ in marks)
+        return max(ref.elapsed_time(m[1]) for m in marks) - min(ref.elapsed_time(m[0]) for m in marks)
+
+    def post_window_ms(ref, marks):
+        # post kernels of one step (isl_body_post: resize/blur/NMS, peaks, PAF scoring, assembly)
+        return max(ref.elapsed_time(m[2]) for m in marks) - min(ref.elapsed_time(m[1]) for m in marks)
 
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize(dev)
-    # validate one step's records (no overflow / errors) outside the timed region
+    # validate one step's records (no overflow / errors) outside the timed region, and
+    # count the (A, B) candidate pairs the PAF kernel scores (sum over limbs of nA * nB)
+    pairs = 0
     for ln in lanes:
         host = ln.h_res.numpy()
         for f in range(ln.b):
             o = f * ln.lay.record_bytes + ln.lay.status
             st = int(host[o:o + 4].view(np.int32)[0])
             assert st == 0, "post status %d on frame %d" % (st, f)
+            o = f * ln.lay.record_bytes + ln.lay.n_peaks
+            npk = host[o:o + 128].view(np.int32)
+            pairs += sum(int(npk[a]) * int(npk[b]) for a, b in synth.BODY25_LIMBS)
         assert ln.net.range_ok(), "split-fp16 range exceeded in warmup"
     for ln in lanes:
         ln.net.set_timing(True)      # per-op HIP events on each lane's stream, inside the timed region
@@ -172,10 +184,11 @@ def main():
         ln.net.set_timing(False)
     ops = [ln.net.timing() for ln in lanes]
     net_ms = float(np.mean([net_window_ms(r, m) for r, m in ev]))
+    post_ms = float(np.mean([post_window_ms(r, m) for r, m in ev]))
     if dist:
-        t = torch.tensor([elapsed, net_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, net_ms, post_ms], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed, net_ms = float(t[0]), float(t[1])
+        elapsed, net_ms, post_ms = float(t[0]), float(t[1]), float(t[2])
     if rank != 0:
         if dist:
             torch.distributed.destroy_process_group()
@@ -242,6 +255,18 @@ def main():
                      "all_convs_tflops": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2),
                      "ms_per_step_by_kind": {KIND[k]: round(v["ms"] / args.steps, 3) for k, v in kinds.items()},
                      "net_ms_per_step": round(net_ms, 3)},
+        "post": {
+            "ms_per_step": round(post_ms, 3),
+            "frames_per_s": round(B / (post_ms * 1e-3), 1),
+            "nms_algorithmic_bytes_per_frame": 25 * H * W * 4,
+            "nms_effective_GBps": round(25 * H * W * 4 * B / (post_ms * 1e-3) / 1e9, 1),
+            "paf_pairs_per_frame": round(pairs / B, 1),
+            "paf_pairs_per_s": round(pairs / (post_ms * 1e-3), 1),
+            "basis": "HIP events around isl_body_post on the lane stream (fused resize+blur+NMS, peak lists, PAF "
+                     "scoring, greedy matching, assembly; D2H excluded). nms_effective_GBps = SURVEY 8(d)'s NMS "
+                     "bytes (25 x H x W x 4 B f32 heat per frame) / whole post time: the fused kernel never "
+                     "materialises those planes, so this is an effective rate, not HBM traffic",
+        },
         "cpu_baseline": None,
     }
     if not args.no_cpu and args.cpu_frames > 0 and world == 1:

@@ -497,11 +497,30 @@ static bool x3_small_tiles() {
 // which cut the L2->LDS bytes per FLOP ~2x and measured +10 % over the 128-pixel
 // tiles (r01); 16 rather than 8 waves for the narrow (96/64/32-channel) tiles
 // +2-9 %.  7x7 layers keep 128-pixel tiles (their slab is 2.3x larger).
+static int device_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
+
+// 512-pixel, 16-wave tiles (one block per CU) unless they cannot fill the chip: a
+// layer with fewer such blocks than CUs (the 23x41 stages of Mode R, small hand
+// scales) runs ~2x faster on the 128-pixel, 4-wave family (tools/gpu_tiles.sh).
+static bool x3_big_tiles(const ConvLaunch& c) {
+  if (c.ks > 3 || x3_small_tiles() || x3_var() != 0) return false;
+  const long long px_tiles = (c.H * c.W + tile_pixels(c, 512, x3_segmax(512)) - 1) / tile_pixels(c, 512, x3_segmax(512));
+  return (long long)c.n * px_tiles * ((c.cout + c.bco - 1) / c.bco) >= device_cus();
+}
+
 template <int KS>
 static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   const int var = KS <= 3 ? x3_var() : 0;
   if constexpr (KS <= 3) {
-    if (!x3_small_tiles() && var == 0) {
+    if (x3_big_tiles(c)) {
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 0, 4>(c, s);   // 16 waves, 64co x 64px each
         case 96: return launch_t<KS, 1, 16, 3, 1, 0, 4>(c, s);   // 16 waves, 96co x 32px
@@ -538,7 +557,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
 bool x3_fits(const ConvLaunch& c) { return c.in_pad >= c.ks / 2; }
 
 double conv_x3_mfma_flops(const ConvLaunch& c) {
-  const int BPX = (c.ks <= 3 && !x3_small_tiles() && x3_var() == 0) ? 512 : 128;
+  const int BPX = x3_big_tiles(c) ? 512 : 128;
   const double co = (double)((c.cout + c.bco - 1) / c.bco) * c.bco;
   const double px = std::ceil((double)c.H * c.W / tile_pixels(c, BPX, x3_segmax(BPX))) * BPX;
   return 3.0 * 2.0 * co * (((c.cin_chunks + 1) / 2) * 16.0) * c.ks * c.ks * px * c.n;

@@ -20,8 +20,9 @@ from islpose.body import BodyEstimator, scale_geometry  # noqa: E402
 
 def main():
     B, H, W = 32, 368, 656
+    scale = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
     est = BodyEstimator(synth.synth_weights(0), "body25")
-    geoms = [g[1:] for g in scale_geometry(H, W, (1.0,))]
+    geoms = [g[1:] for g in scale_geometry(H, W, (scale,))]
     nh, nw = geoms[0][0] // 8, geoms[0][1] // 8
     des = [synth.designed_pose_maps(nh, nw, 3, seed=i) for i in range(B)]
     paf = torch.from_numpy(np.stack([a for a, _ in des])).cuda()
@@ -44,7 +45,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             out["%s_fused%s_ms" % (name, fused)] = round(e0.elapsed_time(e1) / 5, 3)
-    print(json.dumps(out))
+    print(json.dumps(dict(out, scale=scale)))
 
 
 if __name__ == "__main__":

@@ -94,7 +94,7 @@ class KeypointExtractor:
     """Runs `model.call_batch(bgr_frames) -> [(candidate, subset, all_hand_peaks)]` over
     videos in batches and writes the reference's per-frame outputs."""
 
-    def __init__(self, model, out_base: str, batch: int = 16, resume: bool = True, write_json: bool = True,
+    def __init__(self, model, out_base: str, batch: int = 64, resume: bool = True, write_json: bool = True,
                  export: bool = True):
         self.model = model
         self.export = export
@@ -130,7 +130,7 @@ class KeypointExtractor:
         return rows
 
 
-def extract_dataset(rows, decode, model, out_base: str, rank: int = 0, world: int = 1, batch: int = 16,
+def extract_dataset(rows, decode, model, out_base: str, rank: int = 0, world: int = 1, batch: int = 64,
                     resume: bool = True, write_json: bool = True, export: bool = True):
     """rows: [{'Filepath', 'type', 'expression'}] (the dataset CSV of extract_features_mp.py:187).
     Videos are sharded contiguously across ranks; returns (this rank's feature rows, extractor)."""
@@ -156,7 +156,7 @@ def read_dataset_csv(path: str):
         return [dict(r) for r in csv.DictReader(f)]
 
 
-def run(rows, decode, model, out_base: str, rank: int, world: int, batch: int = 16, resume: bool = True,
+def run(rows, decode, model, out_base: str, rank: int, world: int, batch: int = 64, resume: bool = True,
         write_json: bool = True, group=None, export: bool = True):
     """One rank's share + the host-side gather; rank 0 writes the combined CSV like the
     reference's __main__ (extract_features_mp.py:225-239). Returns (rows on rank 0 or None, stats)."""

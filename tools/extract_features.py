@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--body-weights")
     ap.add_argument("--hand-weights")
-    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=64, help="frames of one video per GPU call (Mode R nets fill the GPU from ~64)")
     ap.add_argument("--synthetic", help="T,H,W: synthetic videos instead of .npy files")
     ap.add_argument("--videos", type=int, default=4, help="number of synthetic videos (without --csv)")
     ap.add_argument("--no-resume", action="store_true")

@@ -214,11 +214,13 @@ def main():
     executed = dk["mfma_flops"] / sec / 1e12                   # what the matrix cores ran (tile padding included)
     conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3, 4))
     conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3, 4))
-    traffic = None
+    traffic = mfma_busy = clk = None
     prof = os.path.join(REPO, "profiles", "conv_traffic.json")
     if os.path.exists(prof):
-        traffic = json.load(open(prof)).get({1: "direct", 2: "wino", 3: "x3", 4: "wino_x3"}.get(dom, "x3")
-                                            + "_hbm_bytes_per_launch")
+        pj = json.load(open(prof))
+        key = {1: "direct", 2: "wino", 3: "x3", 4: "wino_x3"}.get(dom, "x3")
+        traffic = pj.get(key + "_hbm_bytes_per_launch")
+        mfma_busy, clk = pj.get(key + "_mfma_busy_frac"), pj.get(key + "_effective_clock_ghz")
     out = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -254,7 +256,12 @@ def main():
                      "algorithmic_gflop_per_launch": round(dk["flops"] / dk["launches"] / 1e9, 3),
                      "all_convs_tflops": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2),
                      "ms_per_step_by_kind": {KIND[k]: round(v["ms"] / args.steps, 3) for k, v in kinds.items()},
-                     "net_ms_per_step": round(net_ms, 3)},
+                     "net_ms_per_step": round(net_ms, 3),
+                     # PMC (profiles/conv_traffic.json, from tools/profile_round.sh): MFMA pipe busy
+                     # fraction of the conv kernels' wall cycles, and the DVFS clock they ran at
+                     "mfma_busy_pmc": mfma_busy,
+                     "effective_clock_ghz": clk,
+                     "frac_at_effective_clock": round(achieved / (peak * clk / 2.4), 4) if clk else None},
         "post": {
             "ms_per_step": round(post_ms, 3),
             "frames_per_s": round(B / (post_ms * 1e-3), 1),

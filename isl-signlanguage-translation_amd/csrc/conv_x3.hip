@@ -37,6 +37,7 @@
 //            fp16 hi / lo in registers and written as [hi|lo][h][px] x 16 B.
 // Double-buffered, one barrier per step; per step and wave KS taps x WM*WN
 // accumulator tiles x 3 MFMAs.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <type_traits>
@@ -65,6 +66,9 @@ struct X3Args {
 
 // input segment capacity in pixels for a BPX-pixel tile (host: tile_pixels)
 constexpr int x3_segmax(int bpx) { return bpx + 64; }
+// capacity of the row-union run (VAR 512): 2 x (1536 + 4 x 857) x 16 B = 155 KiB of LDS
+// with the 128-channel 3x3 weight slabs
+constexpr int x3_segu_max() { return 856; }
 
 template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, int VAR, int OCC>
 __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Args a) {
@@ -82,11 +86,20 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   static_assert(WSLAB % 64 == 0, "weight slab is whole 1 KiB DMA pieces");
   static_assert(BPX <= SEGMAX, "segment must hold a tile");
   constexpr int NBUF = (VAR & 256) ? 3 : 2;        // VAR 256: 3-stage LDS-DMA ring
-  static_assert(NBUF * BUF * 16 <= 160 * 1024, "LDS");
+  // VAR 512 ("row union"): the KS input rows of a chunk pair are staged once, as one
+  // run covering rows -P..+P of the tile, a third per ky step; ky then only offsets
+  // the B reads by ky*Wi.  For tiles spanning several image rows (46x82, 92x164)
+  // this stages 2-2.5x fewer input bytes than one run per (pair, ky).
+  constexpr bool UNION = (VAR & 512) != 0;
+  constexpr int SEGUP = x3_segu_max() + 1;       // + dummy slot
+  constexpr int XSLABU = 2 * 2 * SEGUP;          // [hi|lo][h][px]
+  constexpr int SMEM = UNION ? 2 * (WSLAB + XSLABU) : NBUF * BUF;
+  static_assert(SMEM * 16 <= 160 * 1024, "LDS");
+  static_assert(!UNION || (2 * x3_segu_max() + KS - 1) / KS <= NT, "one union item per thread and step");
   constexpr bool WEAVE = (VAR & 2) != 0;         // interleave the stores with the MFMAs
   constexpr bool NO_STAGE = (VAR & 8) != 0;      // ablation: skip global loads + LDS stores
   constexpr bool NO_MATH = (VAR & 16) != 0;      // ablation: skip LDS reads + MFMAs
-  __shared__ f16x8 smem[NBUF * BUF];
+  __shared__ f16x8 smem[SMEM];
 
   // XCD-aware tile order (conv.hip): co-tiles of a pixel tile, then neighbouring
   // pixel tiles, on one XCD / L2.
@@ -279,6 +292,93 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+  } else if constexpr (UNION) {
+    const int Pw = P * Wi;
+    const int segu = Lb - La + 2 * Pw + 2 * P + 1;        // rows -P..+P of the tile, one run
+    const long long ubase = (long long)La - Pw - P;
+    const int third = (2 * segu + KS - 1) / KS;           // staging items per ky step
+    f32x4 ru[2];
+    int u_ih = 0, u_px = -1;
+    auto load_u = [&](int c2, int ky) __attribute__((always_inline)) {
+      const int it = ky * third + tid;
+      u_px = -1;
+      if (tid < third && it < 2 * segu) {
+        u_ih = it >= segu ? 1 : 0;
+        u_px = it - u_ih * segu;
+      }
+      const int c = 2 * c2 + u_ih;
+      if (u_px >= 0 && c < a.cin_chunks) {
+        const float* src = in_f + (size_t)c * a.in_chs + (size_t)(ubase + u_px) * 8;
+        ru[0] = *(const f32x4*)src;
+        ru[1] = *(const f32x4*)(src + 4);
+      } else {
+        ru[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ru[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    auto store_u = [&](int bx) __attribute__((always_inline)) {
+      if (u_px < 0) return;
+      f16x8* sx = smem + 2 * WSLAB + bx * XSLABU;
+      f16x8 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = ru[j >> 2][j & 3];
+        hi[j] = (_Float16)x;
+        lo[j] = (_Float16)(x - (float)hi[j]);
+      }
+      sx[(0 * 2 + u_ih) * SEGUP + u_px] = hi;
+      sx[(1 * 2 + u_ih) * SEGUP + u_px] = lo;
+    };
+    auto issue_wu = [&](int t, int bw) __attribute__((always_inline)) {
+      const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
+      f16x8* dst = smem + bw * WSLAB;
+#pragma unroll
+      for (int q0 = 0; q0 < WSLAB / 64; q0 += NWAVES) {
+        const int q = q0 + wave_u;
+        if ((WSLAB / 64) % NWAVES == 0 || q < WSLAB / 64)
+          __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
+                                           (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
+      }
+    };
+    auto compute_u = [&](int bw, int bx, int ky) __attribute__((always_inline)) {
+      const f16x8* sw = smem + bw * WSLAB + h * BCO + wave_m * WM * 32 + l32;
+      const f16x8* sx = smem + 2 * WSLAB + bx * XSLABU + h * SEGUP + ky * Wi;
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) {
+        f16x8 A[WM][2], B[WN][2];
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) {
+#pragma unroll
+          for (int wm = 0; wm < WM; ++wm) A[wm][hl] = sw[(kx * 2 + hl) * 2 * BCO + wm * 32];
+#pragma unroll
+          for (int wn = 0; wn < WN; ++wn) B[wn][hl] = sx[hl * 2 * SEGUP + rel[wn] + kx];
+        }
+#pragma unroll
+        for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+          for (int wn = 0; wn < WN; ++wn) {
+            acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][0], acc[wm][wn], 0, 0, 0);
+            acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][1], acc[wm][wn], 0, 0, 0);
+            acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[wn][0], acc[wm][wn], 0, 0, 0);
+          }
+      }
+    };
+    // prologue: weights of step 0, the whole union of pair 0
+    issue_wu(0, 0);
+    for (int ky = 0; ky < KS; ++ky) {
+      load_u(0, ky);
+      store_u(0);
+    }
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+      const int c2 = t / KS, ky = t - c2 * KS;
+      const bool next = c2 + 1 < a.pairs;
+      if (t + 1 < T) issue_wu(t + 1, (t + 1) & 1);
+      if (next) load_u(c2 + 1, ky);      // a third of the next pair's union per step
+      compute_u(t & 1, c2 & 1, ky);
+      if (next) store_u((c2 + 1) & 1);
+      __syncthreads();
+    }
   } else if constexpr ((VAR & 64) != 0) {
     issue_w(0, 0);
     issue_x(0, 0);
@@ -516,9 +616,33 @@ static bool x3_big_tiles(const ConvLaunch& c) {
   return (long long)c.n * px_tiles * ((c.cout + c.bco - 1) / c.bco) >= device_cus();
 }
 
+// Row-union staging (VAR 512) when the longest union run of any 512-pixel tile fits.
+static bool x3_union(const ConvLaunch& c) {
+  static const bool off = getenv("ISLPOSE_X3_UNION") && getenv("ISLPOSE_X3_UNION")[0] == '0';
+  if (off || c.ks != 3) return false;
+  const int P = c.ks / 2, Wi = c.W + 2 * c.in_pad, HW = c.H * c.W;
+  const int tpx = tile_pixels(c, 512, x3_segmax(512));
+  int span = 0;
+  for (int m0 = 0; m0 < HW; m0 += tpx) {
+    const int ml = std::min(m0 + tpx, HW) - 1;
+    span = std::max(span, (ml / c.W - m0 / c.W) * Wi + (ml % c.W - m0 % c.W));
+  }
+  return span + 2 * P * Wi + 2 * P + 1 <= x3_segu_max();
+}
+
 template <int KS>
 static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   const int var = KS <= 3 ? x3_var() : 0;
+  if constexpr (KS == 3) {
+    if (x3_big_tiles(c) && x3_union(c)) {
+      switch (c.bco) {
+        case 128: return launch_t<KS, 2, 8, 2, 2, 512, 4>(c, s);
+        case 96: return launch_t<KS, 1, 16, 3, 1, 512, 4>(c, s);
+        case 64: return launch_t<KS, 2, 8, 1, 2, 512, 4>(c, s);
+        case 32: return launch_t<KS, 1, 16, 1, 1, 512, 4>(c, s);
+      }
+    }
+  }
   if constexpr (KS <= 3) {
     if (x3_big_tiles(c)) {
       switch (c.bco) {

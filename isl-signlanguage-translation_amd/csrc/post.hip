@@ -120,7 +120,7 @@ __device__ __forceinline__ float sample(const MapSrc& m, int f, int c, int y, in
 // horizontal pass is computed once per source row the tile needs (OpenCV's
 // HResizeCubic, stored in LDS), then every output combines 4 of those rows
 // (VResizeCubic) -- the same values OpenCV computes, with 4-5x fewer loads.
-constexpr int RS_TY = 32, RS_TX = 256, RS_MAXR = 40;   // 32 rows: amortise the horizontal pass
+constexpr int RS_TY = 64, RS_TX = 256, RS_MAXR = 40;   // 64 rows: amortise the horizontal pass
 __global__ void __launch_bounds__(256) resize_sep_kernel(MapSrc m, int nch, int oh, int ow, int ty_rows, int mode,
                                                           float inv_div_f, void* out) {
   __shared__ float s_h[RS_MAXR][RS_TX];

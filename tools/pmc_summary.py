@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc passes of bench.py into per-step HBM traffic.
 
-Usage: python tools/pmc_summary.py <fetch_dir> <write_dir> [<sq_dir>] --steps S --out profiles/rNN/pmc_summary.json
+Usage: python tools/pmc_summary.py <fetch_dir> <write_dir> --steps S --out profiles/rNN/pmc_summary.json
+           [--traffic-out profiles/conv_traffic.json] [--sq <sq_dir> --stats <kernel_stats.csv>]
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (§HBM), gfx950's
 FETCH_SIZE reports half of the bytes of wide coalesced reads: the read side is
@@ -41,6 +42,34 @@ def load(d, name):
     return out, {k: len(v) for k, v in disp.items()}
 
 
+def mfma_busy(sq_dir, stats_csv, sq_out):
+    """MFMA pipe busy fraction and effective clock of the x3 conv kernels.
+    SQ_VALU_MFMA_BUSY_CYCLES counts 32 cycles per 32x32x16 MFMA summed over the chip's
+    1024 SIMDs; GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md)."""
+    f = glob.glob(os.path.join(sq_dir, "**", "*counter_collection.csv"), recursive=True)[0]
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    for r in csv.DictReader(open(f)):
+        n = r["Kernel_Name"]
+        k = "conv_x3_f16" if "conv_x3" in n else n.split("(")[0].replace("void ", "").replace("isl::", "")
+        acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(r.get("Dispatch_Id", ""))
+    json.dump({"note": "raw SQ/GRBM counter sums per kernel class over the profiled bench run",
+               "kernels": {k: dict(v, dispatches=len(disp[k])) for k, v in acc.items()}}, open(sq_out, "w"), indent=1)
+    x = acc.get("conv_x3_f16")
+    if not x or not x.get("GRBM_GUI_ACTIVE"):
+        return {}
+    wall_ns = sum(float(r["TotalDurationNs"]) for r in csv.DictReader(open(stats_csv)) if "conv_x3" in r["Name"])
+    active = x["GRBM_GUI_ACTIVE"] / 8
+    return {"x3_mfma_busy_frac": round(x["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / active, 4),
+            "x3_effective_clock_ghz": round(active / wall_ns, 3),
+            "mfma_note": "SQ_VALU_MFMA_BUSY_CYCLES (32 cycles per 32x32x16 MFMA, summed over 1024 SIMDs) / 1024 / "
+                         "(GRBM_GUI_ACTIVE / 8 XCDs): the fraction of the conv kernels' cycles the MFMA pipes were "
+                         "busy, at the clock the chip actually ran (DVFS); effective clock = GRBM_GUI_ACTIVE / 8 / "
+                         "summed conv_x3 duration of the trace pass of the same command. Source: "
+                         + os.path.relpath(sq_out)}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("fetch")
@@ -48,6 +77,8 @@ def main():
     p.add_argument("--steps", type=int, required=True)
     p.add_argument("--out", required=True)
     p.add_argument("--traffic-out", default=None)
+    p.add_argument("--sq", default=None, help="SQ/GRBM pass dir (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)")
+    p.add_argument("--stats", default=None, help="kernel_stats.csv of the trace pass of the same command")
     a = p.parse_args()
     (fe, nfe), (wr, nwr) = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
     res = {}
@@ -70,6 +101,8 @@ def main():
             if cls in res:
                 t[key + "_hbm_bytes_per_launch"] = res[cls]["hbm_bytes_per_launch"]
                 t[key + "_dispatches"] = res[cls]["dispatches"]
+        if a.sq and a.stats:
+            t.update(mfma_busy(a.sq, a.stats, os.path.join(os.path.dirname(a.out), "sq_counters.json")))
         json.dump(t, open(a.traffic_out, "w"), indent=1)
     for k, v in res.items():
         print("%-40s read %10.1f MB  write %10.1f MB" % (k, v["read_bytes_per_step"] / 1e6, v["write_bytes_per_step"] / 1e6))

@@ -21,8 +21,11 @@ Out of scope: the ffmpeg ``Writer`` -- constructing it raises.
 """
 from __future__ import annotations
 
+import collections
+
 import numpy as np
 import torch
+import xxhash
 
 from islpose import translate
 from islpose.body import BodyEstimator
@@ -101,10 +104,13 @@ class ISLSignPos(object):
 class ISLSignPosTranslator(ISLSignPos):
     window_size = translate.WINDOW
 
+    cache_frames = 64   # per-frame feature rows kept for overlapping windows
+
     def __init__(self, body_model, hand_model, translation_model):
         super().__init__(body_model, hand_model)
         self.model_type = 'body25'
         self.translation_layer = translation_model
+        self._rows = collections.OrderedDict()
 
     def populate_features(self, bodypose_circles, handpose_peaks):
         return translate.populate_features(bodypose_circles, handpose_peaks)
@@ -125,12 +131,31 @@ class ISLSignPosTranslator(ISLSignPos):
             rows.extend(self.frame_features(*r) for r in self.call_batch(frames[s:s + batch]))
         return np.array(rows, dtype=np.float64).reshape(len(rows), translate.N_FEATURES)
 
+    def cached_features(self, frames):
+        """Feature rows of frames, reusing the rows of frames seen in recent calls (keyed by
+        a 128-bit hash of the pixels): the demo's rolling window (demo_isl_translate.py:
+        183-190) shares 19 of its 20 frames with the previous call, so only the new frame
+        goes through the keypoint nets.  Rows are identical to computing them afresh."""
+        keys = [(f.shape, xxhash.xxh3_128_digest(np.ascontiguousarray(f))) for f in frames]
+        miss = [i for i, k in enumerate(keys) if k not in self._rows]
+        if miss:
+            res = self.call_batch(np.stack([frames[i] for i in miss]))
+            for i, r in zip(miss, res):
+                self._rows[keys[i]] = self.frame_features(*r)
+        rows = []
+        for k in keys:
+            self._rows.move_to_end(k)
+            rows.append(self._rows[k])
+        while len(self._rows) > max(self.cache_frames, len(frames)):
+            self._rows.popitem(last=False)
+        return rows
+
     def call(self, window):
         """ISL_Model_parameter.py:318-337: window [20, H, W, 3] -> translation_model of the
         [1, 20, 156] feature window.  Shorter windows fail as in the reference, whose
         padding branch reads ``.shape`` of a list (:331-333); longer ones fail its reshape."""
         frames = _as_numpy(window)
-        feats = [self.frame_features(*r) for r in self.call_batch(frames)] if len(frames) else []
+        feats = self.cached_features(frames) if len(frames) else []
         if len(feats) < self.window_size:
             raise AttributeError("'list' object has no attribute 'shape'")
         return self.translation_layer(np.array(feats).reshape(1, self.window_size, translate.N_FEATURES))

@@ -155,6 +155,25 @@ def test_translator_window_logic():
     assert len(t.translate_stream(frames[:10])) == 0
 
 
+def test_translator_rolling_window_reuses_rows():
+    """The demo's rolling window: after the first call only the new frame is computed,
+    and every result equals a fresh computation."""
+    seen = []
+    t = _fake_translator(lambda x: (seen.append(np.array(x)), np.asarray(x).sum())[1])
+    counted = []
+    inner = t.call_batch
+    t.call_batch = lambda f: (counted.append(len(f)), inner(f))[1]
+    frames = np.zeros((25, 4, 4, 3), np.uint8)
+    frames[:, 0, 0, 0] = np.arange(25) + 1
+    for s in range(6):
+        t.call(frames[s:s + 20])
+    assert counted == [20, 1, 1, 1, 1, 1]
+    fresh = _fake_translator(lambda x: np.asarray(x).sum())
+    for s in range(6):
+        np.testing.assert_array_equal(seen[s][0], fresh.features(frames[s:s + 20]))
+    assert len(t._rows) <= t.cache_frames
+
+
 # ---------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 def test_sign_classifier_matches_oracle():

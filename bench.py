@@ -61,6 +61,8 @@ def parse():
                    help="conv arithmetic: split-fp16 x3 on the FP16 matrix cores (default), Winograd or direct fp32")
     p.add_argument("--cpu-frames", type=int, default=6, help="frames for the CPU baseline sample (0 = skip)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--split-k", action="store_true",
+                   help="split-K on small conv grids (isl_net_set_split_k): batch-1 latency mode")
     return p.parse_args()
 
 
@@ -102,6 +104,8 @@ def main():
             self.est = BodyEstimator(weights, "body25", device=local, scale_search=(args.scale,))
             self.net = self.est.net
             self.net.set_algo(args.algo)
+            if args.split_k:
+                self.net.set_split_k(True)
             self.b = B // S
             sl = slice(s * self.b, (s + 1) * self.b)
             self.frames, self.paf, self.heat = frames[sl], d_paf[sl], d_heat[sl]
@@ -239,7 +243,7 @@ def main():
         "config": {"workload": "configs[1]: body_25 single-scale %dx%d frames, batch %d per GPU, net input %dx%d"
                                % (H, W, B, nh, nw),
                    "batch_per_gpu": B, "frame_hw": [H, W], "scale_search": [args.scale], "net_hw": [nh, nw],
-                   "streams_per_gpu": S, "conv_algo": args.algo,
+                   "streams_per_gpu": S, "conv_algo": args.algo, "split_k": bool(args.split_k),
                    "parallelism": "frame-sharded x%d (no collective)" % world},
         "roofline": {"bound": "mfma", "kernel": KIND[dom],
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

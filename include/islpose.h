@@ -117,6 +117,13 @@ int isl_net_run(isl_net* net, float* d_out0, float* d_out1, void* stream);
 int isl_net_set_algo(isl_net* net, int algo);
 int isl_net_get_algo(const isl_net* net);
 
+/* Split-K for ISL_ALGO_X3 layers whose grid cannot fill the GPU (batch-1 frames,
+ * single hand crops): the K range is spread over up to 8 blocks per tile and
+ * reduced in a fixed order (deterministic).  Off by default (env
+ * ISLPOSE_X3_SPLITK=1 turns it on at create time): with it, a frame's maps differ
+ * in the last bits between batch sizes (always within the fp32 tolerance). */
+int isl_net_set_split_k(isl_net* net, int on);
+
 /* Range guard of ISL_ALGO_X3: waits for the device, returns ISL_E_RANGE if any
  * conv output since the last clear left the fp16 split range (the results of
  * those runs are then not fp32-accurate and must be recomputed with

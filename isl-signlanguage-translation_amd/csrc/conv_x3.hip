@@ -62,6 +62,9 @@ struct X3Args {
   float wscale_inv;             // 2^-s
   int in_pad, out_pad;
   int H, W, cin_chunks, pairs, cout, co_tiles, px_tiles, tpx, act, nblocks;
+  int ksplit;                   // split-K (VAR 2048): blocks per tile, each over a range of chunk pairs
+  int nfr;                      // frames (split-K partial-sum layout)
+  float* ws;                    // split-K partial sums [ksplit][nfr][cout/8][H*W][8]
 };
 
 // input segment capacity in pixels for a BPX-pixel tile (host: tile_pixels)
@@ -97,6 +100,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   static_assert(SMEM * 16 <= 160 * 1024, "LDS");
   static_assert(!UNION || (2 * x3_segu_max() + KS - 1) / KS <= NT, "one union item per thread and step");
   constexpr bool WEAVE = (VAR & 2) != 0;         // interleave the stores with the MFMAs
+  // VAR 2048 (split-K, small grids such as batch-1 frames): the block computes the
+  // partial sum of a contiguous range of chunk pairs into a.ws; x3_splitk_reduce
+  // adds the ranges in a fixed order and applies the epilogue
+  constexpr bool SPLIT = (VAR & 2048) != 0;
   constexpr bool NO_STAGE = (VAR & 8) != 0;      // ablation: skip global loads + LDS stores
   constexpr bool NO_MATH = (VAR & 16) != 0;      // ablation: skip LDS reads + MFMAs
   __shared__ f16x8 smem[SMEM];
@@ -107,6 +114,11 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   {
     const int nb = a.nblocks, q = nb >> 3, r = nb & 7, xcd = bid & 7, k = bid >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  int ks_i = 0;
+  if constexpr (SPLIT) {
+    ks_i = bid % a.ksplit;
+    bid /= a.ksplit;
   }
   const int co_t = bid % a.co_tiles;
   const int rest = bid / a.co_tiles;
@@ -394,18 +406,24 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     }
   } else if constexpr ((VAR & 1) == 0) {
     // weights by LDS-DMA one step ahead, input rows register-staged one step ahead
-    issue_w(0, 0);
-    load_x(0);
+    int t0 = 0, t1 = T;
+    if constexpr (SPLIT) {
+      const int pps = (a.pairs + a.ksplit - 1) / a.ksplit;
+      t0 = ks_i * pps * KS;
+      t1 = min(a.pairs, (ks_i + 1) * pps) * KS;
+    }
+    issue_w(t0, 0);
+    load_x(t0);
     store_x(0);
     __syncthreads();
-    for (int t = 0; t < T; ++t) {
-      const int buf = t & 1;
-      if (t + 1 < T) {
+    for (int t = t0; t < t1; ++t) {
+      const int buf = (t - t0) & 1;
+      if (t + 1 < t1) {
         issue_w(t + 1, buf ^ 1);
         load_x(t + 1);
       }
       compute(buf);
-      if (t + 1 < T) store_x(buf ^ 1);
+      if (t + 1 < t1) store_x(buf ^ 1);
       __syncthreads();
     }
   } else {
@@ -504,6 +522,31 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     }
   }
 
+  if constexpr (SPLIT) {
+    // partial sums x 2^-s (exact) into this range's slice of the workspace; the
+    // workspace carries round8(cout) channels, so the 4-channel groups never overrun
+    const size_t plane = (size_t)HW * 8;
+    float* wsb = a.ws + ((size_t)ks_i * a.nfr + n) * (size_t)((a.cout + 7) / 8) * plane;
+#pragma unroll
+    for (int wn = 0; wn < WN; ++wn) {
+      const int m = m0 + (wave_n * WN + wn) * 32 + l32;
+      if (m > mlast) continue;
+#pragma unroll
+      for (int wm = 0; wm < WM; ++wm) {
+        const int cob = co_t * BCO + (wave_m * WM + wm) * 32 + 4 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int co = cob + 8 * q;
+          if (co >= a.cout) continue;
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[wm][wn][4 * q + e] * a.wscale_inv;
+          *(f32x4*)(wsb + (size_t)(co >> 3) * plane + (size_t)m * 8 + (co & 7)) = v;
+        }
+      }
+    }
+    return;
+  }
   // epilogue: x 2^-s, bias + activation, range check, masked float4 stores
   const int Wo = a.W + 2 * a.out_pad;
   float* out_f = a.out + (size_t)n * a.out_fs;
@@ -548,6 +591,50 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   if (bad) atomicOr(a.range_flag, 1);
 }
 
+// Split-K reduction: the ranges' partial sums added in range order (deterministic),
+// then the epilogue of conv_x3_f16 (bias, activation, range check, masked stores).
+// One thread per (frame, 4-channel group, pixel).
+__global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
+  const int HW = a.H * a.W, g4 = (a.cout + 3) / 4;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)a.nfr * g4 * HW) return;
+  const int m = (int)(i % HW);
+  const long long r = i / HW;
+  const int g = (int)(r % g4), n = (int)(r / g4);
+  const int co = 4 * g, c8 = (a.cout + 7) / 8;
+  const size_t plane = (size_t)HW * 8;
+  const float* p = a.ws + ((size_t)n * c8 + (co >> 3)) * plane + (size_t)m * 8 + (co & 7);
+  const size_t split_stride = (size_t)a.nfr * c8 * plane;
+  f32x4 sum = *(const f32x4*)p;
+  for (int k = 1; k < a.ksplit; ++k) sum += *(const f32x4*)(p + k * split_stride);
+  const f32x4 b = *(const f32x4*)(a.bias + co);
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = sum[e] + b[e];
+  if (a.act == ACT_RELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+  } else if (a.act == ACT_PRELU) {
+    const f32x4 sl = *(const f32x4*)(a.slope + co);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
+  }
+  bool bad = false;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bad |= co + e < a.cout && !(__builtin_fabsf(v[e]) < 65504.f);
+  const int y = m / a.W, x = m - y * a.W, Wo = a.W + 2 * a.out_pad;
+  float* oc = a.out + (size_t)n * a.out_fs + (size_t)(co >> 3) * a.out_chs +
+              (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8 + (co & 7);
+  if (co + 3 < a.cout) {
+    *(f32x4*)oc = v;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (co + e < a.cout) oc[e] = v[e];
+  }
+  if (bad) atomicOr(a.range_flag, 1);
+}
+
 template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, int VAR, int OCC>
 static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   constexpr int BCO = WAVES_M * WM * 32;
@@ -574,11 +661,19 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   a.tpx = tile_pixels(c, BPX, SEGCAP);
   a.px_tiles = (c.H * c.W + a.tpx - 1) / a.tpx;
   a.act = c.act;
-  const long long nb = (long long)c.n * a.px_tiles * a.co_tiles;
+  a.ksplit = (VAR & 2048) ? c.ksplit : 1;
+  a.nfr = c.n;
+  a.ws = c.ws;
+  if ((VAR & 2048) && (!c.ws || c.ksplit < 2)) { set_error("conv_x3: split-K without workspace"); return hipErrorInvalidValue; }
+  const long long nb = (long long)c.n * a.px_tiles * a.co_tiles * a.ksplit;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
   hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN, VAR, OCC>), dim3(a.nblocks),
                      dim3(WAVES_M * WAVES_N * 64), 0, s, a);
+  if constexpr ((VAR & 2048) != 0) {
+    const long long nt = (long long)c.n * ((c.cout + 3) / 4) * c.H * c.W;
+    hipLaunchKernelGGL(x3_splitk_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 
@@ -665,6 +760,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   switch (c.bco) {
 #define X3_CASE(BC, WMS, WNS, WMM, WNN)                                                   \
   case BC:                                                                                \
+    if (var == 0 && c.ksplit > 1) return launch_t<KS, WMS, WNS, WMM, WNN, 2048, 2>(c, s); \
     if (var == 1) return launch_t<KS, WMS, WNS, WMM, WNN, (KS <= 3 ? 1 : 0), 2>(c, s);    \
     if (var == 3) return launch_t<KS, WMS, WNS, WMM, WNN, (KS <= 3 ? 3 : 0), 2>(c, s);    \
     return launch_t<KS, WMS, WNS, WMM, WNN, 0, 2>(c, s);
@@ -687,7 +783,36 @@ double conv_x3_mfma_flops(const ConvLaunch& c) {
   return 3.0 * 2.0 * co * (((c.cin_chunks + 1) / 2) * 16.0) * c.ks * c.ks * px * c.n;
 }
 
-hipError_t launch_conv_x3(const ConvLaunch& c, hipStream_t s) {
+// Split-K factor for a launch on the 128-pixel family: when the grid cannot half-fill
+// the CUs (batch-1 frames, single hand crops, the 23x41 stages of small batches), the
+// chunk pairs are split over up to 8 blocks per tile, at least 2 pairs each.
+// Opt-in per net (isl_net_set_split_k): the split adds the K ranges in a different
+// association, so a frame's maps then depend (in the last bits) on the batch it came
+// in; by default every frame gives the same bits at any batch size.
+static int x3_ksplit(const ConvLaunch& c) {
+  if (!c.allow_split || x3_big_tiles(c) || x3_var() != 0) return 1;
+  const int tpx = tile_pixels(c, 128, x3_segmax(128));
+  const long long blocks = (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * ((c.cout + c.bco - 1) / c.bco);
+  const int cus = device_cus(), pairs = (c.cin_chunks + 1) / 2;
+  if (2 * blocks > cus || pairs < 4) return 1;
+  int S = (int)std::min<long long>({8, pairs / 2, (cus + blocks - 1) / blocks});
+  // the kernel's ranges are ceil(pairs / S) pairs long: keep every one non-empty
+  while (S > 1 && (S - 1) * ((pairs + S - 1) / S) >= pairs) --S;
+  return S;
+}
+
+size_t x3_splitk_ws_floats(const ConvLaunch& c) {
+  const int S = x3_ksplit(c);
+  return S > 1 ? (size_t)S * c.n * ((c.cout + 7) / 8) * 8 * c.H * c.W : 0;
+}
+
+hipError_t launch_conv_x3(const ConvLaunch& c0, hipStream_t s) {
+  ConvLaunch c = c0;
+  c.ksplit = 1;
+  if (c.ws) {
+    const int S = x3_ksplit(c);
+    if (S > 1 && (size_t)S * c.n * ((c.cout + 7) / 8) * 8 * c.H * c.W <= c.ws_floats) c.ksplit = S;
+  }
   switch (c.ks) {
     case 1: return launch_ks<1>(c, s);
     case 3: return launch_ks<3>(c, s);

@@ -41,6 +41,11 @@ struct ConvLaunch {
   const void* wx3 = nullptr;   // pre-split weights [co_tile][pair][ky][kx][hi|lo][h][BCO][8] fp16
   float wscale_inv = 1.f;      // 2^-s, the inverse of the per-layer weight scale
   int* range_flag = nullptr;   // raised when an output leaves the fp16 split range
+  // split-K workspace (conv_x3 on grids too small to fill the GPU); null = no split
+  float* ws = nullptr;
+  size_t ws_floats = 0;
+  int ksplit = 1;              // set by launch_conv_x3
+  int allow_split = 0;         // the net's split-K switch (isl_net_set_split_k)
 };
 
 // Pixels per tile of the flattened-raster conv kernels: BPX, or fewer when the
@@ -67,6 +72,8 @@ hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
 hipError_t launch_conv_x3(const ConvLaunch& c, hipStream_t s);
 bool x3_fits(const ConvLaunch& c);
 double conv_x3_mfma_flops(const ConvLaunch& c);
+// floats of split-K workspace launch_conv_x3 would use for c (0 = no split)
+size_t x3_splitk_ws_floats(const ConvLaunch& c);
 // Split-fp16 Winograd F(2x2,3x3) (wino_x3.hip): 3x3 layers with cout % 4 == 0;
 // c.wx3 then holds the split transformed filters [co_tile][pair][xi][hi|lo][h][64][8].
 hipError_t launch_wino_x3(const ConvLaunch& c, hipStream_t s);

@@ -202,6 +202,9 @@ struct isl_net {
   // post scratch
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  // split-K partial sums of the x3 convs on small grids (grow-only)
+  float* d_ks = nullptr;
+  size_t ks_floats = 0;
   // per-op event timing (isl_net_set_timing / isl_net_timing)
   struct TimedRun {
     std::vector<hipEvent_t> ev;          // ops + 1 events: before op 0, after every op
@@ -212,6 +215,7 @@ struct isl_net {
   std::vector<TimedRun> timed;
   // conv algorithm (ISL_ALGO_*) and the split-fp16 range flag (isl_net_check)
   int algo = ISL_ALGO_X3;
+  int split_k = 0;             // isl_net_set_split_k (default: env ISLPOSE_X3_SPLITK=1)
   int* d_flag = nullptr;
   // pre-processing image table (device, grow-only; refilled stream-ordered per call)
   void* d_tab = nullptr;
@@ -654,6 +658,18 @@ static int run_ops(isl_net* net, hipStream_t s) {
       HIP_OK(launch_wino_x3(L, s));
       kind = 4; mf = wino_x3_mfma_flops(L);
     } else if (net->algo == ISL_ALGO_X3 && x3_fits(L)) {
+      L.allow_split = net->split_k;
+      const size_t need = x3_splitk_ws_floats(L);
+      if (need > net->ks_floats) {
+        // grow-only; hipFree waits for the queued work that may still read the old one
+        if (net->d_ks) HIP_OK(hipFree(net->d_ks));
+        net->d_ks = nullptr;
+        net->ks_floats = 0;
+        HIP_OK(hipMalloc(&net->d_ks, need * sizeof(float)));
+        net->ks_floats = need;
+      }
+      L.ws = net->d_ks;
+      L.ws_floats = net->ks_floats;
       HIP_OK(launch_conv_x3(L, s));
       kind = 3; mf = conv_x3_mfma_flops(L);
     } else {
@@ -721,6 +737,10 @@ int isl_net_create(int kind, int device, isl_net** out) {
   net->kind = kind;
   net->device = device;
   net->algo = default_algo();
+  {
+    const char* e = getenv("ISLPOSE_X3_SPLITK");
+    net->split_k = e && e[0] == '1';
+  }
   net->layers = kind == ISL_BODY25 ? body25_layers() : kind == ISL_COCO ? coco_layers() : hand_layers();
   for (size_t i = 0; i < net->layers.size(); ++i) {
     const ConvLayer& c = net->layers[i];
@@ -751,6 +771,7 @@ int isl_net_destroy(isl_net* net) {
   if (net->d_tab) (void)hipFree(net->d_tab);
   for (auto& kv : net->plans) (void)hipFree(kv.second.first);
   if (net->scratch) (void)hipFree(net->scratch);
+  if (net->d_ks) (void)hipFree(net->d_ks);
   for (auto& r : net->timed)
     for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
   delete net;
@@ -933,6 +954,12 @@ int isl_net_set_algo(isl_net* net, int algo) {
 }
 
 int isl_net_get_algo(const isl_net* net) { return net ? net->algo : fail(ISL_E_ARG, "net is NULL"); }
+
+int isl_net_set_split_k(isl_net* net, int on) {
+  if (!net) return fail(ISL_E_ARG, "net is NULL");
+  net->split_k = on != 0;
+  return ISL_OK;
+}
 
 int isl_net_check(isl_net* net, int clear) {
   if (!net) return fail(ISL_E_ARG, "net is NULL");

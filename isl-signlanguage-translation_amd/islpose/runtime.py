@@ -24,7 +24,7 @@ EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destr
            "isl_net_param_info", "isl_net_set_param", "isl_net_forward", "isl_net_preprocess", "isl_net_run", "isl_net_debug_input",
            "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post",
            "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops",
-           "isl_sign_param_count", "isl_sign_classify"]
+           "isl_sign_param_count", "isl_sign_classify", "isl_net_set_split_k"]
 
 
 class IslCaps(ctypes.Structure):
@@ -87,6 +87,7 @@ def lib():
                                 ctypes.POINTER(vp), ctypes.POINTER(IslCaps), vp, vp]
     L.isl_hand_post.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp), vp, vp]
     L.isl_sign_param_count.argtypes = [i32, i32, ctypes.POINTER(i64)]
+    L.isl_net_set_split_k.argtypes = [vp, i32]
     L.isl_sign_classify.argtypes = [vp, i32, i32, i32, vp, i32, vp, vp]
     for name in EXPORTS[2:]:
         getattr(L, name).restype = i32
@@ -197,6 +198,10 @@ class Net:
         """'x3' (split-fp16 on the FP16 matrix cores, fp32-accurate; default), 'wino'
         (Winograd F(2x2,3x3), FP32 MFMA) or 'direct' (implicit GEMM, FP32 MFMA)."""
         check(lib().isl_net_set_algo(self.h, ALGOS[algo]), "isl_net_set_algo")
+
+    def set_split_k(self, on: bool):
+        """Split-K for small grids (batch-1 latency, ~2x at 184x328); see isl_net_set_split_k."""
+        check(lib().isl_net_set_split_k(self.h, int(bool(on))), "isl_net_set_split_k")
 
     def algo_scope(self, algo: str):
         import contextlib

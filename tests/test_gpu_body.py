@@ -239,6 +239,27 @@ def test_x3_range_guard_falls_back_to_fp32(w25):
     assert net.algo == "x3"
 
 
+@pytest.mark.parametrize("n,h,w", [(1, 184, 328), (1, 368, 656), (2, 92, 164)])
+def test_x3_splitk_small_grids(net25, w25, n, h, w):
+    """Batch-1 frames (grids smaller than the GPU) split the K range of the x3 convs
+    over several blocks and reduce in a fixed order: deterministic, within 1e-5 of the
+    unsplit kernel, and within the tolerance of the oracle."""
+    x = torch.from_numpy(_inputs(n, h, w, seed=n * h + w)).cuda()
+    p0, h0 = net25.forward(x)
+    net25.set_split_k(True)
+    try:
+        p1, h1 = net25.forward(x)
+        p2, h2 = net25.forward(x)
+    finally:
+        net25.set_split_k(False)
+    assert torch.equal(p1, p2) and torch.equal(h1, h2)
+    assert _rel(p1.cpu().numpy(), p0.cpu().numpy()) < 1e-5
+    assert _rel(h1.cpu().numpy(), h0.cpu().numpy()) < 1e-5
+    if h <= 184:
+        rp, rh = cpu_ref.make_net_fn("body25", w25)(x.cpu().numpy())
+        assert _rel(p1.cpu().numpy(), rp) < TOL and _rel(h1.cpu().numpy(), rh) < TOL
+
+
 def test_x3_matches_direct_small_shapes(net25):
     """Split-fp16 vs fp32 direct on awkward shapes (narrow images, one-row tiles,
     odd chunk counts) -- both within the tolerance of each other."""

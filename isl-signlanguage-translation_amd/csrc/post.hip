@@ -432,7 +432,7 @@ __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ pla
 // The low-res bound of the fused path for TL_TILES consecutive blur tiles per block
 // (one wave per tile at a time); live tiles are appended to `live` with one atomic
 // per block (order irrelevant: every tile owns its mask words).
-constexpr int TL_TILES = 64;
+constexpr int TL_TILES = 16;   // 4 tiles per wave: enough blocks to hide the load latency
 __global__ void __launch_bounds__(256) tile_live_kernel(MapSrc m, int nch, int H, int W, int tiles_x, int tiles_y,
                                                         int n_tiles, double thre, int* __restrict__ live,
                                                         int* __restrict__ live_count) {
@@ -462,7 +462,8 @@ __global__ void __launch_bounds__(256) tile_live_kernel(MapSrc m, int nch, int H
   }
   __syncthreads();
   if (threadIdx.x < 64) {
-    const int fl = s_flag[lane];
+    static_assert(TL_TILES <= 64, "one wave publishes the block's flags");
+    const int fl = lane < TL_TILES ? s_flag[lane] : 0;
     const unsigned long long bal = __ballot(fl);
     int base = 0;
     if (lane == 0 && bal) base = atomicAdd(live_count, (int)__popcll(bal));

@@ -216,6 +216,22 @@ def test_fused_resize_blur_matches_unfused(est25, monkeypatch, H, W):
         assert np.array_equal(fused[i].subset, subset), i
 
 
+def test_fused_post_reads_the_arena(est25, monkeypatch):
+    """Mode N estimate (scale 1.0: the fused resize + blur) reading the net's own arena
+    output == the same maps handed over as caller tensors == the unfused kernels."""
+    from islpose.body import BodyEstimator
+    est = BodyEstimator(model_type="body25", scale_search=(1.0,), net=est25.net)
+    frames = torch.from_numpy(synth.synth_frames(2, 368, 200, seed=21)).cuda()
+    arena = est.estimate(frames, details=True)
+    geoms, pafs, heats = est.run_scales(frames, keep_maps=True)
+    caller = est.post_maps(368, 200, geoms, pafs, heats)
+    monkeypatch.setenv("ISLPOSE_FUSED_BLUR", "0")
+    plain = est.post_maps(368, 200, geoms, pafs, heats)
+    for a, b, c in zip(arena, caller, plain):
+        assert np.array_equal(a.candidate, b.candidate) and np.array_equal(a.subset, b.subset)
+        assert np.array_equal(a.candidate, c.candidate) and np.array_equal(a.subset, c.subset)
+
+
 def test_x3_range_guard_falls_back_to_fp32(w25):
     """Activations beyond the fp16 split range (|x| >= 65504) raise the net's range
     flag; Net.forward then recomputes on the fp32 kernels, so the result still

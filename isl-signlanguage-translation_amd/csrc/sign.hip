@@ -13,9 +13,10 @@
 // stored at the original time index; the mask propagates to the second layer.
 // LSTM gates in keras order (i, f, c, o), sigmoid / tanh; BN eps = 1e-3.
 //
-// Thread map (256 lanes = 4 waves): lane = direction * 128 + gate-row.  The input
-// projection x_t @ K for all T steps is one pass over K (coalesced over the gate
-// row, x broadcast from LDS); the recurrence keeps the lane's column of the
+// Thread map (1024 lanes = 16 waves): lane % 256 = direction * 128 + gate-row.  The
+// input projection x_t @ K is split over four step ranges (lane / 256), one pass over
+// K each (coalesced over the gate row, x broadcast from LDS); the recurrence (lanes
+// < 256) keeps the lane's column of the
 // recurrent kernel in 32 VGPRs and needs two barriers per step (gate
 // activations, then the 64 (direction, unit) cell updates).  The work is tiny
 // (≈2 MFLOP per window) and latency-bound; the point of the kernel is one launch
@@ -33,7 +34,9 @@ constexpr int SC_D = 32;            // Dense widths of the head
 constexpr int SC_TMAX = 32;         // longest window
 constexpr int SC_FMAX = 256;        // widest feature vector
 constexpr int SC_CMAX = 1024;       // most classes
-constexpr int SC_THREADS = 2 * SC_G;
+constexpr int SC_THREADS = 2 * SC_G;  // lanes of the recurrence: (direction, gate row)
+constexpr int SC_BLOCK = 4 * SC_THREADS; // the projections also split the window in 4 step ranges
+constexpr int SC_TQT = SC_TMAX / 4;      // steps per range
 constexpr float SC_EPS = 1e-3f;     // keras BatchNormalization epsilon
 
 struct SignArgs {
@@ -62,23 +65,40 @@ __device__ __forceinline__ float sc_bn(const float* p, int n, int j, float v) {
   return (v - p[2 * n + j]) / sqrtf(p[3 * n + j] + SC_EPS) * p[j] + p[n + j];
 }
 
-// z[t][d][g] = b[g] + sum_f in[t][f] * K[f][g] for every step (one lane per (d, g)).
-__device__ void sc_project(const float* in, int F, int T, const float* K, const float* b, int g, float* zrow) {
-  float acc[SC_TMAX];
+// z[t][d][g] = b[g] + sum_f in[t][f] * K[f][g] (one lane per (d, g, range of 8 steps)).
+// A lone window is latency-bound: 1024 lanes on one CU, four K rows per iteration and
+// 16-byte LDS reads of the inputs; the sum over f keeps its order.
+__device__ void sc_project(const float* in, int F, int T, const float* K, const float* b, int g, int tq,
+                           float* zrow) {
+  const int tb = tq * SC_TQT;
+  if (tb >= T) return;
+  float acc[SC_TQT];
   const float bias = b[g];
 #pragma unroll
-  for (int t = 0; t < SC_TMAX; ++t) acc[t] = bias;
-  // unrolled so several K rows are in flight: a lone window is latency-bound here
-#pragma unroll 8
-  for (int f = 0; f < F; ++f) {
-    const float w = K[(size_t)f * SC_G + g];
+  for (int k = 0; k < SC_TQT; ++k) acc[k] = bias;
+  if ((F & 3) == 0) {
+#pragma unroll 4
+    for (int f = 0; f < F; f += 4) {
+      const float w0 = K[(size_t)f * SC_G + g], w1 = K[(size_t)(f + 1) * SC_G + g];
+      const float w2 = K[(size_t)(f + 2) * SC_G + g], w3 = K[(size_t)(f + 3) * SC_G + g];
 #pragma unroll
-    for (int t = 0; t < SC_TMAX; ++t)
-      if (t < T) acc[t] += in[t * F + f] * w;
+      for (int k = 0; k < SC_TQT; ++k)
+        if (tb + k < T) {
+          const float4 v = *(const float4*)(in + (tb + k) * F + f);
+          acc[k] = (((acc[k] + v.x * w0) + v.y * w1) + v.z * w2) + v.w * w3;
+        }
+    }
+  } else {
+    for (int f = 0; f < F; ++f) {
+      const float w = K[(size_t)f * SC_G + g];
+#pragma unroll
+      for (int k = 0; k < SC_TQT; ++k)
+        if (tb + k < T) acc[k] += in[(tb + k) * F + f] * w;
+    }
   }
 #pragma unroll
-  for (int t = 0; t < SC_TMAX; ++t)
-    if (t < T) zrow[t * SC_THREADS] = acc[t];
+  for (int k = 0; k < SC_TQT; ++k)
+    if (tb + k < T) zrow[(tb + k) * SC_THREADS] = acc[k];
 }
 
 // One bidirectional LSTM layer over s_z (projected inputs); seq != nullptr writes
@@ -86,19 +106,22 @@ __device__ void sc_project(const float* in, int F, int T, const float* K, const 
 // final (carried) hidden state of each direction.
 __device__ void sc_recur(const float* s_z, const int* s_mask, int T, const float* R, int d, int g, int tid,
                          float (*s_h)[SC_U], float (*s_act)[SC_G], float* seq, float* h_last) {
+  const bool act = tid < SC_THREADS;     // the other lanes only keep the barriers
   float r[SC_U];
 #pragma unroll
-  for (int k = 0; k < SC_U; ++k) r[k] = R[k * SC_G + g];
+  for (int k = 0; k < SC_U; ++k) r[k] = act ? R[k * SC_G + g] : 0.0f;
   const int gate = g / SC_U;
   float c = 0.0f;
   if (tid < 2 * SC_U) s_h[tid / SC_U][tid % SC_U] = 0.0f;
   __syncthreads();
   for (int s = 0; s < T; ++s) {
-    const int t = d == 0 ? s : T - 1 - s;
-    float z = s_z[t * SC_THREADS + d * SC_G + g];
+    if (act) {
+      const int t = d == 0 ? s : T - 1 - s;
+      float z = s_z[t * SC_THREADS + d * SC_G + g];
 #pragma unroll
-    for (int k = 0; k < SC_U; ++k) z += s_h[d][k] * r[k];
-    s_act[d][g] = gate == 2 ? tanhf(z) : sc_sigmoid(z);
+      for (int k = 0; k < SC_U; ++k) z += s_h[d][k] * r[k];
+      s_act[d][g] = gate == 2 ? tanhf(z) : sc_sigmoid(z);
+    }
     __syncthreads();
     if (tid < 2 * SC_U) {
       const int dd = tid / SC_U, u = tid % SC_U;
@@ -117,10 +140,10 @@ __device__ void sc_recur(const float* s_z, const int* s_mask, int T, const float
   __syncthreads();
 }
 
-__global__ __launch_bounds__(SC_THREADS) void sign_classify_kernel(SignArgs a) {
-  __shared__ float s_x[SC_TMAX * SC_FMAX];          // 32 KB: window, then BN'd
+__global__ __launch_bounds__(SC_BLOCK) void sign_classify_kernel(SignArgs a) {
+  __shared__ __attribute__((aligned(16))) float s_x[SC_TMAX * SC_FMAX];          // 32 KB: window, then BN'd
   __shared__ float s_z[SC_TMAX * SC_THREADS];       // 32 KB: projected gates
-  __shared__ float s_seq[SC_TMAX * 2 * SC_U];       //  8 KB: layer-1 sequence
+  __shared__ __attribute__((aligned(16))) float s_seq[SC_TMAX * 2 * SC_U];       //  8 KB: layer-1 sequence
   __shared__ float s_h[2][SC_U];
   __shared__ float s_act[2][SC_G];
   __shared__ int s_mask[SC_TMAX];
@@ -128,28 +151,30 @@ __global__ __launch_bounds__(SC_THREADS) void sign_classify_kernel(SignArgs a) {
   __shared__ float s_logit[SC_CMAX];
   __shared__ float s_red[SC_THREADS / 64];
 
-  const int tid = threadIdx.x, d = tid / SC_G, g = tid % SC_G;
+  const int tid = threadIdx.x, lt = tid % SC_THREADS, tq = tid / SC_THREADS;
+  const int d = lt / SC_G, g = lt % SC_G;
+  const bool hw = tid < SC_THREADS;   // the head's lanes
   const int T = a.T, F = a.F, C = a.C;
   const float* x = a.x + (size_t)blockIdx.x * T * F;
 
   if (tid < SC_TMAX) s_mask[tid] = 0;
   __syncthreads();
-  for (int i = tid; i < T * F; i += SC_THREADS) {
+  for (int i = tid; i < T * F; i += SC_BLOCK) {
     const float v = x[i];
     s_x[i] = v;
     if (v != 0.0f) s_mask[i / F] = 1;               // Masking(mask_value=0.)
   }
   __syncthreads();
-  for (int i = tid; i < T * F; i += SC_THREADS) s_x[i] = sc_bn(a.bn0, F, i % F, s_x[i]);
+  for (int i = tid; i < T * F; i += SC_BLOCK) s_x[i] = sc_bn(a.bn0, F, i % F, s_x[i]);
   __syncthreads();
 
   // layer 1: Bidirectional(LSTM(32, return_sequences=True))
-  sc_project(s_x, F, T, a.k1[d], a.b1[d], g, s_z + d * SC_G + g);
+  sc_project(s_x, F, T, a.k1[d], a.b1[d], g, tq, s_z + d * SC_G + g);
   __syncthreads();
   sc_recur(s_z, s_mask, T, a.r1[d], d, g, tid, s_h, s_act, s_seq, s_v);
 
   // layer 2: Bidirectional(LSTM(32)) over the 64-wide sequence
-  sc_project(s_seq, 2 * SC_U, T, a.k2[d], a.b2[d], g, s_z + d * SC_G + g);
+  sc_project(s_seq, 2 * SC_U, T, a.k2[d], a.b2[d], g, tq, s_z + d * SC_G + g);
   __syncthreads();
   sc_recur(s_z, s_mask, T, a.r2[d], d, g, tid, s_h, s_act, nullptr, s_v);
 
@@ -169,29 +194,29 @@ __global__ __launch_bounds__(SC_THREADS) void sign_classify_kernel(SignArgs a) {
   }
   __syncthreads();
   float mx = -INFINITY;
-  for (int c = tid; c < C; c += SC_THREADS) {
+  for (int c = tid; hw && c < C; c += SC_THREADS) {
     float acc = a.b3[c];
     for (int i = 0; i < SC_D; ++i) acc += s_y2[i] * a.d3[i * C + c];
     s_logit[c] = acc;
     mx = fmaxf(mx, acc);
   }
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if ((tid & 63) == 0) s_red[tid / 64] = mx;
+  if (hw && (tid & 63) == 0) s_red[tid / 64] = mx;
   __syncthreads();
   mx = fmaxf(fmaxf(s_red[0], s_red[1]), fmaxf(s_red[2], s_red[3]));
   __syncthreads();
   float sum = 0.0f;
-  for (int c = tid; c < C; c += SC_THREADS) {
+  for (int c = tid; hw && c < C; c += SC_THREADS) {
     const float e = expf(s_logit[c] - mx);
     s_logit[c] = e;
     sum += e;
   }
   for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-  if ((tid & 63) == 0) s_red[tid / 64] = sum;
+  if (hw && (tid & 63) == 0) s_red[tid / 64] = sum;
   __syncthreads();
   sum = (s_red[0] + s_red[1]) + (s_red[2] + s_red[3]);
   float* out = a.out + (size_t)blockIdx.x * C;
-  for (int c = tid; c < C; c += SC_THREADS) out[c] = s_logit[c] / sum;
+  for (int c = tid; hw && c < C; c += SC_THREADS) out[c] = s_logit[c] / sum;
 }
 
 // Offsets of keras `model.get_weights()` (Sequential order) in the flat buffer.
@@ -246,7 +271,7 @@ extern "C" int isl_sign_classify(const float* d_params, int n_features, int wind
   a.F = n_features;
   a.C = n_classes;
   sign_layout(n_features, n_classes, &a, d_params);
-  hipLaunchKernelGGL(sign_classify_kernel, dim3(batch), dim3(SC_THREADS), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(sign_classify_kernel, dim3(batch), dim3(SC_BLOCK), 0, (hipStream_t)stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     set_error(std::string("sign_classify_kernel: ") + hipGetErrorString(e));

@@ -64,6 +64,17 @@ def test_keras_weight_layout_matches_native_count():
     assert len(w) == 28
 
 
+def test_keras_weights_npz_round_trip(tmp_path):
+    """np.savez(path, *model.get_weights()) -> load_keras_weights: same arrays, same order."""
+    w = translate.keras_default_weights(seed=5)
+    p = str(tmp_path / "w.npz")
+    np.savez(p, *w)
+    back = translate.load_keras_weights(p)
+    assert len(back) == len(w) == 28
+    for a, b in zip(w, back):
+        np.testing.assert_array_equal(a, b)
+
+
 def _trained_like_weights(F=156, K=167, seed=3):
     """Keras default init plus BN statistics of pixel-scale features, so the LSTMs see
     unit-scale inputs (as with trained weights) instead of saturating."""

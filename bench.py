@@ -12,9 +12,14 @@ The post stage is fed designed pose maps (3 persons per frame) so that its cost
 is that of real footage (raw outputs of random weights produce ~4k peaks, see
 SURVEY.md §8d); the network still runs in full every step.
 
-Multi-GPU: one process per GPU (torch.distributed.run), frames sharded across
-ranks with no collective on the data path (weak scaling); a barrier + sync
-brackets the timed region and rank 0 reports the max-over-ranks time.
+Multi-GPU: one process per GPU, frames sharded across ranks with no collective
+on the data path (weak scaling).  `--gpus N` without a WORLD_SIZE in the
+environment starts the N rank processes itself (islpose.parallel.spawn_ranks);
+under torch.distributed.run the ranks come from the environment.  A barrier +
+device sync brackets the timed region; rank 0 reports the max-over-ranks time.
+The barrier and the timing reductions run on gloo over the host: nothing on the
+data path needs RCCL.  `--dry-run` exercises that whole launch / shard / gather
+structure on the CPU (tests/test_bench_launch.py).
 """
 from __future__ import annotations
 
@@ -31,9 +36,12 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from islpose import parallel  # noqa: E402
+
 METRIC = "frames/sec body_25 368×656 fwd+NMS+PAF at 1/8 MI355X; conv MFMA util %"
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix peak (spec) = 256 CU x 4 SIMD x 64 FLOP/clk x 2.4 GHz
 PEAK_FP16_MFMA_TFLOPS = 2516.6     # dense FP16/BF16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF, no sparsity)
+PEAK_HBM_GBPS = 8000.0             # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 KIND = {0: "maxpool2_kernel", 1: "conv_mfma_f32 (direct fp32)", 2: "wino_f23_mfma (Winograd F(2x2,3x3) fp32)",
         3: "conv_x3_f16 (split-fp16 x3, fp32-accurate)",
         4: "wino_x3_f16 (Winograd F(2x2,3x3), split-fp16 x3, fp32-accurate)"}
@@ -42,7 +50,7 @@ ALG_FACTOR = {1: 1.0, 2: 16.0 / 36.0, 3: 3.0, 4: 3.0 * 16.0 / 36.0}
 KIND_PEAK = {1: PEAK_FP32_MFMA_TFLOPS, 2: PEAK_FP32_MFMA_TFLOPS, 3: PEAK_FP16_MFMA_TFLOPS, 4: PEAK_FP16_MFMA_TFLOPS}
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
@@ -61,39 +69,111 @@ def parse():
                    help="conv arithmetic: split-fp16 x3 on the FP16 matrix cores (default), Winograd or direct fp32")
     p.add_argument("--cpu-frames", type=int, default=6, help="frames for the CPU baseline sample (0 = skip)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--e2e-steps", type=int, default=3,
+                   help="batches timed through the caller path (host frames in, Python results out); 0 = skip")
     p.add_argument("--split-k", action="store_true",
                    help="split-K on small conv grids (isl_net_set_split_k): batch-1 latency mode")
-    return p.parse_args()
+    p.add_argument("--dry-run", action="store_true",
+                   help="no GPU: run the rank launch, shard and max-over-ranks timing structure only")
+    return p.parse_args(argv)
+
+
+def rank_env():
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def init_group(world):
+    """Host-side (gloo) group for the barrier and the timing reductions only."""
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.distributed.init_process_group("gloo")
+        assert torch.distributed.get_world_size() == world
+
+
+def gather_floats(vals, world):
+    """All ranks' float vectors (host gloo all_gather) -> [world, len(vals)] numpy."""
+    t = torch.tensor(vals, dtype=torch.float64)
+    if world == 1:
+        return t[None].numpy()
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    torch.distributed.all_gather(parts, t)
+    return torch.stack(parts).numpy()
+
+
+def frame_shard(rank, batch):
+    """Frame indices of one rank's per-step batch: disjoint across ranks (weak scaling)."""
+    return rank * batch, (rank + 1) * batch
 
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launcher: N rank processes, this process never touches the GPU
+        codes, out0 = parallel.spawn_ranks([os.path.abspath(__file__)] + sys.argv[1:], args.gpus)
+        sys.stdout.write(out0 or "")
+        sys.stdout.flush()
+        sys.exit(next((c for c in codes if c), 0))
+    rank, local, world = rank_env()
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    init_group(world)
+    try:
+        if args.dry_run:
+            dry_run(args, rank, world)
+        else:
+            gpu_main(args, rank, local, world)
+    finally:
+        if world > 1:
+            torch.distributed.destroy_process_group()
 
+
+def dry_run(args, rank, world):
+    """The launch / shard / timing skeleton of gpu_main without a GPU: every rank
+    'processes' its own frame shard per step; rank 0 prints what the real run
+    would report about ranks and shards."""
+    lo, hi = frame_shard(rank, args.batch)
+    for _ in range(args.warmup):
+        pass
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    g = gather_floats([elapsed, lo, hi], world)
+    if rank != 0:
+        return
+    print(json.dumps({"dry_run": True, "n_gpus": world,
+                      "world_observed": torch.distributed.get_world_size() if world > 1 else 1,
+                      "shards": [[int(a), int(b)] for a, b in g[:, 1:]],
+                      "elapsed_max_s": float(g[:, 0].max()), "steps": args.steps, "warmup": args.warmup}))
+
+
+def gpu_main(args, rank, local, world):
+    import ctypes
+
+    from islpose import runtime as rt
     from islpose import synth
     from islpose.body import BodyEstimator, scale_geometry
 
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     B, H, W = args.batch, args.height, args.width
     S = args.streams
     assert B % S == 0, "batch must split evenly over the streams"
     weights = synth.synth_weights(0)
-    # frames of this rank (frame index = rank * B + i: disjoint shards)
-    frames = torch.from_numpy(synth.synth_frames(B, H, W, seed=1000 + rank)).to(dev)
+    lo, hi = frame_shard(rank, B)
+    # frames of this rank: indices [lo, hi), disjoint shards
+    frames_h = synth.synth_frames(B, H, W, seed=1000 + rank)
+    frames = torch.from_numpy(frames_h).to(dev)
     (mult, nh, nw, vh, vw), = scale_geometry(H, W, (args.scale,))
     geoms = [(nh, nw, vh, vw)]
-    maps = [synth.designed_pose_maps(nh // 8, nw // 8, args.persons, seed=rank * B + i) for i in range(B)]
+    maps = [synth.designed_pose_maps(nh // 8, nw // 8, args.persons, seed=i) for i in range(lo, hi)]
     d_paf = torch.from_numpy(np.stack([m[0] for m in maps])).to(dev)
     d_heat = torch.from_numpy(np.stack([m[1] for m in maps])).to(dev)
-    import ctypes
-    from islpose import runtime as rt
     L = rt.lib()
     main_stream = torch.cuda.current_stream(dev)
 
@@ -134,12 +214,11 @@ def main():
             e0.record(ln.stream)
             ln.net.run(stream=ln.stream)
             e1.record(ln.stream)
-            marks.append((e0, e1))
             rt.check(L.isl_body_post(ln.net.h, ln.b, H, W, 1, ln.g, ln.pp, ln.hp, ctypes.byref(ln.caps),
                                      rt.ptr(ln.d_res), ln.sh), "post")
             e2 = torch.cuda.Event(enable_timing=True)
             e2.record(ln.stream)
-            marks[-1] = (e0, e1, e2)
+            marks.append((e0, e1, e2))
             with torch.cuda.stream(ln.stream):
                 ln.h_res.copy_(ln.d_res, non_blocking=True)
         for ln in lanes:
@@ -174,14 +253,14 @@ def main():
         assert ln.net.range_ok(), "split-fp16 range exceeded in warmup"
     for ln in lanes:
         ln.net.set_timing(True)      # per-op HIP events on each lane's stream, inside the timed region
-    if dist:
-        torch.distributed.barrier()
     torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize(dev)
-    if dist:
+    if world > 1:
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     for ln in lanes:
@@ -189,13 +268,11 @@ def main():
     ops = [ln.net.timing() for ln in lanes]
     net_ms = float(np.mean([net_window_ms(r, m) for r, m in ev]))
     post_ms = float(np.mean([post_window_ms(r, m) for r, m in ev]))
-    if dist:
-        t = torch.tensor([elapsed, net_ms, post_ms], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed, net_ms, post_ms = float(t[0]), float(t[1]), float(t[2])
+    e2e = e2e_rate(args, lanes[0].est, frames_h, maps, dev) if args.e2e_steps > 0 else None
+    g = gather_floats([elapsed, net_ms, post_ms, B * args.steps / elapsed, lo, hi,
+                       e2e["frames_per_s"] if e2e else 0.0], world)
+    elapsed, net_ms, post_ms = float(g[:, 0].max()), float(g[:, 1].max()), float(g[:, 2].max())
     if rank != 0:
-        if dist:
-            torch.distributed.destroy_process_group()
         return
     total_frames = B * world * args.steps
     fps = total_frames / elapsed
@@ -245,6 +322,10 @@ def main():
                    "batch_per_gpu": B, "frame_hw": [H, W], "scale_search": [args.scale], "net_hw": [nh, nw],
                    "streams_per_gpu": S, "conv_algo": args.algo, "split_k": bool(args.split_k),
                    "parallelism": "frame-sharded x%d (no collective)" % world},
+        "ranks": {"world_observed": torch.distributed.get_world_size() if world > 1 else 1,
+                  "per_rank_frames_per_s": [round(float(v), 2) for v in g[:, 3]],
+                  "frame_shards": [[int(a), int(b)] for a, b in g[:, 4:6]],
+                  "timing_collectives": "gloo (host): barrier + all_gather of per-rank times; no data-path collective"},
         "roofline": {"bound": "mfma", "kernel": KIND[dom],
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -266,25 +347,69 @@ def main():
                      "mfma_busy_pmc": mfma_busy,
                      "effective_clock_ghz": clk,
                      "frac_at_effective_clock": round(achieved / (peak * clk / 2.4), 4) if clk else None},
-        "post": {
-            "ms_per_step": round(post_ms, 3),
-            "frames_per_s": round(B / (post_ms * 1e-3), 1),
-            "nms_algorithmic_bytes_per_frame": 25 * H * W * 4,
-            "nms_effective_GBps": round(25 * H * W * 4 * B / (post_ms * 1e-3) / 1e9, 1),
-            "paf_pairs_per_frame": round(pairs / B, 1),
-            "paf_pairs_per_s": round(pairs / (post_ms * 1e-3), 1),
-            "basis": "HIP events around isl_body_post on the lane stream (fused resize+blur+NMS, peak lists, PAF "
-                     "scoring, greedy matching, assembly; D2H excluded). nms_effective_GBps = SURVEY 8(d)'s NMS "
-                     "bytes (25 x H x W x 4 B f32 heat per frame) / whole post time: the fused kernel never "
-                     "materialises those planes, so this is an effective rate, not HBM traffic",
-        },
+        "post": post_fields(H, W, B, post_ms, pairs),
+        "e2e": e2e,
         "cpu_baseline": None,
     }
     if not args.no_cpu and args.cpu_frames > 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(args, mult, nh, nw)
     print(json.dumps(out))
-    if dist:
-        torch.distributed.destroy_process_group()
+    sys.stdout.flush()
+
+
+def post_fields(H, W, B, post_ms, pairs):
+    """The metric's "NMS and PAF" part: live post time (HIP events around isl_body_post),
+    plus the counter-backed HBM traffic and rocprof durations of the NMS / PAF kernels
+    from the last committed profile (profiles/post_traffic.json)."""
+    out = {
+        "ms_per_step": round(post_ms, 3),
+        "frames_per_s": round(B / (post_ms * 1e-3), 1),
+        "nms_algorithmic_bytes_per_frame": 25 * H * W * 4,
+        "nms_effective_GBps": round(25 * H * W * 4 * B / (post_ms * 1e-3) / 1e9, 1),
+        "paf_pairs_per_frame": round(pairs / B, 1),
+        "paf_pairs_per_s": round(pairs / (post_ms * 1e-3), 1),
+        "basis": "HIP events around isl_body_post on the lane stream (fused resize+blur+NMS, peak lists, PAF "
+                 "scoring, greedy matching, assembly; D2H excluded). nms_effective_GBps = SURVEY 8(d)'s NMS "
+                 "bytes (25 x H x W x 4 B f32 heat per frame) / whole post time: the fused kernel never "
+                 "materialises those planes, so this is an effective rate, not HBM traffic",
+    }
+    prof = os.path.join(REPO, "profiles", "post_traffic.json")
+    if os.path.exists(prof):
+        pj = json.load(open(prof))
+        out["pmc"] = {k: pj[k] for k in ("blur_nms_kernel", "limb_kernel", "tile_live_kernel", "compact_kernel")
+                      if k in pj}
+        out["pmc_source"] = pj.get("source")
+        out["pmc_peak_GBps"] = PEAK_HBM_GBPS
+        out["pmc_basis"] = pj.get("note")
+    return out
+
+
+def e2e_rate(args, est, frames_h, maps, dev):
+    """Caller-path rate (what Body.estimate_batch users get): host uint8 frames -> H2D ->
+    preprocess + net -> post on the designed maps -> D2H of the records -> Python decode
+    into (candidate, subset) per frame.  Timed per batch, after the main timed region."""
+    from islpose.body import scale_geometry
+    H, W = frames_h.shape[1:3]
+    geoms = [g[1:] for g in scale_geometry(H, W, (args.scale,))]
+    paf = torch.from_numpy(np.stack([m[0] for m in maps])).to(dev)
+    heat = torch.from_numpy(np.stack([m[1] for m in maps])).to(dev)
+
+    def once():
+        t = torch.from_numpy(frames_h).to(dev)
+        est.run_scales(t)
+        return est.post_maps(H, W, geoms, [paf], [heat], details=False)
+
+    once()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.e2e_steps):
+        res = once()
+    dt = (time.perf_counter() - t0) / args.e2e_steps
+    assert len(res) == len(frames_h)
+    return {"frames_per_s": round(len(frames_h) / dt, 2), "ms_per_batch": round(dt * 1e3, 3),
+            "batch": len(frames_h), "batches_timed": args.e2e_steps,
+            "basis": "host frames -> H2D -> preprocess + body_25 -> isl_body_post (designed maps) -> D2H -> "
+                     "BodyEstimator.decode to the reference's (candidate, subset); wall time per batch, rank 0"}
 
 
 def cpu_baseline(args, mult, nh, nw):
@@ -293,8 +418,10 @@ def cpu_baseline(args, mult, nh, nw):
     for the post exactly as on the GPU."""
     from oracle import cpu_ref
     from islpose import synth
-    cores = len(os.sched_getaffinity(0))
-    cores = min(cores, 16)
+    affinity = len(os.sched_getaffinity(0))
+    # the GPU box exports OMP_NUM_THREADS = its CPU share per GPU: honour it, report both
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cores = min(affinity, omp) if omp > 0 else affinity
     torch.set_num_threads(cores)
     w = synth.synth_weights(0)
     fwd = cpu_ref.make_net_fn("body25", w)
@@ -312,6 +439,9 @@ def cpu_baseline(args, mult, nh, nw):
         t_post.append(t2 - t1)
     per = float(np.median(t_fwd[1:] if len(t_fwd) > 2 else t_fwd)) + float(np.median(t_post[1:] if len(t_post) > 2 else t_post))
     return {"value": round(1.0 / per, 4), "unit": "frames/s", "cores": cores, "kind": "port",
+            "affinity_cores": affinity,
+            "threads_basis": "torch.set_num_threads(min(len(sched_getaffinity), OMP_NUM_THREADS)) = %d; "
+                             "OMP_NUM_THREADS=%s is the box's CPU share per GPU" % (cores, omp or "unset"),
             "sample": "%d frames %dx%d (scale %.2f, net %dx%d), median of frames 2..N: fwd %.3f s + post %.3f s per frame"
                       % (args.cpu_frames, args.height, args.width, args.scale, nh, nw,
                          float(np.median(t_fwd[1:])), float(np.median(t_post[1:])))}

@@ -8,9 +8,10 @@
  *                  (src/model.py:179-207, 302-329, 394-407), weights loaded through
  *                  util.transfer (src/util.py:35-44)          -> isl_net_create,
  *                  isl_net_set_param, isl_net_forward
- *   frame seam   : Body.__call__ (src/body.py:39-235)         -> isl_body_preprocess +
- *                  isl_net_run + isl_body_post (isl_body_estimate chains them)
- *                  Hand.__call__ (src/hand.py:24-74)          -> isl_hand_post
+ *   frame seam   : Body.__call__ (src/body.py:39-235)         -> isl_net_preprocess
+ *                  (one call per pyramid scale) + isl_net_run + isl_body_post
+ *                  Hand.__call__ (src/hand.py:24-74)          -> isl_net_preprocess /
+ *                  isl_net_preprocess_crops + isl_net_run + isl_hand_post
  *
  * Conventions
  *   - every function returns 0 (ISL_OK) or a negative ISL_E_* code and records a
@@ -111,6 +112,15 @@ int isl_net_preprocess_crops(isl_net* net, const uint8_t* d_frames, int n_frames
  * in the arena (low-res, 8-channel chunks) for the post kernels, and are also
  * copied to d_out0/d_out1 (NCHW) when those are non-NULL. */
 int isl_net_run(isl_net* net, float* d_out0, float* d_out1, void* stream);
+
+/* Activation arenas (not in the reference: torch's caching allocator plays this
+ * role there).  A net keeps one arena per net input size (h, w), sized by
+ * capacity: a batch of n frames reuses an arena holding n' >= n frames, and a
+ * larger n replaces it.  Arenas of other sizes are evicted least-recently-used
+ * once the net's arenas would exceed the byte budget (env ISLPOSE_ARENA_BUDGET_MB,
+ * default 65536; the arena in use is never evicted).  Reports the bytes held and
+ * the number of arenas. */
+int isl_net_arena_info(const isl_net* net, int64_t* bytes, int* n_arenas);
 
 /* Select the conv arithmetic of a net (default ISL_ALGO_X3, or the env
  * ISLPOSE_CONV_ALGO=x3|wino|direct at create time). */

@@ -11,6 +11,7 @@
 #include <array>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -196,9 +197,18 @@ struct isl_net {
   // plan
   int pn = 0, ph = 0, pw = 0;
   std::vector<Act> act;
-  std::map<long long, std::pair<void*, std::vector<Act>>> plans;
+  // activation arenas by net input size (h, w), sized by frame capacity (plan())
+  struct Arena {
+    void* base = nullptr;
+    int n_cap = 0;
+    std::vector<size_t> offs;   // buffer offsets for n_cap frames
+    size_t bytes = 0;
+    unsigned long long last_use = 0;
+  };
+  std::map<long long, Arena> plans;
+  unsigned long long plan_clock = 0;
+  size_t plans_bytes = 0;
   void* arena = nullptr;
-  size_t arena_bytes = 0;
   // post scratch
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -563,37 +573,78 @@ static int upload_params(isl_net* net) {
   return ISL_OK;
 }
 
-// Activation arena per (n, h, w): cached, so the scales of a pyramid (or the 4
-// hand scales) each keep their own arena instead of reallocating per call.
-static int plan(isl_net* net, int n, int h, int w) {
-  if (net->pn == n && net->ph == h && net->pw == w && net->arena) return ISL_OK;
-  if (n <= 0 || h < 8 || w < 8) return fail(ISL_E_ARG, "net input must be at least 8x8 with n >= 1");
-  const long long key = ((long long)n << 40) | ((long long)h << 20) | w;
-  auto it = net->plans.find(key);
-  if (it != net->plans.end()) {
-    net->arena = it->second.first;
-    net->act = it->second.second;
-    net->pn = n; net->ph = h; net->pw = w;
-    return ISL_OK;
+// Activation arenas: one per net input size (h, w), sized by frame capacity, so
+// the scales of a pyramid (or the 4 hand scales) keep their own arena instead of
+// reallocating per call, and a batch of n frames reuses an arena that holds
+// n' >= n (the buffers of the n'-frame layout hold any n <= n' frames; their
+// rings and gap channels were zeroed once and no kernel writes them).  A larger n
+// replaces the arena of its size; arenas of other sizes are evicted least-recently-
+// used when the net's total would pass the budget.  Variable crop counts
+// (HandEstimator.estimate_crops) therefore cost at most one arena per hand scale,
+// of the largest count seen.
+static size_t arena_budget() {
+  static const size_t b = [] {
+    const char* e = getenv("ISLPOSE_ARENA_BUDGET_MB");
+    const long long mb = e ? atoll(e) : 65536;
+    return (size_t)(mb > 0 ? mb : 65536) << 20;
+  }();
+  return b;
+}
+
+static void drop_arena(isl_net* net, std::map<long long, isl_net::Arena>::iterator it) {
+  // hipFree waits for queued work that may still use the arena
+  (void)hipFree(it->second.base);
+  net->plans_bytes -= it->second.bytes;
+  if (net->arena == it->second.base) {
+    net->arena = nullptr;
+    net->pn = net->ph = net->pw = 0;
   }
-  int lh[4] = {h, h / 2, h / 4, h / 8}, lw[4] = {w, w / 2, w / 4, w / 8};
-  net->arena = nullptr;
+  net->plans.erase(it);
+}
+
+static int plan(isl_net* net, int n, int h, int w) {
+  if (n <= 0 || h < 8 || w < 8) return fail(ISL_E_ARG, "net input must be at least 8x8 with n >= 1");
+  const long long key = ((long long)h << 20) | w;
+  auto it = net->plans.find(key);
+  if (it != net->plans.end() && it->second.n_cap < n) {
+    drop_arena(net, it);
+    it = net->plans.end();
+  }
+  if (it == net->plans.end()) {
+    const int lh0[4] = {h, h / 2, h / 4, h / 8}, lw0[4] = {w, w / 2, w / 4, w / 8};
+    isl_net::Arena ar;
+    ar.n_cap = n;
+    for (const BufSpec& b : net->bufs) {
+      Act a;
+      a.n = n; a.H = lh0[b.level]; a.W = lw0[b.level]; a.pad = b.pad; a.cs = b.cs;
+      ar.offs.push_back(ar.bytes);
+      ar.bytes += (a.bytes() + 255) / 256 * 256;
+    }
+    // LRU eviction of the other sizes' arenas over the budget
+    while (net->plans_bytes + ar.bytes > arena_budget() && !net->plans.empty()) {
+      auto lru = net->plans.begin();
+      for (auto j = net->plans.begin(); j != net->plans.end(); ++j)
+        if (j->second.last_use < lru->second.last_use) lru = j;
+      drop_arena(net, lru);
+    }
+    HIP_OK(hipMalloc(&ar.base, ar.bytes));
+    HIP_OK(hipMemset(ar.base, 0, ar.bytes));  // zero rings and gap channels, once
+    net->plans_bytes += ar.bytes;
+    it = net->plans.emplace(key, std::move(ar)).first;
+  }
+  isl_net::Arena& ar = it->second;
+  ar.last_use = ++net->plan_clock;
+  if (net->arena == ar.base && net->pn == n && net->ph == h && net->pw == w) return ISL_OK;
+  const int lh[4] = {h, h / 2, h / 4, h / 8}, lw[4] = {w, w / 2, w / 4, w / 8};
   net->act.assign(net->bufs.size(), Act{});
-  size_t total = 0;
-  std::vector<size_t> offs;
   for (size_t i = 0; i < net->bufs.size(); ++i) {
     const BufSpec& b = net->bufs[i];
     Act& a = net->act[i];
     a.n = n; a.H = lh[b.level]; a.W = lw[b.level]; a.pad = b.pad; a.cs = b.cs;
-    offs.push_back(total);
-    total += (a.bytes() + 255) / 256 * 256;
+    a.base = (float*)((char*)ar.base + ar.offs[i]);
   }
-  HIP_OK(hipMalloc(&net->arena, total));
-  HIP_OK(hipMemset(net->arena, 0, total));  // zero rings and gap channels, once
-  for (size_t i = 0; i < net->bufs.size(); ++i) net->act[i].base = (float*)((char*)net->arena + offs[i]);
-  net->arena_bytes = total;
+  net->arena = ar.base;
   net->pn = n; net->ph = h; net->pw = w;
-  net->plans[key] = {net->arena, net->act};
   return ISL_OK;
 }
 
@@ -769,7 +820,7 @@ int isl_net_destroy(isl_net* net) {
   }
   if (net->d_flag) (void)hipFree(net->d_flag);
   if (net->d_tab) (void)hipFree(net->d_tab);
-  for (auto& kv : net->plans) (void)hipFree(kv.second.first);
+  for (auto& kv : net->plans) (void)hipFree(kv.second.base);
   if (net->scratch) (void)hipFree(net->scratch);
   if (net->d_ks) (void)hipFree(net->d_ks);
   for (auto& r : net->timed)
@@ -973,6 +1024,13 @@ int isl_net_check(isl_net* net, int clear) {
 }
 
 const int* isl_net_range_flag(const isl_net* net) { return net ? net->d_flag : nullptr; }
+
+int isl_net_arena_info(const isl_net* net, int64_t* bytes, int* n_arenas) {
+  if (!net) return fail(ISL_E_ARG, "net is NULL");
+  if (bytes) *bytes = (int64_t)net->plans_bytes;
+  if (n_arenas) *n_arenas = (int)net->plans.size();
+  return ISL_OK;
+}
 
 int isl_net_run(isl_net* net, float* d_out0, float* d_out1, void* stream) {
   if (!net || !net->arena) return fail(ISL_E_STATE, "isl_net_run before isl_net_preprocess");

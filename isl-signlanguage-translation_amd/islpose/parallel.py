@@ -26,6 +26,37 @@ def dist_env():
             int(os.environ.get("WORLD_SIZE", "1")))
 
 
+def free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(argv, world: int, env=None):
+    """Start `world` child processes running `argv` (one per GPU: RANK = LOCAL_RANK =
+    r, WORLD_SIZE = world, rendezvous on 127.0.0.1) -- the launcher the reference
+    builds from mp.Process (extract_features_mp.py:205-220), with every child on its
+    own device instead of cuda:0.  The caller must not have touched the GPU (children
+    are separate processes, never an exec of this one).  Returns (exit codes, rank-0
+    stdout); the other ranks' stdout and every stderr pass through."""
+    import subprocess
+    import sys
+    port = free_port()
+    procs = []
+    for r in range(world):
+        e = dict(os.environ if env is None else env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=e,
+                                      stdout=subprocess.PIPE if r == 0 else None, text=True))
+    out0 = procs[0].communicate()[0]
+    codes = [p.wait() for p in procs]
+    return codes, out0
+
+
 def run_sharded(n_frames, get_frames, estimate, batch: int, rank: int, world: int):
     """Process this rank's shard in batches: get_frames(start, end) -> frames,
     estimate(frames) -> list of per-frame results. Returns [(frame_index, result)]."""

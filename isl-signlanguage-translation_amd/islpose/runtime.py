@@ -24,7 +24,7 @@ EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destr
            "isl_net_param_info", "isl_net_set_param", "isl_net_forward", "isl_net_preprocess", "isl_net_run", "isl_net_debug_input",
            "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post",
            "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops",
-           "isl_sign_param_count", "isl_sign_classify", "isl_net_set_split_k"]
+           "isl_sign_param_count", "isl_sign_classify", "isl_net_set_split_k", "isl_net_arena_info"]
 
 
 class IslCaps(ctypes.Structure):
@@ -88,6 +88,7 @@ def lib():
     L.isl_hand_post.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp), vp, vp]
     L.isl_sign_param_count.argtypes = [i32, i32, ctypes.POINTER(i64)]
     L.isl_net_set_split_k.argtypes = [vp, i32]
+    L.isl_net_arena_info.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i32)]
     L.isl_sign_classify.argtypes = [vp, i32, i32, i32, vp, i32, vp, vp]
     for name in EXPORTS[2:]:
         getattr(L, name).restype = i32
@@ -134,6 +135,7 @@ class Net:
         check(lib().isl_net_create(kind, device, ctypes.byref(h)), "isl_net_create")
         self.h = h
         self.loaded = False
+        self.split_k = os.environ.get("ISLPOSE_X3_SPLITK", "")[:1] == "1"   # isl_net_create's default
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -202,6 +204,7 @@ class Net:
     def set_split_k(self, on: bool):
         """Split-K for small grids (batch-1 latency, ~2x at 184x328); see isl_net_set_split_k."""
         check(lib().isl_net_set_split_k(self.h, int(bool(on))), "isl_net_set_split_k")
+        self.split_k = bool(on)
 
     def algo_scope(self, algo: str):
         import contextlib
@@ -252,6 +255,12 @@ class Net:
 
     def run(self, out0=None, out1=None, stream=None):
         check(lib().isl_net_run(self.h, ptr(out0), ptr(out1), stream_handle(stream)), "isl_net_run")
+
+    def arena_info(self):
+        """(bytes, arenas) of the net's activation arenas (isl_net_arena_info)."""
+        b, k = ctypes.c_int64(), ctypes.c_int32()
+        check(lib().isl_net_arena_info(self.h, ctypes.byref(b), ctypes.byref(k)), "isl_net_arena_info")
+        return b.value, k.value
 
     def set_timing(self, on: bool):
         """Record HIP events around every op of the following runs (isl_net_set_timing)."""

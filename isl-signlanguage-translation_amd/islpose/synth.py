@@ -108,13 +108,16 @@ COCO_MAPIDX = [[12, 13], [20, 21], [14, 15], [16, 17], [22, 23], [24, 25], [0, 1
 
 
 def designed_pose_maps(h8: int, w8: int, n_persons: int, seed: int, model_type: str = "body25",
-                       sigma: float = 1.0, strip: float = 1.0):
+                       sigma: float = 1.0, strip: float = 1.0, drop_limbs=()):
     """Low-resolution (paf, heat) maps, NCHW without batch: ([npaf,h8,w8], [njoint,h8,w8]) f32.
 
     Persons are placed left to right with seeded jitter; each keypoint is a
     Gaussian blob (std ``sigma`` low-res px), each limb a strip of unit vectors
-    (half-width ``strip``) in its two PAF channels.  The last heat channel is
-    the background (1 - max of parts).
+    (half-width ``strip``) in its two PAF channels, except the limbs listed in
+    ``drop_limbs`` (indices into the limb table): e.g. COCO limb 12 (neck -> nose)
+    dropped makes every head its own subset row until the redundant ear limbs 17/18
+    merge it into the body (the found == 2 branch of body.py:204-218).  The last
+    heat channel is the background (1 - max of parts).
     """
     if model_type == "body25":
         tmpl, limbs, mapidx, njoint, npaf = _BODY25_TEMPLATE, BODY25_LIMBS, BODY25_MAPIDX, 26, 52
@@ -139,6 +142,8 @@ def designed_pose_maps(h8: int, w8: int, n_persons: int, seed: int, model_type: 
             g[g < 1e-3] = 0.0          # truncated tails keep the maps sparse
             heat[k] = np.maximum(heat[k], g)
         for li, (a, b) in enumerate(limbs):
+            if li in drop_limbs:
+                continue
             pa, pb = kp[a], kp[b]
             d = pb - pa
             ln = np.hypot(d[0], d[1])

@@ -46,15 +46,38 @@ class ISLSignPos(object):
         self.npaf_body = 52
         self._body = None
         self._hand = None
+        self._device = None          # pinned by .to(); default: the current HIP device
+
+    def to(self, device):
+        """Pin the HIP device the keypoint nets run on and return self: the reference
+        class is a keras.Model, and extract_features_mp.py:150 / extract_featuressingle.py
+        :150 call ``model.to(device)``.  A CPU device leaves the placement unchanged
+        (the engine runs on the GPU only)."""
+        d = torch.device(device)
+        if d.type == "cuda":
+            self._device = d.index if d.index is not None else torch.cuda.current_device()
+        return self
 
     def _estimators(self):
-        dev = torch.cuda.current_device()
+        dev = self._device if self._device is not None else torch.cuda.current_device()
         bnet, hnet = self.pt_body.native(dev), self.pt_hand.native(dev)
         if self._body is None or self._body.net is not bnet:
             self._body = BodyEstimator(model_type="body25", device=dev, scale_search=(0.5,), net=bnet)
         if self._hand is None or self._hand.net is not hnet:
             self._hand = HandEstimator(device=dev, net=hnet)
         return self._body, self._hand
+
+    def state_key(self):
+        """Identity of what produces the keypoints: the two modules, their current
+        parameters (storage and in-place version, as _NativeNet.native() tracks them)
+        and the native nets' split-K state."""
+        def part(m):
+            if m is None:
+                return (None,)
+            net = getattr(m, "_native_net", None)
+            return (id(m), tuple((p.data_ptr(), p._version) for p in m.parameters()),
+                    getattr(net, "split_k", None))
+        return part(self.pt_body) + part(self.pt_hand)
 
     def bodypos(self, oriImg):
         return self._estimators()[0].estimate(np.ascontiguousarray(_as_numpy(oriImg), dtype=np.uint8))
@@ -111,6 +134,7 @@ class ISLSignPosTranslator(ISLSignPos):
         self.model_type = 'body25'
         self.translation_layer = translation_model
         self._rows = collections.OrderedDict()
+        self._rows_key = None
 
     def populate_features(self, bodypose_circles, handpose_peaks):
         return translate.populate_features(bodypose_circles, handpose_peaks)
@@ -135,7 +159,14 @@ class ISLSignPosTranslator(ISLSignPos):
         """Feature rows of frames, reusing the rows of frames seen in recent calls (keyed by
         a 128-bit hash of the pixels): the demo's rolling window (demo_isl_translate.py:
         183-190) shares 19 of its 20 frames with the previous call, so only the new frame
-        goes through the keypoint nets.  Rows are identical to computing them afresh."""
+        goes through the keypoint nets.  The cache is dropped whenever the nets, their
+        weights or their split-K state change (ISLSignPos.state_key), so rows are those of
+        computing them afresh (up to the range guard: a batch recomputed on the fp32
+        kernels gives rows within the fp32 tolerance, not the same bits)."""
+        state = self.state_key()
+        if self._rows_key != state:
+            self._rows.clear()
+            self._rows_key = state
         keys = [(f.shape, xxhash.xxh3_128_digest(np.ascontiguousarray(f))) for f in frames]
         miss = [i for i, k in enumerate(keys) if k not in self._rows]
         if miss:

@@ -3,9 +3,13 @@
 Follows /root/reference/src/util.py:
   padRightDownCorner 12-32, transfer 35-44, get_bodypose 99-151,
   get_handpose 187-219, handDetect 242-306, npmax 394-399.
-The drawing helpers (draw_bodypose, draw_handpose, drawStickmodel, ...) render
-with OpenCV/matplotlib after the path; they are out of scope here
-and raise NotImplementedError.
+The drawing helpers (draw_bodypose, draw_handpose, draw_handpose_by_opencv,
+drawStickmodel, crop_to_drawing; util.py:47-96,154-185,222-238,308-391) render with
+OpenCV/matplotlib after the path and are out of scope of the engine (SURVEY §2 row
+5): they call the reference's own util.py (the original ``src`` this package falls
+through to, see src/__init__.py), so extract_features_mp.py's ``test = True``
+rendering (:57, :90) works where the reference's dependencies are installed.
+Without the original ``src`` they raise NotImplementedError.
 """
 from __future__ import annotations
 
@@ -133,8 +137,42 @@ def get_handpose(all_hand_peaks, show_number=False):
     return (export_edges, export_peaks)
 
 
-def _drawing(*_a, **_k):
-    raise NotImplementedError("drawing helpers are presentation-only and out of scope of the MI355X engine")
+_reference_util = None
 
 
-draw_bodypose = draw_handpose = draw_handpose_by_opencv = drawStickmodel = crop_to_drawing = _drawing
+def reference_util():
+    """The reference's own util module (drawing helpers), loaded from the original
+    ``src`` directory under a private name; None when the original is not found."""
+    global _reference_util
+    if _reference_util is None:
+        import importlib.util
+        import os
+        from . import reference_src
+        d = reference_src()
+        if d is None or not os.path.isfile(os.path.join(d, "util.py")):
+            return None
+        spec = importlib.util.spec_from_file_location("src._reference_util", os.path.join(d, "util.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _reference_util = mod
+    return _reference_util
+
+
+def _drawing(name):
+    def fn(*args, **kwargs):
+        ref = reference_util()
+        if ref is None:
+            raise NotImplementedError(
+                "%s renders with OpenCV/matplotlib and is out of scope of the MI355X engine; it runs from the "
+                "reference's own src/util.py, which was not found (set ISLPOSE_REFERENCE_SRC or keep the original "
+                "src as src.orig)" % name)
+        return getattr(ref, name)(*args, **kwargs)
+    fn.__name__ = name
+    return fn
+
+
+draw_bodypose = _drawing("draw_bodypose")
+draw_handpose = _drawing("draw_handpose")
+draw_handpose_by_opencv = _drawing("draw_handpose_by_opencv")
+drawStickmodel = _drawing("drawStickmodel")
+crop_to_drawing = _drawing("crop_to_drawing")

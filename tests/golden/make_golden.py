@@ -207,6 +207,32 @@ def g2_body_post():
     return cases
 
 
+def g2_merge_cases():
+    """Extra G2 cases appended to g2_body_post.npz (the other cases are left as they
+    are): COCO maps with the neck -> nose limb (12) dropped, so every head first forms
+    its own subset row (limbs 13-16) and the redundant ear limbs 17/18 then join it to
+    the body row -- the found == 2 merge of body.py:204-218."""
+    path = os.path.join(HERE, "g2_body_post.npz")
+    z = dict(np.load(path))
+    spec = [("coco_merge_R_p1", (368, 656), (0.5,), 1, 31), ("coco_merge_R_p3", (368, 656), (0.5,), 3, 32),
+            ("coco_merge_N_p2", (368, 656), (1.0,), 2, 33)]
+    for name, hw, scales, persons, seed in spec:
+        def maps(h8, w8, persons=persons, seed=seed):
+            return synth.designed_pose_maps(h8, w8, persons, seed, "coco", drop_limbs=(12,))
+        outs, cand, subset, err = run_body("coco", hw, scales, maps)
+        z[name + "/model_type"] = np.array("coco")
+        z[name + "/frame_hw"] = np.array(hw)
+        z[name + "/scales"] = np.array(scales, np.float64)
+        for i, (paf, heat) in enumerate(outs):
+            z[name + "/paf%d" % i] = paf
+            z[name + "/heat%d" % i] = heat
+        z[name + "/candidate"] = cand
+        z[name + "/subset"] = subset
+        z[name + "/error"] = np.array(err)
+        print(name, "candidate", cand.shape, "subset", subset.shape, err)
+    np.savez_compressed(path, **z)
+
+
 def g4_hand_post():
     import src.hand as hand_mod
     out = {}
@@ -342,6 +368,9 @@ def main():
     install_shims()
     if sys.argv[1:] == ["g9"]:
         g9_translator_features()
+        return
+    if sys.argv[1:] == ["g2merge"]:
+        g2_merge_cases()
         return
     g7_state_dict_keys()
     g8_export_formats()

@@ -1,0 +1,48 @@
+"""bench.py's multi-rank launch on the CPU: `--gpus N` without a torch.distributed.run
+environment starts N rank processes itself (islpose.parallel.spawn_ranks), the ranks
+meet over gloo, shard the frames disjointly and rank 0 reports (extract_features_mp.py:
+183-239 is the reference's process launcher).  --dry-run keeps the GPU out of it."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env():
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    e["HIP_VISIBLE_DEVICES"] = ""
+    return e
+
+
+def _run(*argv):
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + list(argv), env=_env(),
+                          capture_output=True, text=True, timeout=240)
+
+
+def test_bench_spawns_two_ranks_dry_run():
+    r = _run("--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1", "--batch", "4")
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["world_observed"] == 2
+    assert out["shards"] == [[0, 4], [4, 8]]  # disjoint frame shards
+    assert out["steps"] == 3 and out["elapsed_max_s"] > 0
+
+
+def test_bench_single_rank_dry_run():
+    r = _run("--dry-run", "--steps", "1", "--warmup", "0", "--batch", "2")
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["n_gpus"] == 1 and out["shards"] == [[0, 2]]
+
+
+def test_bench_rejects_world_mismatch():
+    e = _env()
+    e.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"], env=e,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

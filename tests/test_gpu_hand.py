@@ -102,3 +102,21 @@ def test_hand_net_split_k(hest):
         assert torch.equal(h1, h2)
         d = (h1 - h0).abs().max().item() / max(h0.abs().max().item(), 1e-30)
         assert d < 1e-5, d
+
+
+def test_arena_bounded_over_crop_counts():
+    """estimate_crops with a different crop count per batch keeps one arena
+    per hand scale, sized by the largest count seen -- not one per (count, scale)."""
+    from islpose import runtime as rt
+    est = HandEstimator(synth.synth_weights(2))
+    frames = synth.synth_frames(2, 160, 200, seed=29)
+    counts = [3, 1, 5, 2, 4, 5, 1]
+    for c in counts:
+        boxes = [(i % 2, 10 + 7 * i, 5 + 3 * i, 60) for i in range(c)]
+        est.estimate_crops(frames, boxes)
+    used, n = est.net.arena_info()
+    assert n == len(HAND_SCALES), n
+    ref = HandEstimator(net=rt.Net(rt.ISL_HAND))
+    ref.net.load_weights(synth.synth_weights(2))
+    ref.estimate_crops(frames, [(i % 2, 10 + 7 * i, 5 + 3 * i, 60) for i in range(max(counts))])
+    assert used == ref.net.arena_info()[0]

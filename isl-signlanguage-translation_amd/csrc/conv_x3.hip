@@ -65,6 +65,7 @@ struct X3Args {
   int ksplit;                   // split-K (VAR 2048): blocks per tile, each over a range of chunk pairs
   int nfr;                      // frames (split-K partial-sum layout)
   float* ws;                    // split-K partial sums [ksplit][nfr][cout/8][H*W][8]
+  unsigned long long* dbg;      // VAR 16384 (development): s_memtime stamps of block 0
 };
 
 // input segment capacity in pixels for a BPX-pixel tile (host: tile_pixels)
@@ -104,6 +105,17 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   // partial sum of a contiguous range of chunk pairs into a.ws; x3_splitk_reduce
   // adds the ranges in a fixed order and applies the epilogue
   constexpr bool SPLIT = (VAR & 2048) != 0;
+  // VAR 4096 (with 512): branch-free union loop -- every load and DMA issued
+  // unconditionally (clamped addresses, zeroes selected at use, idle items write a
+  // dummy slot) so the compiler's counted waits leave the weight DMA of step t+1 in
+  // flight: no vmcnt(0) between the DMA issue and the K step's MFMAs
+  constexpr bool UCLEAN = (VAR & 4096) != 0;
+  // VAR 8192: bias / PReLU slopes staged in LDS before the epilogue, so the output
+  // stores stream without a global load (and its vmcnt(0)) between them
+  constexpr bool EPI_LDS = (VAR & 8192) != 0;
+  // VAR 16384 (development build of the branch-free union loop): lane 0 of every wave
+  // of block 0 stamps s_memtime at 4 points of each K step into a.dbg
+  constexpr bool STAMP = (VAR & 16384) != 0;
   constexpr bool NO_STAGE = (VAR & 8) != 0;      // ablation: skip global loads + LDS stores
   constexpr bool NO_MATH = (VAR & 16) != 0;      // ablation: skip LDS reads + MFMAs
   __shared__ f16x8 smem[SMEM];
@@ -375,6 +387,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
           }
       }
     };
+    if constexpr (!UCLEAN) {
     // prologue: weights of step 0, the whole union of pair 0
     issue_wu(0, 0);
     for (int ky = 0; ky < KS; ++ky) {
@@ -390,6 +403,121 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       compute_u(t & 1, c2 & 1, ky);
       if (next) store_u((c2 + 1) & 1);
       __syncthreads();
+    }
+    } else {
+    // Role-split form.  Issuing every wave's global loads and DMA pieces at the top of
+    // a K step stalls all 16 waves on the CU's vector-memory issue (~1.6k cycles per
+    // step, s_memtime stamps) before any of them reaches its MFMAs.  Here waves 0-9
+    // (the threads < third) stage the input union, waves 10-15 stream the weight
+    // slab, and both issue between MFMA groups: the DMA of step t+1 before the kx = 0
+    // group, the input loads of the next pair after it.
+    static_assert(NWAVES == 16, "role split sized for 16-wave blocks");
+    constexpr int LOADER_WAVES = 10, DMA_WAVES = NWAVES - LOADER_WAVES;
+    constexpr int NP = WSLAB / 64;                               // 1 KiB DMA pieces per step
+    constexpr int DPW = (NP + DMA_WAVES - 1) / DMA_WAVES;
+    const bool loader = wave_u < LOADER_WAVES;
+    int c_ih[KS], c_px[KS];
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky) {
+      const int it = ky * third + tid;
+      const bool ok = tid < third && it < 2 * segu;
+      c_ih[ky] = ok && it >= segu ? 1 : 0;
+      c_px[ky] = ok ? it - c_ih[ky] * segu : -1;
+    }
+    auto load_c = [&](int c2, int ky) __attribute__((always_inline)) {
+      if (c_px[ky] >= 0) {
+        const int c = min(2 * c2 + c_ih[ky], a.cin_chunks - 1);
+        const float* src = in_f + (size_t)c * a.in_chs + (size_t)(ubase + c_px[ky]) * 8;
+        ru[0] = *(const f32x4*)src;
+        ru[1] = *(const f32x4*)(src + 4);
+      }
+    };
+    auto store_c = [&](int c2, int ky, int bx) __attribute__((always_inline)) {
+      f16x8* sx = smem + 2 * WSLAB + bx * XSLABU;
+      const bool zero = 2 * c2 + c_ih[ky] >= a.cin_chunks;
+      f16x8 hi, lo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = zero ? 0.f : ru[j >> 2][j & 3];
+        hi[j] = (_Float16)x;
+        lo[j] = (_Float16)(x - (float)hi[j]);
+      }
+      const int px = c_px[ky] < 0 ? SEGUP - 1 : c_px[ky];   // idle items: the dummy slot
+      sx[(0 * 2 + c_ih[ky]) * SEGUP + px] = hi;
+      sx[(1 * 2 + c_ih[ky]) * SEGUP + px] = lo;
+    };
+    auto issue_c = [&](int t, int bw) __attribute__((always_inline)) {
+      const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
+      f16x8* dst = smem + bw * WSLAB;
+#pragma unroll
+      for (int k = 0; k < DPW; ++k) {
+        const int q = (wave_u - LOADER_WAVES) * DPW + k;
+        if (NP % DMA_WAVES == 0 || q < NP)
+          __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
+                                           (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
+      }
+    };
+    auto compute_kx = [&](int bw, int bx, int ky, int kx) __attribute__((always_inline)) {
+      const f16x8* sw = smem + bw * WSLAB + h * BCO + wave_m * WM * 32 + l32;
+      const f16x8* sx = smem + 2 * WSLAB + bx * XSLABU + h * SEGUP + ky * Wi;
+      f16x8 A[WM][2], B[WN][2];
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) {
+#pragma unroll
+        for (int wm = 0; wm < WM; ++wm) A[wm][hl] = sw[(kx * 2 + hl) * 2 * BCO + wm * 32];
+#pragma unroll
+        for (int wn = 0; wn < WN; ++wn) B[wn][hl] = sx[hl * 2 * SEGUP + rel[wn] + kx];
+      }
+#pragma unroll
+      for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+        for (int wn = 0; wn < WN; ++wn) {
+          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][0], acc[wm][wn], 0, 0, 0);
+          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][1], acc[wm][wn], 0, 0, 0);
+          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[wn][0], acc[wm][wn], 0, 0, 0);
+        }
+    };
+    // Static priority: the loader waves win the MFMA arbitration on their SIMD, finish
+    // their MFMAs first and convert + store the next union while the DMA waves' MFMAs
+    // still run, so the store phase leaves the step's critical path.
+    if constexpr ((VAR & 32768) != 0) {
+      if (loader) __builtin_amdgcn_s_setprio(1);
+    }
+    // prologue: weights of step 0, the whole union of pair 0
+    if (!loader) issue_c(0, 0);
+#pragma unroll
+    for (int ky = 0; ky < KS; ++ky) {
+      load_c(0, ky);
+      store_c(0, ky, 0);
+    }
+    __syncthreads();
+    for (int c2 = 0; c2 < a.pairs; ++c2) {
+      const bool next = c2 + 1 < a.pairs;
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky) {
+        const int t = c2 * KS + ky;
+        auto stamp = [&](int k) __attribute__((always_inline)) {
+          if constexpr (STAMP) {
+            if (blockIdx.x == 0 && lane == 0) a.dbg[((size_t)wave * T + t) * 4 + k] = __builtin_amdgcn_s_memtime();
+          }
+        };
+        stamp(0);
+        if (!loader && t + 1 < T && (VAR & 65536) == 0) issue_c(t + 1, (t + 1) & 1);
+        stamp(1);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_kx(t & 1, c2 & 1, ky, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (loader && next && (VAR & 131072) == 0) load_c(c2 + 1, ky);   // a third of the next pair's union per step
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kx = 1; kx < KS; ++kx) compute_kx(t & 1, c2 & 1, ky, kx);
+        __builtin_amdgcn_sched_barrier(0);
+        stamp(2);
+        if (loader && next) store_c(c2 + 1, ky, (c2 + 1) & 1);
+        stamp(3);
+        __syncthreads();
+      }
+    }
     }
   } else if constexpr ((VAR & 64) != 0) {
     issue_w(0, 0);
@@ -551,6 +679,15 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   const int Wo = a.W + 2 * a.out_pad;
   float* out_f = a.out + (size_t)n * a.out_fs;
   bool bad = false;
+  float* ebias = (float*)smem;                  // EPI_LDS: [BCO] bias, [BCO] slope
+  if constexpr (EPI_LDS) {
+    // the K loop ended on a barrier: the LDS is free
+    for (int i = tid; i < BCO; i += NT) {
+      ebias[i] = a.bias[co_t * BCO + i];
+      ebias[BCO + i] = a.act == ACT_PRELU ? a.slope[co_t * BCO + i] : 0.f;
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int wn = 0; wn < WN; ++wn) {
     const int m = m0 + (wave_n * WN + wn) * 32 + l32;
@@ -563,7 +700,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int co = cob + 8 * q;
-        const f32x4 b = *(const f32x4*)(a.bias + co);
+        const f32x4 b = EPI_LDS ? *(const f32x4*)(ebias + co - co_t * BCO) : *(const f32x4*)(a.bias + co);
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[wm][wn][4 * q + e] * a.wscale_inv + b[e];
@@ -571,7 +708,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
         } else if (a.act == ACT_PRELU) {
-          const f32x4 sl = *(const f32x4*)(a.slope + co);
+          const f32x4 sl = EPI_LDS ? *(const f32x4*)(ebias + BCO + co - co_t * BCO) : *(const f32x4*)(a.slope + co);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
         }
@@ -664,6 +801,7 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   a.ksplit = (VAR & 2048) ? c.ksplit : 1;
   a.nfr = c.n;
   a.ws = c.ws;
+  a.dbg = c.dbg;
   if ((VAR & 2048) && (!c.ws || c.ksplit < 2)) { set_error("conv_x3: split-K without workspace"); return hipErrorInvalidValue; }
   const long long nb = (long long)c.n * a.px_tiles * a.co_tiles * a.ksplit;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
@@ -712,8 +850,13 @@ static bool x3_big_tiles(const ConvLaunch& c) {
 }
 
 // Row-union staging (VAR 512) when the longest union run of any 512-pixel tile fits.
+static int x3_union_mode() {
+  static const int m = getenv("ISLPOSE_X3_UNION") ? atoi(getenv("ISLPOSE_X3_UNION")) : 1;
+  return m;
+}
+
 static bool x3_union(const ConvLaunch& c) {
-  static const bool off = getenv("ISLPOSE_X3_UNION") && getenv("ISLPOSE_X3_UNION")[0] == '0';
+  const bool off = x3_union_mode() == 0;
   if (off || c.ks != 3) return false;
   const int P = c.ks / 2, Wi = c.W + 2 * c.in_pad, HW = c.H * c.W;
   const int tpx = tile_pixels(c, 512, x3_segmax(512));
@@ -730,6 +873,45 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   const int var = KS <= 3 ? x3_var() : 0;
   if constexpr (KS == 3) {
     if (x3_big_tiles(c) && x3_union(c)) {
+      if (x3_union_mode() == 2) {
+        switch (c.bco) {
+          case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192, 4>(c, s);
+          case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 4096 | 8192, 4>(c, s);
+          case 64: return launch_t<KS, 2, 8, 1, 2, 512 | 4096 | 8192, 4>(c, s);
+          case 32: return launch_t<KS, 1, 16, 1, 1, 512 | 4096 | 8192, 4>(c, s);
+        }
+      }
+      if (x3_union_mode() == 4) {
+        switch (c.bco) {
+          case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 16384 | 32768, 4>(c, s);
+          case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 4096 | 8192 | 16384 | 32768, 4>(c, s);
+        }
+      }
+      if (x3_union_mode() == 6) {   // ablation (timing only): no weight DMA in the loop
+        if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 16384 | 65536, 4>(c, s);
+      }
+      if (x3_union_mode() == 7) {   // ablation (timing only): no input loads in the loop
+        if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 16384 | 131072, 4>(c, s);
+      }
+      if (x3_union_mode() == 8) {   // ablation (timing only): neither
+        if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 16384 | 65536 | 131072, 4>(c, s);
+      }
+      if (x3_union_mode() == 5) {
+        switch (c.bco) {
+          case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 32768, 4>(c, s);
+          case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 4096 | 8192 | 32768, 4>(c, s);
+          case 64: return launch_t<KS, 2, 8, 1, 2, 512 | 4096 | 8192 | 32768, 4>(c, s);
+          case 32: return launch_t<KS, 1, 16, 1, 1, 512 | 4096 | 8192 | 32768, 4>(c, s);
+        }
+      }
+      if (x3_union_mode() == 3) {
+        switch (c.bco) {
+          case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 8192, 4>(c, s);
+          case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 8192, 4>(c, s);
+          case 64: return launch_t<KS, 2, 8, 1, 2, 512 | 8192, 4>(c, s);
+          case 32: return launch_t<KS, 1, 16, 1, 1, 512 | 8192, 4>(c, s);
+        }
+      }
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 512, 4>(c, s);
         case 96: return launch_t<KS, 1, 16, 3, 1, 512, 4>(c, s);

@@ -46,6 +46,7 @@ struct ConvLaunch {
   size_t ws_floats = 0;
   int ksplit = 1;              // set by launch_conv_x3
   int allow_split = 0;         // the net's split-K switch (isl_net_set_split_k)
+  unsigned long long* dbg = nullptr;   // development stamps (tools/convbench), never set by the runtime
 };
 
 // Pixels per tile of the flattened-raster conv kernels: BPX, or fewer when the

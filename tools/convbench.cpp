@@ -68,6 +68,14 @@ int main(int argc, char** argv) {
   L.out = out.base; L.out_pad = pout; L.out_cs = cs_out; L.out_coff = 0;
   L.bias = bias; L.slope = slope; L.n = n; L.H = H; L.W = W; L.ks = ks; L.cin_chunks = chunks; L.cout = cout;
   L.act = ACT_PRELU; L.wx3 = wx; L.wscale_inv = 1.f / 16384.f; L.range_flag = flag;
+  // ISLPOSE_X3_UNION=4: s_memtime stamps of block 0 (16 waves x K steps x 4 points)
+  const int T = pairs * ks;
+  unsigned long long* dbg = nullptr;
+  if (getenv("ISLPOSE_X3_UNION") && atoi(getenv("ISLPOSE_X3_UNION")) == 4) {
+    CK(hipMalloc(&dbg, (size_t)16 * T * 4 * 8));
+    CK(hipMemset(dbg, 0, (size_t)16 * T * 4 * 8));
+    L.dbg = dbg;
+  }
   const double flops = 2.0 * cout * cin * ks * ks * (double)H * W * n;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -101,6 +109,32 @@ int main(int argc, char** argv) {
       printf("  round %d %-7s %9.1f us  fp32-equiv %7.1f TF  alg-MFMA %7.1f TF\n", r, a.c_str(), us,
              flops / us / 1e6, fac * flops / us / 1e6);
     }
+  }
+  if (dbg) {
+    // per step: issue (0->1), compute (1->2), store (2->3), barrier (3 -> next 0), for
+    // the earliest and latest wave, averaged over the steps of the last launch
+    std::vector<unsigned long long> h((size_t)16 * T * 4);
+    CK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    auto at = [&](int w, int t, int k) { return (double)h[((size_t)w * T + t) * 4 + k]; };
+    double ph[4] = {0, 0, 0, 0}, step = 0;
+    int nst = 0;
+    for (int t = 1; t + 1 < T; ++t, ++nst) {
+      double mn0 = 1e300, mx3 = 0;
+      for (int w = 0; w < 16; ++w) {
+        ph[0] += (at(w, t, 1) - at(w, t, 0)) / 16;
+        ph[1] += (at(w, t, 2) - at(w, t, 1)) / 16;
+        ph[2] += (at(w, t, 3) - at(w, t, 2)) / 16;
+        ph[3] += (at(w, t + 1, 0) - at(w, t, 3)) / 16;
+        mn0 = std::min(mn0, at(w, t, 0));
+        mx3 = std::max(mx3, at(w, t, 3));
+      }
+      step += at(0, t + 1, 0) - at(0, t, 0);
+    }
+    printf("  stamps (cycles per step, mean over waves and %d steps): issue %.0f compute %.0f store %.0f barrier %.0f; "
+           "step %.0f\n", nst, ph[0] / nst, ph[1] / nst, ph[2] / nst, ph[3] / nst, step / nst);
+    for (int w = 0; w < 16; ++w)
+      printf("    wave %2d step 5: compute %.0f store %.0f wait %.0f\n", w, at(w, 5, 2) - at(w, 5, 1),
+             at(w, 5, 3) - at(w, 5, 2), at(w, 6, 0) - at(w, 5, 3));
   }
   return 0;
 }

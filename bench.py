@@ -72,7 +72,8 @@ def parse(argv=None):
     p.add_argument("--e2e-steps", type=int, default=3,
                    help="batches timed through the caller path (host frames in, Python results out); 0 = skip")
     p.add_argument("--split-k", action="store_true",
-                   help="split-K on small conv grids (isl_net_set_split_k): batch-1 latency mode")
+                   help="latency mode of the conv K ranges (isl_net_set_split_k mode 2: also an adaptive, "
+                        "batch-dependent split of small grids); the default is mode 1 (canonical ranges)")
     p.add_argument("--dry-run", action="store_true",
                    help="no GPU: run the rank launch, shard and max-over-ranks timing structure only")
     return p.parse_args(argv)
@@ -185,7 +186,7 @@ def gpu_main(args, rank, local, world):
             self.net = self.est.net
             self.net.set_algo(args.algo)
             if args.split_k:
-                self.net.set_split_k(True)
+                self.net.set_split_k(2)
             self.b = B // S
             sl = slice(s * self.b, (s + 1) * self.b)
             self.frames, self.paf, self.heat = frames[sl], d_paf[sl], d_heat[sl]

@@ -127,12 +127,20 @@ int isl_net_arena_info(const isl_net* net, int64_t* bytes, int* n_arenas);
 int isl_net_set_algo(isl_net* net, int algo);
 int isl_net_get_algo(const isl_net* net);
 
-/* Split-K for ISL_ALGO_X3 layers whose grid cannot fill the GPU (batch-1 frames,
- * single hand crops): the K range is spread over up to 8 blocks per tile and
- * reduced in a fixed order (deterministic).  Off by default (env
- * ISLPOSE_X3_SPLITK=1 turns it on at create time): with it, a frame's maps differ
- * in the last bits between batch sizes (always within the fp32 tolerance). */
-int isl_net_set_split_k(isl_net* net, int on);
+/* K ranges of the ISL_ALGO_X3 convolutions (latency of small grids such as batch-1
+ * frames; not in the reference, whose torch conv runs per frame):
+ *   mode 1 (default)  canonical ranges: layers of <= 1024 pixels per frame (Mode R's
+ *                     23x41 body stages, the 184 px hand scale) sum their input
+ *                     channels in up to 8 ranges fixed by the layer shape; a small grid
+ *                     spreads the ranges over blocks (split-K, fixed-order reduction),
+ *                     a large one keeps them in one block -- the same bits either way,
+ *                     so a frame's maps do not depend on the batch it came in;
+ *   mode 0            no ranges;
+ *   mode 2            latency: mode 1, plus an adaptive split of every other layer
+ *                     whose grid cannot half-fill the GPU (those layers' bits then
+ *                     depend on the batch size, within the fp32 tolerance).
+ * Env ISLPOSE_X3_SPLITK=0|1|2 sets the mode at create time. */
+int isl_net_set_split_k(isl_net* net, int mode);
 
 /* Range guard of ISL_ALGO_X3: waits for the device, returns ISL_E_RANGE if any
  * conv output since the last clear left the fp16 split range (the results of

@@ -37,6 +37,19 @@
 //            fp16 hi / lo in registers and written as [hi|lo][h][px] x 16 B.
 // Double-buffered, one barrier per step; per step and wave KS taps x WM*WN
 // accumulator tiles x 3 MFMAs.
+//
+// Variants (template VAR bits):
+//   512   row union (3x3 on 512-pixel tiles): the three kernel rows of a chunk pair
+//         are staged once as one run, a third per ky step, by loader waves, while
+//         DMA waves stream the weights (role split, see the union loop);
+//   1024  canonical K ranges (in-block): the chunk pairs are summed in S ranges,
+//         each from zero, and the range sums added in order -- the same bits as
+//   2048  split-K across blocks: each block writes one range's sum, x3_splitk_reduce
+//         adds them in range order.  S depends on the layer shape only
+//         (x3_canonical_ranges), so a frame gives the same bits at any batch size
+//         whether its ranges ran in one block (large grids) or across blocks (small
+//         grids: batch-1 frames).
+//   16384 development only: s_memtime stamps of the union loop (tools/convbench).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -62,7 +75,7 @@ struct X3Args {
   float wscale_inv;             // 2^-s
   int in_pad, out_pad;
   int H, W, cin_chunks, pairs, cout, co_tiles, px_tiles, tpx, act, nblocks;
-  int ksplit;                   // split-K (VAR 2048): blocks per tile, each over a range of chunk pairs
+  int ksplit;                   // K ranges (VAR 1024 / 2048)
   int nfr;                      // frames (split-K partial-sum layout)
   float* ws;                    // split-K partial sums [ksplit][nfr][cout/8][H*W][8]
   unsigned long long* dbg;      // VAR 16384 (development): s_memtime stamps of block 0
@@ -89,35 +102,15 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr int IT = (2 * SEGMAX + NT - 1) / NT; // staging items (h, px) per thread
   static_assert(WSLAB % 64 == 0, "weight slab is whole 1 KiB DMA pieces");
   static_assert(BPX <= SEGMAX, "segment must hold a tile");
-  constexpr int NBUF = (VAR & 256) ? 3 : 2;        // VAR 256: 3-stage LDS-DMA ring
-  // VAR 512 ("row union"): the KS input rows of a chunk pair are staged once, as one
-  // run covering rows -P..+P of the tile, a third per ky step; ky then only offsets
-  // the B reads by ky*Wi.  For tiles spanning several image rows (46x82, 92x164)
-  // this stages 2-2.5x fewer input bytes than one run per (pair, ky).
   constexpr bool UNION = (VAR & 512) != 0;
   constexpr int SEGUP = x3_segu_max() + 1;       // + dummy slot
   constexpr int XSLABU = 2 * 2 * SEGUP;          // [hi|lo][h][px]
-  constexpr int SMEM = UNION ? 2 * (WSLAB + XSLABU) : NBUF * BUF;
+  constexpr int SMEM = UNION ? 2 * (WSLAB + XSLABU) : 2 * BUF;
   static_assert(SMEM * 16 <= 160 * 1024, "LDS");
-  static_assert(!UNION || (2 * x3_segu_max() + KS - 1) / KS <= NT, "one union item per thread and step");
-  constexpr bool WEAVE = (VAR & 2) != 0;         // interleave the stores with the MFMAs
-  // VAR 2048 (split-K, small grids such as batch-1 frames): the block computes the
-  // partial sum of a contiguous range of chunk pairs into a.ws; x3_splitk_reduce
-  // adds the ranges in a fixed order and applies the epilogue
+  constexpr bool RANGED = (VAR & 1024) != 0;
   constexpr bool SPLIT = (VAR & 2048) != 0;
-  // VAR 4096 (with 512): branch-free union loop -- every load and DMA issued
-  // unconditionally (clamped addresses, zeroes selected at use, idle items write a
-  // dummy slot) so the compiler's counted waits leave the weight DMA of step t+1 in
-  // flight: no vmcnt(0) between the DMA issue and the K step's MFMAs
-  constexpr bool UCLEAN = (VAR & 4096) != 0;
-  // VAR 8192: bias / PReLU slopes staged in LDS before the epilogue, so the output
-  // stores stream without a global load (and its vmcnt(0)) between them
-  constexpr bool EPI_LDS = (VAR & 8192) != 0;
-  // VAR 16384 (development build of the branch-free union loop): lane 0 of every wave
-  // of block 0 stamps s_memtime at 4 points of each K step into a.dbg
   constexpr bool STAMP = (VAR & 16384) != 0;
-  constexpr bool NO_STAGE = (VAR & 8) != 0;      // ablation: skip global loads + LDS stores
-  constexpr bool NO_MATH = (VAR & 16) != 0;      // ablation: skip LDS reads + MFMAs
+  static_assert(!(UNION && (RANGED || SPLIT)), "K ranges run on the generic loop");
   __shared__ f16x8 smem[SMEM];
 
   // XCD-aware tile order (conv.hip): co-tiles of a pixel tile, then neighbouring
@@ -151,6 +144,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wave_m = wave % WAVES_M, wave_n = wave / WAVES_M;
   const int h = lane >> 5, l32 = lane & 31;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
 
   int rel[WN];
 #pragma unroll
@@ -161,63 +155,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     rel[wn] = (y + a.in_pad) * Wi + x + a.in_pad - La;
   }
 
-  // staging items of this thread: item = tid + i*NT -> (chunk half ih, pixel ipx)
-  int ih[IT], ipx[IT];
-#pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int it = tid + i * NT;
-    ih[i] = it >= seg ? 1 : 0;
-    ipx[i] = it - ih[i] * seg;
-    if (it >= 2 * seg) ipx[i] = -1;   // idle
-  }
-
   const int T = a.pairs * KS;
-  f32x4 raw[IT][2];
-
-  auto load_x = [&](int t) __attribute__((always_inline)) {
-    const int c2 = t / KS, ky = t - c2 * KS;
-    const long long row = (long long)(La + (ky - P) * Wi - P);
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      const int c = 2 * c2 + ih[i];
-      if (ipx[i] >= 0 && c < a.cin_chunks) {
-        const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + ipx[i]) * 8;
-        raw[i][0] = *(const f32x4*)src;
-        raw[i][1] = *(const f32x4*)(src + 4);
-      } else {
-        raw[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-        raw[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  };
-  auto store_x = [&](int buf) __attribute__((always_inline)) {
-    f16x8* s = smem + buf * BUF + WSLAB;
-#pragma unroll
-    for (int i = 0; i < IT; ++i) {
-      if (ipx[i] < 0) continue;
-      f16x8 hi, lo;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = raw[i][j >> 2][j & 3];
-        hi[j] = (_Float16)x;
-        lo[j] = (_Float16)(x - (float)hi[j]);
-      }
-      s[(0 * 2 + ih[i]) * SEGP + ipx[i]] = hi;
-      s[(1 * 2 + ih[i]) * SEGP + ipx[i]] = lo;
-    }
-  };
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  auto issue_w = [&](int t, int buf) __attribute__((always_inline)) {
-    const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
-    f16x8* dst = smem + buf * BUF;
-#pragma unroll
-    for (int q0 = 0; q0 < WSLAB / 64; q0 += NWAVES) {
-      const int q = q0 + wave_u;
-      if ((WSLAB / 64) % NWAVES == 0 || q < WSLAB / 64)
-        __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
-                                         (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
-    }
-  };
 
   f32x16 acc[WM][WN];
 #pragma unroll
@@ -227,195 +165,48 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[wm][wn][r] = 0.f;
 
-  auto compute = [&](int buf) __attribute__((always_inline)) {
-    if constexpr (NO_MATH) return;
-    // (T5, s_setprio(1) around this MFMA cluster, measured +0-2 %: not used)
-    const f16x8* sw = smem + buf * BUF + h * BCO + wave_m * WM * 32 + l32;
-    const f16x8* sx = smem + buf * BUF + WSLAB + h * SEGP;
+  // one tap (kx) of a K step: WM x WN accumulator tiles x 3 MFMAs from the weight
+  // slab sw and the input run sx (both already offset to this lane's fragments)
+  auto tap = [&](const f16x8* sw, const f16x8* sx, int sx_plane, int kx) __attribute__((always_inline)) {
+    f16x8 A[WM][2], B[WN][2];
 #pragma unroll
-    for (int kx = 0; kx < KS; ++kx) {
-      f16x8 A[WM][2], B[WN][2];
+    for (int hl = 0; hl < 2; ++hl) {
 #pragma unroll
-      for (int hl = 0; hl < 2; ++hl) {
+      for (int wm = 0; wm < WM; ++wm) A[wm][hl] = sw[(kx * 2 + hl) * 2 * BCO + wm * 32];
 #pragma unroll
-        for (int wm = 0; wm < WM; ++wm) A[wm][hl] = sw[(kx * 2 + hl) * 2 * BCO + wm * 32];
-#pragma unroll
-        for (int wn = 0; wn < WN; ++wn) B[wn][hl] = sx[hl * 2 * SEGP + rel[wn] + kx];
-      }
-#pragma unroll
-      for (int wm = 0; wm < WM; ++wm)
-#pragma unroll
-        for (int wn = 0; wn < WN; ++wn) {
-          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][0], acc[wm][wn], 0, 0, 0);
-          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][1], acc[wm][wn], 0, 0, 0);
-          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[wn][0], acc[wm][wn], 0, 0, 0);
-        }
+      for (int wn = 0; wn < WN; ++wn) B[wn][hl] = sx[hl * 2 * sx_plane + rel[wn] + kx];
     }
+#pragma unroll
+    for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+      for (int wn = 0; wn < WN; ++wn) {
+        acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][0], acc[wm][wn], 0, 0, 0);
+        acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][1], acc[wm][wn], 0, 0, 0);
+        acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[wn][0], acc[wm][wn], 0, 0, 0);
+      }
   };
 
-  // ablation (VAR & 64): input rows by LDS-DMA too, raw fp32 halves as if they
-  // were pre-split fp16 planes (wrong numbers, right traffic): what a split
-  // activation storage would buy
-  auto issue_x = [&](int t, int buf) __attribute__((always_inline)) {
-    const int c2 = t / KS, ky = t - c2 * KS;
-    const long long row = (long long)(La + (ky - P) * Wi - P);
-    f16x8* dst = smem + buf * BUF + WSLAB;
-    const int nch = (seg + 63) >> 6;
-    for (int q = wave_u; q < 4 * nch; q += NWAVES) {
-      const int run = q / nch, ch = q - run * nch;          // run = hl*2 + h
-      const int hl = run >> 1, hh = run & 1;
-      const int c = min(2 * c2 + hh, a.cin_chunks - 1);
-      const int px = min(ch * 64 + lane, seg - 1);
-      const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + px) * 8 + 4 * hl;
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(dst + run * SEGP + ch * 64), 16, 0, 0);
-    }
-  };
-  // ablation (VAR & 256): both operands by LDS-DMA (input as fake-split raw fp32)
-  // through a 3-buffer ring whose loads stay in flight ACROSS the barrier: every
-  // wave issues exactly DW + DX DMA pieces per step (count padded with harmless
-  // duplicate pieces), so a counted s_waitcnt vmcnt(DW + DX) retires step t while
-  // step t+1's pieces keep flying; raw s_barrier (no vmcnt(0) drain).
-  if constexpr ((VAR & 256) != 0) {
-    constexpr int DW = (WSLAB / 64 + NWAVES - 1) / NWAVES;
-    constexpr int NCH = (SEGMAX + 63) / 64;
-    constexpr int DX = (4 * NCH + NWAVES - 1) / NWAVES;
-    auto ring_issue = [&](int t, int buf) __attribute__((always_inline)) {
-      t = min(t, T - 1);      // past the end: duplicate of the last step (never read)
-      const f16x8* wsrc = a.wpk + ((size_t)co_t * T + t) * WSLAB;
-      f16x8* dst = smem + buf * BUF;
-#pragma unroll
-      for (int k = 0; k < DW; ++k) {
-        const int q = min(wave_u + k * NWAVES, WSLAB / 64 - 1);
-        __builtin_amdgcn_global_load_lds((const void*)(wsrc + q * 64 + lane),
-                                         (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
-      }
-      const int c2 = t / KS, ky = t - c2 * KS;
-      const long long row = (long long)(La + (ky - P) * Wi - P);
-      f16x8* xd = dst + WSLAB;
-#pragma unroll
-      for (int k = 0; k < DX; ++k) {
-        const int q = min(wave_u + k * NWAVES, 4 * NCH - 1);
-        const int run = q / NCH, ch = q - run * NCH;
-        const int hl = run >> 1, hh = run & 1;
-        const int c = min(2 * c2 + hh, a.cin_chunks - 1);
-        const int px = min(ch * 64 + lane, seg - 1);
-        const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + px) * 8 + 4 * hl;
-        __builtin_amdgcn_global_load_lds((const void*)src,
-                                         (__attribute__((address_space(3))) void*)(xd + run * SEGP + ch * 64), 16,
-                                         0, 0);
-      }
-    };
-    ring_issue(0, 0);
-    ring_issue(1, 1);
-    for (int t = 0; t < T; ++t) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DW + DX) : "memory");   // my pieces of step t landed
-      __builtin_amdgcn_s_barrier();                                     // everyone's; compute(t-1) done
-      ring_issue(t + 2, (t + 2) % 3);
-      compute(t % 3);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  } else if constexpr (UNION) {
-    const int Pw = P * Wi;
-    const int segu = Lb - La + 2 * Pw + 2 * P + 1;        // rows -P..+P of the tile, one run
-    const long long ubase = (long long)La - Pw - P;
-    const int third = (2 * segu + KS - 1) / KS;           // staging items per ky step
-    f32x4 ru[2];
-    int u_ih = 0, u_px = -1;
-    auto load_u = [&](int c2, int ky) __attribute__((always_inline)) {
-      const int it = ky * third + tid;
-      u_px = -1;
-      if (tid < third && it < 2 * segu) {
-        u_ih = it >= segu ? 1 : 0;
-        u_px = it - u_ih * segu;
-      }
-      const int c = 2 * c2 + u_ih;
-      if (u_px >= 0 && c < a.cin_chunks) {
-        const float* src = in_f + (size_t)c * a.in_chs + (size_t)(ubase + u_px) * 8;
-        ru[0] = *(const f32x4*)src;
-        ru[1] = *(const f32x4*)(src + 4);
-      } else {
-        ru[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-        ru[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    };
-    auto store_u = [&](int bx) __attribute__((always_inline)) {
-      if (u_px < 0) return;
-      f16x8* sx = smem + 2 * WSLAB + bx * XSLABU;
-      f16x8 hi, lo;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = ru[j >> 2][j & 3];
-        hi[j] = (_Float16)x;
-        lo[j] = (_Float16)(x - (float)hi[j]);
-      }
-      sx[(0 * 2 + u_ih) * SEGUP + u_px] = hi;
-      sx[(1 * 2 + u_ih) * SEGUP + u_px] = lo;
-    };
-    auto issue_wu = [&](int t, int bw) __attribute__((always_inline)) {
-      const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
-      f16x8* dst = smem + bw * WSLAB;
-#pragma unroll
-      for (int q0 = 0; q0 < WSLAB / 64; q0 += NWAVES) {
-        const int q = q0 + wave_u;
-        if ((WSLAB / 64) % NWAVES == 0 || q < WSLAB / 64)
-          __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
-                                           (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
-      }
-    };
-    auto compute_u = [&](int bw, int bx, int ky) __attribute__((always_inline)) {
-      const f16x8* sw = smem + bw * WSLAB + h * BCO + wave_m * WM * 32 + l32;
-      const f16x8* sx = smem + 2 * WSLAB + bx * XSLABU + h * SEGUP + ky * Wi;
-#pragma unroll
-      for (int kx = 0; kx < KS; ++kx) {
-        f16x8 A[WM][2], B[WN][2];
-#pragma unroll
-        for (int hl = 0; hl < 2; ++hl) {
-#pragma unroll
-          for (int wm = 0; wm < WM; ++wm) A[wm][hl] = sw[(kx * 2 + hl) * 2 * BCO + wm * 32];
-#pragma unroll
-          for (int wn = 0; wn < WN; ++wn) B[wn][hl] = sx[hl * 2 * SEGUP + rel[wn] + kx];
-        }
-#pragma unroll
-        for (int wm = 0; wm < WM; ++wm)
-#pragma unroll
-          for (int wn = 0; wn < WN; ++wn) {
-            acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][0], acc[wm][wn], 0, 0, 0);
-            acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][1], acc[wm][wn], 0, 0, 0);
-            acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[wn][0], acc[wm][wn], 0, 0, 0);
-          }
-      }
-    };
-    if constexpr (!UCLEAN) {
-    // prologue: weights of step 0, the whole union of pair 0
-    issue_wu(0, 0);
-    for (int ky = 0; ky < KS; ++ky) {
-      load_u(0, ky);
-      store_u(0);
-    }
-    __syncthreads();
-    for (int t = 0; t < T; ++t) {
-      const int c2 = t / KS, ky = t - c2 * KS;
-      const bool next = c2 + 1 < a.pairs;
-      if (t + 1 < T) issue_wu(t + 1, (t + 1) & 1);
-      if (next) load_u(c2 + 1, ky);      // a third of the next pair's union per step
-      compute_u(t & 1, c2 & 1, ky);
-      if (next) store_u((c2 + 1) & 1);
-      __syncthreads();
-    }
-    } else {
-    // Role-split form.  Issuing every wave's global loads and DMA pieces at the top of
-    // a K step stalls all 16 waves on the CU's vector-memory issue (~1.6k cycles per
-    // step, s_memtime stamps) before any of them reaches its MFMAs.  Here waves 0-9
-    // (the threads < third) stage the input union, waves 10-15 stream the weight
-    // slab, and both issue between MFMA groups: the DMA of step t+1 before the kx = 0
-    // group, the input loads of the next pair after it.
+  if constexpr (UNION) {
+    // Row union, role split.  The KS input rows of a chunk pair are staged once, as
+    // one run covering rows -P..+P of the tile, a third per ky step (ky then only
+    // offsets the B reads by ky*Wi); for tiles spanning several image rows (46x82,
+    // 92x164) that stages 2-2.5x fewer input bytes than one run per (pair, ky).
+    // Issuing every wave's loads and DMA pieces at the top of a step stalled all 16
+    // waves on the CU's vector-memory issue (~1.6k cycles per step, s_memtime
+    // stamps) before any reached its MFMAs; here waves 0-9 (the threads < third)
+    // stage the input union, waves 10-15 stream the weight slab, and both issue
+    // between MFMA groups: the DMA of step t+1 ahead of the kx = 0 group, the input
+    // loads of the next pair after it (+2-4 % per layer over issuing both at the top).
     static_assert(NWAVES == 16, "role split sized for 16-wave blocks");
     constexpr int LOADER_WAVES = 10, DMA_WAVES = NWAVES - LOADER_WAVES;
     constexpr int NP = WSLAB / 64;                               // 1 KiB DMA pieces per step
     constexpr int DPW = (NP + DMA_WAVES - 1) / DMA_WAVES;
     const bool loader = wave_u < LOADER_WAVES;
+    const int Pw = P * Wi;
+    const int segu = Lb - La + 2 * Pw + 2 * P + 1;        // rows -P..+P of the tile, one run
+    const long long ubase = (long long)La - Pw - P;
+    const int third = (2 * segu + KS - 1) / KS;           // staging items per ky step (<= 640)
+    f32x4 ru[2];
     int c_ih[KS], c_px[KS];
 #pragma unroll
     for (int ky = 0; ky < KS; ++ky) {
@@ -434,7 +225,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     };
     auto store_c = [&](int c2, int ky, int bx) __attribute__((always_inline)) {
       f16x8* sx = smem + 2 * WSLAB + bx * XSLABU;
-      const bool zero = 2 * c2 + c_ih[ky] >= a.cin_chunks;
+      const bool zero = 2 * c2 + c_ih[ky] >= a.cin_chunks;   // missing odd chunk: zeroed here, at the use
       f16x8 hi, lo;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -457,32 +248,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
                                            (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
       }
     };
-    auto compute_kx = [&](int bw, int bx, int ky, int kx) __attribute__((always_inline)) {
-      const f16x8* sw = smem + bw * WSLAB + h * BCO + wave_m * WM * 32 + l32;
-      const f16x8* sx = smem + 2 * WSLAB + bx * XSLABU + h * SEGUP + ky * Wi;
-      f16x8 A[WM][2], B[WN][2];
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl) {
-#pragma unroll
-        for (int wm = 0; wm < WM; ++wm) A[wm][hl] = sw[(kx * 2 + hl) * 2 * BCO + wm * 32];
-#pragma unroll
-        for (int wn = 0; wn < WN; ++wn) B[wn][hl] = sx[hl * 2 * SEGUP + rel[wn] + kx];
-      }
-#pragma unroll
-      for (int wm = 0; wm < WM; ++wm)
-#pragma unroll
-        for (int wn = 0; wn < WN; ++wn) {
-          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][0], acc[wm][wn], 0, 0, 0);
-          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][1], acc[wm][wn], 0, 0, 0);
-          acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[wn][0], acc[wm][wn], 0, 0, 0);
-        }
+    auto tap_u = [&](int bw, int bx, int ky, int kx) __attribute__((always_inline)) {
+      tap(smem + bw * WSLAB + h * BCO + wave_m * WM * 32 + l32,
+          smem + 2 * WSLAB + bx * XSLABU + h * SEGUP + ky * Wi, SEGUP, kx);
     };
-    // Static priority: the loader waves win the MFMA arbitration on their SIMD, finish
-    // their MFMAs first and convert + store the next union while the DMA waves' MFMAs
-    // still run, so the store phase leaves the step's critical path.
-    if constexpr ((VAR & 32768) != 0) {
-      if (loader) __builtin_amdgcn_s_setprio(1);
-    }
     // prologue: weights of step 0, the whole union of pair 0
     if (!loader) issue_c(0, 0);
 #pragma unroll
@@ -502,15 +271,15 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
           }
         };
         stamp(0);
-        if (!loader && t + 1 < T && (VAR & 65536) == 0) issue_c(t + 1, (t + 1) & 1);
+        if (!loader && t + 1 < T) issue_c(t + 1, (t + 1) & 1);
         stamp(1);
         __builtin_amdgcn_sched_barrier(0);
-        compute_kx(t & 1, c2 & 1, ky, 0);
+        tap_u(t & 1, c2 & 1, ky, 0);
         __builtin_amdgcn_sched_barrier(0);
-        if (loader && next && (VAR & 131072) == 0) load_c(c2 + 1, ky);   // a third of the next pair's union per step
+        if (loader && next) load_c(c2 + 1, ky);   // a third of the next pair's union per step
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int kx = 1; kx < KS; ++kx) compute_kx(t & 1, c2 & 1, ky, kx);
+        for (int kx = 1; kx < KS; ++kx) tap_u(t & 1, c2 & 1, ky, kx);
         __builtin_amdgcn_sched_barrier(0);
         stamp(2);
         if (loader && next) store_c(c2 + 1, ky, (c2 + 1) & 1);
@@ -518,28 +287,78 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
         __syncthreads();
       }
     }
+  } else {
+    // Generic loop: one step = (pair, ky); weights by LDS-DMA one step ahead, the
+    // input row run register-staged one step ahead.
+    int ih[IT], ipx[IT];                 // staging items: tid + i*NT -> (chunk half, pixel)
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int it = tid + i * NT;
+      ih[i] = it >= seg ? 1 : 0;
+      ipx[i] = it - ih[i] * seg;
+      if (it >= 2 * seg) ipx[i] = -1;   // idle
     }
-  } else if constexpr ((VAR & 64) != 0) {
-    issue_w(0, 0);
-    issue_x(0, 0);
-    __syncthreads();
-    for (int t = 0; t < T; ++t) {
-      const int buf = t & 1;
-      if (t + 1 < T) {
-        issue_w(t + 1, buf ^ 1);
-        issue_x(t + 1, buf ^ 1);
+    f32x4 raw[IT][2];
+    auto load_x = [&](int t) __attribute__((always_inline)) {
+      const int c2 = t / KS, ky = t - c2 * KS;
+      const long long row = (long long)(La + (ky - P) * Wi - P);
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        const int c = 2 * c2 + ih[i];
+        if (ipx[i] >= 0 && c < a.cin_chunks) {
+          const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + ipx[i]) * 8;
+          raw[i][0] = *(const f32x4*)src;
+          raw[i][1] = *(const f32x4*)(src + 4);
+        } else {
+          raw[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+          raw[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
       }
-      compute(buf);
-      __syncthreads();
-    }
-  } else if constexpr ((VAR & 1) == 0) {
-    // weights by LDS-DMA one step ahead, input rows register-staged one step ahead
-    int t0 = 0, t1 = T;
-    if constexpr (SPLIT) {
+    };
+    auto store_x = [&](int buf) __attribute__((always_inline)) {
+      f16x8* s = smem + buf * BUF + WSLAB;
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        if (ipx[i] < 0) continue;
+        f16x8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = raw[i][j >> 2][j & 3];
+          hi[j] = (_Float16)x;
+          lo[j] = (_Float16)(x - (float)hi[j]);
+        }
+        s[(0 * 2 + ih[i]) * SEGP + ipx[i]] = hi;
+        s[(1 * 2 + ih[i]) * SEGP + ipx[i]] = lo;
+      }
+    };
+    auto issue_w = [&](int t, int buf) __attribute__((always_inline)) {
+      const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
+      f16x8* dst = smem + buf * BUF;
+#pragma unroll
+      for (int q0 = 0; q0 < WSLAB / 64; q0 += NWAVES) {
+        const int q = q0 + wave_u;
+        if ((WSLAB / 64) % NWAVES == 0 || q < WSLAB / 64)
+          __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
+                                           (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
+      }
+    };
+    auto compute = [&](int buf) __attribute__((always_inline)) {
+      const f16x8* sw = smem + buf * BUF + h * BCO + wave_m * WM * 32 + l32;
+      const f16x8* sx = smem + buf * BUF + WSLAB + h * SEGP;
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) tap(sw, sx, SEGP, kx);
+    };
+    // K ranges: [t0, t1) of this block (SPLIT: one range), range length R steps
+    int t0 = 0, t1 = T, R = T;
+    if constexpr (SPLIT || RANGED) {
       const int pps = (a.pairs + a.ksplit - 1) / a.ksplit;
-      t0 = ks_i * pps * KS;
-      t1 = min(a.pairs, (ks_i + 1) * pps) * KS;
+      R = pps * KS;
+      if constexpr (SPLIT) {
+        t0 = ks_i * R;
+        t1 = min(a.pairs, (ks_i + 1) * pps) * KS;
+      }
     }
+    f32x16 tot[RANGED ? WM : 1][RANGED ? WN : 1];
     issue_w(t0, 0);
     load_x(t0);
     store_x(0);
@@ -551,108 +370,35 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
         load_x(t + 1);
       }
       compute(buf);
+      if constexpr (RANGED) {
+        // end of a range: its sum (from zero) joins the total, ranges in order
+        if (t + 1 == t1 || (t + 1) % R == 0) {
+#pragma unroll
+          for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+            for (int wn = 0; wn < WN; ++wn) {
+              if (t + 1 == R) tot[wm][wn] = acc[wm][wn];
+              else tot[wm][wn] += acc[wm][wn];
+#pragma unroll
+              for (int r = 0; r < 16; ++r) acc[wm][wn][r] = 0.f;
+            }
+        }
+      }
       if (t + 1 < t1) store_x(buf ^ 1);
       __syncthreads();
     }
-  } else {
-    // everything register-staged, loads issued two steps ahead (two register
-    // sets; the loop is unrolled by two so set indices are compile-time): a
-    // step's loads have a whole step of MFMAs more to land than with VAR 0.
-    constexpr int WIT = (WSLAB + NT - 1) / NT;
-    f16x8 rw[2][WIT];
-    f32x4 rx[2][IT][2];
-    auto load = [&](auto S_, int t) __attribute__((always_inline)) {
-      constexpr int S = decltype(S_)::value;
-      if constexpr (NO_STAGE) return;
-      t = min(t, T - 1);   // past the end: harmless reload, never stored
-      const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
+    if constexpr (RANGED) {
 #pragma unroll
-      for (int i = 0; i < WIT; ++i) {
-        const int idx = tid + i * NT;
-        if (WSLAB % NT == 0 || idx < WSLAB) rw[S][i] = src[idx];
-      }
-      const int c2 = t / KS, ky = t - c2 * KS;
-      const long long row = (long long)(La + (ky - P) * Wi - P);
+      for (int wm = 0; wm < WM; ++wm)
 #pragma unroll
-      for (int i = 0; i < IT; ++i) {
-        const int c = min(2 * c2 + ih[i], a.cin_chunks - 1);
-        const int px = max(ipx[i], 0);
-        const float* xs = in_f + (size_t)c * a.in_chs + (size_t)(row + px) * 8;
-        rx[S][i][0] = *(const f32x4*)xs;
-        rx[S][i][1] = *(const f32x4*)(xs + 4);
-      }
-    };
-    // (the zeroing of a missing odd chunk happens here, at the use: a select right
-    // after the load would make the compiler wait for it a whole step early)
-    auto store = [&](auto S_, int buf, int t) __attribute__((always_inline)) {
-      constexpr int S = decltype(S_)::value;
-      if constexpr (NO_STAGE) return;
-      const int c2 = t / KS;
-      f16x8* sw = smem + buf * BUF;
-#pragma unroll
-      for (int i = 0; i < WIT; ++i) {
-        const int idx = tid + i * NT;
-        if (WSLAB % NT == 0 || idx < WSLAB) sw[idx] = rw[S][i];
-      }
-      f16x8* sx = smem + buf * BUF + WSLAB;
-#pragma unroll
-      for (int i = 0; i < IT; ++i) {
-        // no branch around idle items (they write the dummy slot): a store under an
-        // exec branch makes the compiler's waitcnt bookkeeping fall back to vmcnt(0)
-        const int px = ipx[i] < 0 ? SEGMAX : ipx[i];
-        f16x8 hi, lo;
-        const bool zero = 2 * c2 + ih[i] >= a.cin_chunks;
-        if constexpr ((VAR & 32) != 0) {   // ablation: no conversion (raw bits as fragments)
-          hi = __builtin_bit_cast(f16x8, rx[S][i][0]);
-          lo = __builtin_bit_cast(f16x8, rx[S][i][1]);
-        } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = zero ? 0.f : rx[S][i][j >> 2][j & 3];
-          hi[j] = (_Float16)x;
-          lo[j] = (_Float16)(x - (float)hi[j]);
-        }
-        }
-        sx[(0 * 2 + ih[i]) * SEGP + px] = hi;
-        sx[(1 * 2 + ih[i]) * SEGP + px] = lo;
-      }
-    };
-    using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
-    load(S0{}, 0);
-    load(S1{}, 1);
-    store(S0{}, 0, 0);
-    __syncthreads();
-    // the loop body is branch-free (a store skipped on some path would make the
-    // compiler's waitcnt bookkeeping fall back to vmcnt(0) at the next reuse)
-    int t = 0;
-    // sched_barrier pins the phase order: loads issued first, the previous set's
-    // stores after this step's MFMAs (hoisting them would wait on young loads)
-    for (; t + 2 < T; t += 2) {
-      load(S0{}, t + 2);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(0);
-      if constexpr (!WEAVE) __builtin_amdgcn_sched_barrier(0);
-      store(S1{}, 1, t + 1);
-      __syncthreads();
-      load(S1{}, t + 3);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(1);
-      if constexpr (!WEAVE) __builtin_amdgcn_sched_barrier(0);
-      store(S0{}, 0, t + 2);
-      __syncthreads();
-    }
-    compute(0);                 // step t; step t+1 if T - t == 2
-    if (t + 1 < T) {
-      store(S1{}, 1, t + 1);
-      __syncthreads();
-      compute(1);
+        for (int wn = 0; wn < WN; ++wn) acc[wm][wn] = tot[wm][wn];
     }
   }
 
   if constexpr (SPLIT) {
-    // partial sums x 2^-s (exact) into this range's slice of the workspace; the
-    // workspace carries round8(cout) channels, so the 4-channel groups never overrun
+    // this range's sum (unscaled, as the in-block ranges keep it) into its slice of
+    // the workspace; the workspace carries round8(cout) channels, so the 4-channel
+    // groups never overrun
     const size_t plane = (size_t)HW * 8;
     float* wsb = a.ws + ((size_t)ks_i * a.nfr + n) * (size_t)((a.cout + 7) / 8) * plane;
 #pragma unroll
@@ -668,26 +414,25 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
           if (co >= a.cout) continue;
           f32x4 v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[wm][wn][4 * q + e] * a.wscale_inv;
+          for (int e = 0; e < 4; ++e) v[e] = acc[wm][wn][4 * q + e];
           *(f32x4*)(wsb + (size_t)(co >> 3) * plane + (size_t)m * 8 + (co & 7)) = v;
         }
       }
     }
     return;
   }
-  // epilogue: x 2^-s, bias + activation, range check, masked float4 stores
+  // epilogue: x 2^-s, bias + activation, range check, masked float4 stores.  Bias and
+  // PReLU slopes come from LDS (staged once), so no global load -- and no vmcnt(0)
+  // behind the stores issued so far -- sits between the output stores.
   const int Wo = a.W + 2 * a.out_pad;
   float* out_f = a.out + (size_t)n * a.out_fs;
   bool bad = false;
-  float* ebias = (float*)smem;                  // EPI_LDS: [BCO] bias, [BCO] slope
-  if constexpr (EPI_LDS) {
-    // the K loop ended on a barrier: the LDS is free
-    for (int i = tid; i < BCO; i += NT) {
-      ebias[i] = a.bias[co_t * BCO + i];
-      ebias[BCO + i] = a.act == ACT_PRELU ? a.slope[co_t * BCO + i] : 0.f;
-    }
-    __syncthreads();
+  float* ebias = (float*)smem;                  // [BCO] bias, [BCO] slope
+  for (int i = tid; i < BCO; i += NT) {         // the K loop ended on a barrier: LDS is free
+    ebias[i] = a.bias[co_t * BCO + i];
+    ebias[BCO + i] = a.act == ACT_PRELU ? a.slope[co_t * BCO + i] : 0.f;
   }
+  __syncthreads();
 #pragma unroll
   for (int wn = 0; wn < WN; ++wn) {
     const int m = m0 + (wave_n * WN + wn) * 32 + l32;
@@ -700,7 +445,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int co = cob + 8 * q;
-        const f32x4 b = EPI_LDS ? *(const f32x4*)(ebias + co - co_t * BCO) : *(const f32x4*)(a.bias + co);
+        const f32x4 b = *(const f32x4*)(ebias + co - co_t * BCO);
         f32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc[wm][wn][4 * q + e] * a.wscale_inv + b[e];
@@ -708,7 +453,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
         } else if (a.act == ACT_PRELU) {
-          const f32x4 sl = EPI_LDS ? *(const f32x4*)(ebias + BCO + co - co_t * BCO) : *(const f32x4*)(a.slope + co);
+          const f32x4 sl = *(const f32x4*)(ebias + BCO + co - co_t * BCO);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
         }
@@ -728,9 +473,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   if (bad) atomicOr(a.range_flag, 1);
 }
 
-// Split-K reduction: the ranges' partial sums added in range order (deterministic),
-// then the epilogue of conv_x3_f16 (bias, activation, range check, masked stores).
-// One thread per (frame, 4-channel group, pixel).
+// Split-K reduction: the ranges' sums added in range order (the order of the in-block
+// ranges, so both give the same bits), then the epilogue of conv_x3_f16 (x 2^-s,
+// bias, activation, range check, masked stores).  One thread per (frame, 4-channel
+// group, pixel).
 __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
   const int HW = a.H * a.W, g4 = (a.cout + 3) / 4;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -747,7 +493,7 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
   const f32x4 b = *(const f32x4*)(a.bias + co);
   f32x4 v;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = sum[e] + b[e];
+  for (int e = 0; e < 4; ++e) v[e] = sum[e] * a.wscale_inv + b[e];
   if (a.act == ACT_RELU) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
@@ -778,10 +524,14 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   constexpr int BPX = WAVES_N * WN * 32;
   constexpr int P = KS / 2;
   constexpr int SEGCAP = x3_segmax(BPX);
+  constexpr bool SPLIT = (VAR & 2048) != 0, RANGED = (VAR & 1024) != 0;
   if (c.in_pad < P) { set_error("conv_x3: input ring narrower than kernel radius"); return hipErrorInvalidValue; }
   if (c.bco != BCO) { set_error("conv_x3: tile mismatch"); return hipErrorInvalidValue; }
   if ((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 7) { set_error("conv_x3: slice not on a chunk"); return hipErrorInvalidValue; }
   if (!c.wx3 || !c.range_flag) { set_error("conv_x3: split weights / range flag missing"); return hipErrorInvalidValue; }
+  if ((SPLIT || RANGED) && c.ksplit < 2) { set_error("conv_x3: K ranges without a range count"); return hipErrorInvalidValue; }
+  if (SPLIT && !c.ws) { set_error("conv_x3: split-K without workspace"); return hipErrorInvalidValue; }
+  if ((VAR & 16384) && !c.dbg) { set_error("conv_x3: stamp build without a stamp buffer"); return hipErrorInvalidValue; }
   X3Args a;
   a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
   a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
@@ -798,26 +548,20 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   a.tpx = tile_pixels(c, BPX, SEGCAP);
   a.px_tiles = (c.H * c.W + a.tpx - 1) / a.tpx;
   a.act = c.act;
-  a.ksplit = (VAR & 2048) ? c.ksplit : 1;
+  a.ksplit = (SPLIT || RANGED) ? c.ksplit : 1;
   a.nfr = c.n;
   a.ws = c.ws;
   a.dbg = c.dbg;
-  if ((VAR & 2048) && (!c.ws || c.ksplit < 2)) { set_error("conv_x3: split-K without workspace"); return hipErrorInvalidValue; }
-  const long long nb = (long long)c.n * a.px_tiles * a.co_tiles * a.ksplit;
+  const long long nb = (long long)c.n * a.px_tiles * a.co_tiles * (SPLIT ? a.ksplit : 1);
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
   hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN, VAR, OCC>), dim3(a.nblocks),
                      dim3(WAVES_M * WAVES_N * 64), 0, s, a);
-  if constexpr ((VAR & 2048) != 0) {
+  if constexpr (SPLIT) {
     const long long nt = (long long)c.n * ((c.cout + 3) / 4) * c.H * c.W;
     hipLaunchKernelGGL(x3_splitk_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, a);
   }
   return hipGetLastError();
-}
-
-static int x3_var() {
-  static const int v = getenv("ISLPOSE_X3_VAR") ? atoi(getenv("ISLPOSE_X3_VAR")) : 0;
-  return v;
 }
 
 static bool x3_small_tiles() {
@@ -825,11 +569,13 @@ static bool x3_small_tiles() {
   return v;
 }
 
-// Tile families.  3x3 / 1x1 layers: 512-pixel tiles (16 waves per block, one
-// block per CU): the weight slab of a K step is then shared by 4x the pixels,
-// which cut the L2->LDS bytes per FLOP ~2x and measured +10 % over the 128-pixel
-// tiles (r01); 16 rather than 8 waves for the narrow (96/64/32-channel) tiles
-// +2-9 %.  7x7 layers keep 128-pixel tiles (their slab is 2.3x larger).
+// 0: no row union (A/B), 1: row union (default), 4: row union with s_memtime stamps
+// (development; needs ConvLaunch::dbg, set only by tools/convbench)
+static int x3_union_mode() {
+  static const int m = getenv("ISLPOSE_X3_UNION") ? atoi(getenv("ISLPOSE_X3_UNION")) : 1;
+  return m;
+}
+
 static int device_cus() {
   static const int n = [] {
     int dev = 0, cus = 0;
@@ -840,24 +586,37 @@ static int device_cus() {
   return n;
 }
 
-// 512-pixel, 16-wave tiles (one block per CU) unless they cannot fill the chip: a
-// layer with fewer such blocks than CUs (the 23x41 stages of Mode R, small hand
-// scales) runs ~2x faster on the 128-pixel, 4-wave family (tools/gpu_tiles.sh).
+// Canonical K ranges of a layer, from its shape alone (never the batch): the small
+// stage layers (<= 1024 pixels per frame: Mode R's 23x41 body stages, the 184 px hand
+// scale) sum their chunk pairs in S ranges, so that a batch-1 frame can spread them
+// over S blocks (split-K) and a large batch can keep them in one block, with the same
+// bits.  Every range is ceil(pairs / S) pairs long and non-empty.
+static int x3_canonical_ranges(const ConvLaunch& c) {
+  const int pairs = (c.cin_chunks + 1) / 2;
+  if (!c.allow_split || c.H * c.W > 1024 || pairs < 4) return 1;
+  int S = std::min(8, pairs / 2);
+  while (S > 1 && (S - 1) * ((pairs + S - 1) / S) >= pairs) --S;
+  return S;
+}
+
+// Tile families.  3x3 / 1x1 layers: 512-pixel tiles (16 waves per block, one
+// block per CU): the weight slab of a K step is then shared by 4x the pixels,
+// which cut the L2->LDS bytes per FLOP ~2x and measured +10 % over the 128-pixel
+// tiles (r01); 16 rather than 8 waves for the narrow (96/64/32-channel) tiles
+// +2-9 %.  7x7 layers keep 128-pixel tiles (their slab is 2.3x larger), and so do
+// layers with canonical K ranges (their second accumulator set needs the 128-pixel
+// family's register budget).  512-pixel tiles are used only when they fill the
+// chip: a layer with fewer such blocks than CUs runs ~2x faster on the 128-pixel,
+// 4-wave family (tools/gpu_tiles.sh).
 static bool x3_big_tiles(const ConvLaunch& c) {
-  if (c.ks > 3 || x3_small_tiles() || x3_var() != 0) return false;
+  if (c.ks > 3 || x3_small_tiles() || x3_canonical_ranges(c) > 1) return false;
   const long long px_tiles = (c.H * c.W + tile_pixels(c, 512, x3_segmax(512)) - 1) / tile_pixels(c, 512, x3_segmax(512));
   return (long long)c.n * px_tiles * ((c.cout + c.bco - 1) / c.bco) >= device_cus();
 }
 
 // Row-union staging (VAR 512) when the longest union run of any 512-pixel tile fits.
-static int x3_union_mode() {
-  static const int m = getenv("ISLPOSE_X3_UNION") ? atoi(getenv("ISLPOSE_X3_UNION")) : 1;
-  return m;
-}
-
 static bool x3_union(const ConvLaunch& c) {
-  const bool off = x3_union_mode() == 0;
-  if (off || c.ks != 3) return false;
+  if (x3_union_mode() == 0 || c.ks != 3) return false;
   const int P = c.ks / 2, Wi = c.W + 2 * c.in_pad, HW = c.H * c.W;
   const int tpx = tile_pixels(c, 512, x3_segmax(512));
   int span = 0;
@@ -868,48 +627,44 @@ static bool x3_union(const ConvLaunch& c) {
   return span + 2 * P * Wi + 2 * P + 1 <= x3_segu_max();
 }
 
+// K-range plan of a launch on the 128-pixel family: S ranges, computed across S blocks
+// per tile (split-K, partials through the workspace) when the plain grid cannot
+// half-fill the CUs, else in one block.  With isl_net_set_split_k(net, 2) (latency
+// mode) layers without canonical ranges also split when their grid is that small --
+// an adaptive S that depends on the batch, so those layers' bits then do too.
+struct X3Ranges {
+  int S = 1;
+  bool across_blocks = false;
+};
+
+static X3Ranges x3_ranges(const ConvLaunch& c) {
+  X3Ranges r;
+  if (x3_big_tiles(c)) return r;
+  const int tpx = tile_pixels(c, 128, x3_segmax(128));
+  const long long blocks = (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * ((c.cout + c.bco - 1) / c.bco);
+  const int cus = device_cus(), pairs = (c.cin_chunks + 1) / 2;
+  r.S = x3_canonical_ranges(c);
+  if (r.S > 1) {
+    r.across_blocks = 2 * blocks <= cus;
+    return r;
+  }
+  if (c.allow_split == 2 && 2 * blocks <= cus && pairs >= 4) {
+    int S = (int)std::min<long long>({8, pairs / 2, (cus + blocks - 1) / blocks});
+    while (S > 1 && (S - 1) * ((pairs + S - 1) / S) >= pairs) --S;
+    r.S = S;
+    r.across_blocks = S > 1;
+  }
+  return r;
+}
+
 template <int KS>
 static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
-  const int var = KS <= 3 ? x3_var() : 0;
   if constexpr (KS == 3) {
     if (x3_big_tiles(c) && x3_union(c)) {
-      if (x3_union_mode() == 2) {
+      if (x3_union_mode() == 4 && c.dbg) {
         switch (c.bco) {
-          case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192, 4>(c, s);
-          case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 4096 | 8192, 4>(c, s);
-          case 64: return launch_t<KS, 2, 8, 1, 2, 512 | 4096 | 8192, 4>(c, s);
-          case 32: return launch_t<KS, 1, 16, 1, 1, 512 | 4096 | 8192, 4>(c, s);
-        }
-      }
-      if (x3_union_mode() == 4) {
-        switch (c.bco) {
-          case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 16384 | 32768, 4>(c, s);
-          case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 4096 | 8192 | 16384 | 32768, 4>(c, s);
-        }
-      }
-      if (x3_union_mode() == 6) {   // ablation (timing only): no weight DMA in the loop
-        if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 16384 | 65536, 4>(c, s);
-      }
-      if (x3_union_mode() == 7) {   // ablation (timing only): no input loads in the loop
-        if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 16384 | 131072, 4>(c, s);
-      }
-      if (x3_union_mode() == 8) {   // ablation (timing only): neither
-        if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 16384 | 65536 | 131072, 4>(c, s);
-      }
-      if (x3_union_mode() == 5) {
-        switch (c.bco) {
-          case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 4096 | 8192 | 32768, 4>(c, s);
-          case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 4096 | 8192 | 32768, 4>(c, s);
-          case 64: return launch_t<KS, 2, 8, 1, 2, 512 | 4096 | 8192 | 32768, 4>(c, s);
-          case 32: return launch_t<KS, 1, 16, 1, 1, 512 | 4096 | 8192 | 32768, 4>(c, s);
-        }
-      }
-      if (x3_union_mode() == 3) {
-        switch (c.bco) {
-          case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 8192, 4>(c, s);
-          case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 8192, 4>(c, s);
-          case 64: return launch_t<KS, 2, 8, 1, 2, 512 | 8192, 4>(c, s);
-          case 32: return launch_t<KS, 1, 16, 1, 1, 512 | 8192, 4>(c, s);
+          case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 16384, 4>(c, s);
+          case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 16384, 4>(c, s);
         }
       }
       switch (c.bco) {
@@ -929,22 +684,14 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
         case 32: return launch_t<KS, 1, 16, 1, 1, 0, 4>(c, s);   // 16 waves, 32co x 32px
       }
     }
-    if (var == 4 && c.bco == 128) return launch_t<KS, 2, 2, 2, 4, 3, 1>(c, s);
-    if (var == 5 && c.bco == 128) return launch_t<KS, 2, 2, 2, 4, 1, 1>(c, s);
-    if (var == 6 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 1, 2>(c, s);
-    if (var == 7 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 0, 2>(c, s);
-    if (var == 8 && c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 1, 4>(c, s);
-    if (var == 256 && c.bco == 128) return launch_t<KS, 2, 4, 2, 2, 256, 2>(c, s);
-    if (var == 64 && c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 64, 4>(c, s);
-    if (var == 64 && c.bco == 96) return launch_t<KS, 1, 8, 3, 2, 64, 2>(c, s);
-    if (var == 64 && c.bco == 64) return launch_t<KS, 1, 8, 2, 2, 64, 2>(c, s);
   }
+  const bool ranged = c.ksplit > 1 && !c.ws;      // launch_conv_x3: in-block ranges
+  const bool split = c.ksplit > 1 && c.ws;        // across blocks
   switch (c.bco) {
-#define X3_CASE(BC, WMS, WNS, WMM, WNN)                                                   \
-  case BC:                                                                                \
-    if (var == 0 && c.ksplit > 1) return launch_t<KS, WMS, WNS, WMM, WNN, 2048, 2>(c, s); \
-    if (var == 1) return launch_t<KS, WMS, WNS, WMM, WNN, (KS <= 3 ? 1 : 0), 2>(c, s);    \
-    if (var == 3) return launch_t<KS, WMS, WNS, WMM, WNN, (KS <= 3 ? 3 : 0), 2>(c, s);    \
+#define X3_CASE(BC, WMS, WNS, WMM, WNN)                                           \
+  case BC:                                                                        \
+    if (split) return launch_t<KS, WMS, WNS, WMM, WNN, 2048, 2>(c, s);            \
+    if (ranged) return launch_t<KS, WMS, WNS, WMM, WNN, 1024, 2>(c, s);           \
     return launch_t<KS, WMS, WNS, WMM, WNN, 0, 2>(c, s);
     X3_CASE(128, 2, 2, 2, 2)
     X3_CASE(96, 1, 4, 3, 1)
@@ -965,35 +712,22 @@ double conv_x3_mfma_flops(const ConvLaunch& c) {
   return 3.0 * 2.0 * co * (((c.cin_chunks + 1) / 2) * 16.0) * c.ks * c.ks * px * c.n;
 }
 
-// Split-K factor for a launch on the 128-pixel family: when the grid cannot half-fill
-// the CUs (batch-1 frames, single hand crops, the 23x41 stages of small batches), the
-// chunk pairs are split over up to 8 blocks per tile, at least 2 pairs each.
-// Opt-in per net (isl_net_set_split_k): the split adds the K ranges in a different
-// association, so a frame's maps then depend (in the last bits) on the batch it came
-// in; by default every frame gives the same bits at any batch size.
-static int x3_ksplit(const ConvLaunch& c) {
-  if (!c.allow_split || x3_big_tiles(c) || x3_var() != 0) return 1;
-  const int tpx = tile_pixels(c, 128, x3_segmax(128));
-  const long long blocks = (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * ((c.cout + c.bco - 1) / c.bco);
-  const int cus = device_cus(), pairs = (c.cin_chunks + 1) / 2;
-  if (2 * blocks > cus || pairs < 4) return 1;
-  int S = (int)std::min<long long>({8, pairs / 2, (cus + blocks - 1) / blocks});
-  // the kernel's ranges are ceil(pairs / S) pairs long: keep every one non-empty
-  while (S > 1 && (S - 1) * ((pairs + S - 1) / S) >= pairs) --S;
-  return S;
-}
-
 size_t x3_splitk_ws_floats(const ConvLaunch& c) {
-  const int S = x3_ksplit(c);
-  return S > 1 ? (size_t)S * c.n * ((c.cout + 7) / 8) * 8 * c.H * c.W : 0;
+  const X3Ranges r = x3_ranges(c);
+  return r.across_blocks ? (size_t)r.S * c.n * ((c.cout + 7) / 8) * 8 * c.H * c.W : 0;
 }
 
 hipError_t launch_conv_x3(const ConvLaunch& c0, hipStream_t s) {
   ConvLaunch c = c0;
-  c.ksplit = 1;
-  if (c.ws) {
-    const int S = x3_ksplit(c);
-    if (S > 1 && (size_t)S * c.n * ((c.cout + 7) / 8) * 8 * c.H * c.W <= c.ws_floats) c.ksplit = S;
+  const X3Ranges r = x3_ranges(c);
+  c.ksplit = r.S;
+  if (r.across_blocks) {
+    if (!c.ws || (size_t)r.S * c.n * ((c.cout + 7) / 8) * 8 * c.H * c.W > c.ws_floats) {
+      set_error("conv_x3: split-K workspace too small");
+      return hipErrorInvalidValue;
+    }
+  } else {
+    c.ws = nullptr;        // in-block ranges (or none)
   }
   switch (c.ks) {
     case 1: return launch_ks<1>(c, s);

@@ -225,7 +225,7 @@ struct isl_net {
   std::vector<TimedRun> timed;
   // conv algorithm (ISL_ALGO_*) and the split-fp16 range flag (isl_net_check)
   int algo = ISL_ALGO_X3;
-  int split_k = 0;             // isl_net_set_split_k (default: env ISLPOSE_X3_SPLITK=1)
+  int split_k = 1;             // isl_net_set_split_k: K-range mode (env ISLPOSE_X3_SPLITK=0|1|2)
   int* d_flag = nullptr;
   // pre-processing image table (device, grow-only; refilled stream-ordered per call)
   void* d_tab = nullptr;
@@ -789,8 +789,9 @@ int isl_net_create(int kind, int device, isl_net** out) {
   net->device = device;
   net->algo = default_algo();
   {
+    // K-range mode (isl_net_set_split_k): 1 canonical ranges (default), 0 none, 2 latency
     const char* e = getenv("ISLPOSE_X3_SPLITK");
-    net->split_k = e && e[0] == '1';
+    net->split_k = e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
   }
   net->layers = kind == ISL_BODY25 ? body25_layers() : kind == ISL_COCO ? coco_layers() : hand_layers();
   for (size_t i = 0; i < net->layers.size(); ++i) {
@@ -1006,9 +1007,10 @@ int isl_net_set_algo(isl_net* net, int algo) {
 
 int isl_net_get_algo(const isl_net* net) { return net ? net->algo : fail(ISL_E_ARG, "net is NULL"); }
 
-int isl_net_set_split_k(isl_net* net, int on) {
+int isl_net_set_split_k(isl_net* net, int mode) {
   if (!net) return fail(ISL_E_ARG, "net is NULL");
-  net->split_k = on != 0;
+  if (mode < 0 || mode > 2) return fail(ISL_E_ARG, "split-K mode must be 0, 1 or 2");
+  net->split_k = mode;
   return ISL_OK;
 }
 

@@ -135,7 +135,8 @@ class Net:
         check(lib().isl_net_create(kind, device, ctypes.byref(h)), "isl_net_create")
         self.h = h
         self.loaded = False
-        self.split_k = os.environ.get("ISLPOSE_X3_SPLITK", "")[:1] == "1"   # isl_net_create's default
+        e = os.environ.get("ISLPOSE_X3_SPLITK", "")[:1]
+        self.split_k = int(e) if e in ("0", "2") else 1      # isl_net_create's default
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -201,10 +202,13 @@ class Net:
         (Winograd F(2x2,3x3), FP32 MFMA) or 'direct' (implicit GEMM, FP32 MFMA)."""
         check(lib().isl_net_set_algo(self.h, ALGOS[algo]), "isl_net_set_algo")
 
-    def set_split_k(self, on: bool):
-        """Split-K for small grids (batch-1 latency, ~2x at 184x328); see isl_net_set_split_k."""
-        check(lib().isl_net_set_split_k(self.h, int(bool(on))), "isl_net_set_split_k")
-        self.split_k = bool(on)
+    def set_split_k(self, mode):
+        """K-range mode of the x3 convs (isl_net_set_split_k): 1 canonical ranges (default,
+        batch-invariant bits), 0 none, 2 latency (also an adaptive, batch-dependent split
+        of the other small grids).  True/False map to 2/0."""
+        mode = {True: 2, False: 0}.get(mode, mode) if isinstance(mode, bool) else int(mode)
+        check(lib().isl_net_set_split_k(self.h, mode), "isl_net_set_split_k")
+        self.split_k = mode
 
     def algo_scope(self, algo: str):
         import contextlib

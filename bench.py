@@ -296,13 +296,14 @@ def gpu_main(args, rank, local, world):
     executed = dk["mfma_flops"] / sec / 1e12                   # what the matrix cores ran (tile padding included)
     conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3, 4))
     conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3, 4))
-    traffic = mfma_busy = clk = None
+    traffic = mfma_busy = clk = busy_s = clk_s = None
     prof = os.path.join(REPO, "profiles", "conv_traffic.json")
     if os.path.exists(prof):
         pj = json.load(open(prof))
         key = {1: "direct", 2: "wino", 3: "x3", 4: "wino_x3"}.get(dom, "x3")
         traffic = pj.get(key + "_hbm_bytes_per_launch")
         mfma_busy, clk = pj.get(key + "_mfma_busy_frac"), pj.get(key + "_effective_clock_ghz")
+        busy_s, clk_s = pj.get(key + "_mfma_busy_frac_at_stamp_clock"), pj.get(key + "_stamp_clock_ghz")
     out = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -347,7 +348,13 @@ def gpu_main(args, rank, local, world):
                      # fraction of the conv kernels' wall cycles, and the DVFS clock they ran at
                      "mfma_busy_pmc": mfma_busy,
                      "effective_clock_ghz": clk,
-                     "frac_at_effective_clock": round(achieved / (peak * clk / 2.4), 4) if clk else None},
+                     "frac_at_effective_clock": round(achieved / (peak * clk / 2.4), 4) if clk else None,
+                     # the GRBM-based clock reads high on sub-10 ms dispatches (MI355X_MICROARCH.md DVFS item 6);
+                     # the in-kernel clock of a stamp build (s_memtime / s_memrealtime) of the dominant shape:
+                     "mfma_busy_pmc_at_stamp_clock": busy_s,
+                     "stamp_clock_ghz": clk_s,
+                     "frac_at_stamp_clock": round(achieved / (peak * clk_s / 2.4), 4) if clk_s else None,
+                     "pmc_source": "profiles/conv_traffic.json (tools/profile_round.sh + tools/pmc_summary.py)"},
         "post": post_fields(H, W, B, post_ms, pairs),
         "e2e": e2e,
         "cpu_baseline": None,

@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr bool UNION = (VAR & 512) != 0;
   constexpr int SEGUP = x3_segu_max() + 1;       // + dummy slot
   constexpr int XSLABU = 2 * 2 * SEGUP;          // [hi|lo][h][px]
-  constexpr int SMEM = UNION ? 2 * (WSLAB + XSLABU) : 2 * BUF;
+  constexpr int SMEM = UNION ? 2 * WSLAB + 2 * XSLABU : 2 * BUF;
   static_assert(SMEM * 16 <= 160 * 1024, "LDS");
   constexpr bool RANGED = (VAR & 1024) != 0;
   constexpr bool SPLIT = (VAR & 2048) != 0;
@@ -271,6 +271,13 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
           }
         };
         stamp(0);
+        if constexpr (STAMP) {
+          // clock check: s_memrealtime (100 MHz) beside s_memtime at steps 1 and T-1, slots past the stamps
+          if (blockIdx.x == 0 && lane == 0 && wave == 0 && (t == 1 || t == T - 1)) {
+            a.dbg[(size_t)16 * T * 4 + (t == 1 ? 0 : 2)] = __builtin_amdgcn_s_memtime();
+            a.dbg[(size_t)16 * T * 4 + (t == 1 ? 1 : 3)] = __builtin_amdgcn_s_memrealtime();
+          }
+        }
         if (!loader && t + 1 < T) issue_c(t + 1, (t + 1) & 1);
         stamp(1);
         __builtin_amdgcn_sched_barrier(0);
@@ -615,8 +622,8 @@ static bool x3_big_tiles(const ConvLaunch& c) {
 }
 
 // Row-union staging (VAR 512) when the longest union run of any 512-pixel tile fits.
-static bool x3_union(const ConvLaunch& c) {
-  if (x3_union_mode() == 0 || c.ks != 3) return false;
+// longest row-union run (pixels) over the 512-pixel tiles of a layer
+static int x3_union_run(const ConvLaunch& c) {
   const int P = c.ks / 2, Wi = c.W + 2 * c.in_pad, HW = c.H * c.W;
   const int tpx = tile_pixels(c, 512, x3_segmax(512));
   int span = 0;
@@ -624,7 +631,12 @@ static bool x3_union(const ConvLaunch& c) {
     const int ml = std::min(m0 + tpx, HW) - 1;
     span = std::max(span, (ml / c.W - m0 / c.W) * Wi + (ml % c.W - m0 % c.W));
   }
-  return span + 2 * P * Wi + 2 * P + 1 <= x3_segu_max();
+  return span + 2 * P * Wi + 2 * P + 1;
+}
+
+static bool x3_union(const ConvLaunch& c) {
+  if (x3_union_mode() == 0 || c.ks != 3) return false;
+  return x3_union_run(c) <= x3_segu_max();
 }
 
 // K-range plan of a launch on the 128-pixel family: S ranges, computed across S blocks

@@ -72,8 +72,8 @@ int main(int argc, char** argv) {
   const int T = pairs * ks;
   unsigned long long* dbg = nullptr;
   if (getenv("ISLPOSE_X3_UNION") && atoi(getenv("ISLPOSE_X3_UNION")) == 4) {
-    CK(hipMalloc(&dbg, (size_t)16 * T * 4 * 8));
-    CK(hipMemset(dbg, 0, (size_t)16 * T * 4 * 8));
+    CK(hipMalloc(&dbg, ((size_t)16 * T * 4 + 4) * 8));
+    CK(hipMemset(dbg, 0, ((size_t)16 * T * 4 + 4) * 8));
     L.dbg = dbg;
   }
   const double flops = 2.0 * cout * cin * ks * ks * (double)H * W * n;
@@ -113,7 +113,7 @@ int main(int argc, char** argv) {
   if (dbg) {
     // per step: issue (0->1), compute (1->2), store (2->3), barrier (3 -> next 0), for
     // the earliest and latest wave, averaged over the steps of the last launch
-    std::vector<unsigned long long> h((size_t)16 * T * 4);
+    std::vector<unsigned long long> h((size_t)16 * T * 4 + 4);
     CK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
     auto at = [&](int w, int t, int k) { return (double)h[((size_t)w * T + t) * 4 + k]; };
     double ph[4] = {0, 0, 0, 0}, step = 0;
@@ -132,6 +132,13 @@ int main(int argc, char** argv) {
     }
     printf("  stamps (cycles per step, mean over waves and %d steps): issue %.0f compute %.0f store %.0f barrier %.0f; "
            "step %.0f\n", nst, ph[0] / nst, ph[1] / nst, ph[2] / nst, ph[3] / nst, step / nst);
+    {
+      const double* z = nullptr;
+      (void)z;
+      const double dt = (double)h[(size_t)16 * T * 4 + 2] - (double)h[(size_t)16 * T * 4];
+      const double dr = (double)h[(size_t)16 * T * 4 + 3] - (double)h[(size_t)16 * T * 4 + 1];
+      if (dr > 0) printf("  in-kernel clock (s_memtime / s_memrealtime x 100 MHz, steps 1..T-1): %.3f GHz\n", dt / dr * 0.1);
+    }
     for (int w = 0; w < 16; ++w)
       printf("    wave %2d step 5: compute %.0f store %.0f wait %.0f\n", w, at(w, 5, 2) - at(w, 5, 1),
              at(w, 5, 3) - at(w, 5, 2), at(w, 6, 0) - at(w, 5, 3));

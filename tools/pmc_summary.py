@@ -42,7 +42,39 @@ def load(d, name):
     return out, {k: len(v) for k, v in disp.items()}
 
 
-def mfma_busy(sq_dir, stats_csv, sq_out):
+def durations(stats_csv):
+    """kernel class -> (calls, average ns) from a rocprofv3 --stats kernel_stats.csv."""
+    out = {}
+    for r in csv.DictReader(open(stats_csv)):
+        k = r["Name"].split("(")[0].replace("void ", "").split("<")[0].replace("isl::", "")
+        c, t = out.get(k, (0, 0.0))
+        out[k] = (c + int(r["Calls"]), t + float(r["TotalDurationNs"]))
+    return {k: (c, t / c) for k, (c, t) in out.items()}
+
+
+POST_KERNELS = ("blur_nms_kernel", "limb_kernel", "tile_live_kernel", "compact_kernel", "assemble_kernel",
+                "resize_sep_kernel")
+
+
+def post_traffic(res, stats_csv, out_path, src):
+    """HBM traffic of the post kernels per launch (PMC) and the rate over their rocprof
+    average duration, against the 8 TB/s HBM peak."""
+    dur = durations(stats_csv)
+    t = {"source": src, "peak_GBps": 8000.0,
+         "note": "per launch (one launch = the post of one bench step, 32 frames): hbm_bytes = FETCH_SIZE x2 (gfx950 "
+                 "wide-read correction) + WRITE_SIZE; avg_us = rocprofv3 --stats average of the same kernel in the "
+                 "trace pass of the same command; GBps = hbm_bytes / avg_us. blur_nms_kernel is bound by fp64 VALU "
+                 "work on live tiles (37 fp64 ops per output per pass, scipy's order), not by HBM"}
+    for k in POST_KERNELS:
+        if k in res and k in dur:
+            b = res[k]["hbm_bytes_per_launch"]
+            us = dur[k][1] / 1e3
+            t[k] = {"hbm_bytes_per_launch": round(b), "avg_us": round(us, 2), "GBps": round(b / us / 1e3, 1),
+                    "frac_of_hbm_peak": round(b / us / 1e3 / 8000.0, 4)}
+    json.dump(t, open(out_path, "w"), indent=1)
+
+
+def mfma_busy(sq_dir, stats_csv, sq_out, clock_ghz=None):
     """MFMA pipe busy fraction and effective clock of the x3 conv kernels.
     SQ_VALU_MFMA_BUSY_CYCLES counts 32 cycles per 32x32x16 MFMA summed over the chip's
     1024 SIMDs; GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md)."""
@@ -61,13 +93,19 @@ def mfma_busy(sq_dir, stats_csv, sq_out):
         return {}
     wall_ns = sum(float(r["TotalDurationNs"]) for r in csv.DictReader(open(stats_csv)) if "conv_x3" in r["Name"])
     active = x["GRBM_GUI_ACTIVE"] / 8
-    return {"x3_mfma_busy_frac": round(x["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / active, 4),
+    extra = {}
+    if clock_ghz:
+        # GRBM_GUI_ACTIVE / 8 / wall reads high on sub-10 ms dispatches (MI355X_MICROARCH.md, DVFS item 6):
+        # the in-kernel clock of a stamp build (s_memtime / s_memrealtime) is the one to divide by
+        extra = {"x3_mfma_busy_frac_at_stamp_clock": round(x["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (wall_ns * clock_ghz), 4),
+                 "x3_stamp_clock_ghz": clock_ghz}
+    return dict(extra, **{"x3_mfma_busy_frac": round(x["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / active, 4),
             "x3_effective_clock_ghz": round(active / wall_ns, 3),
             "mfma_note": "SQ_VALU_MFMA_BUSY_CYCLES (32 cycles per 32x32x16 MFMA, summed over 1024 SIMDs) / 1024 / "
                          "(GRBM_GUI_ACTIVE / 8 XCDs): the fraction of the conv kernels' cycles the MFMA pipes were "
                          "busy, at the clock the chip actually ran (DVFS); effective clock = GRBM_GUI_ACTIVE / 8 / "
                          "summed conv_x3 duration of the trace pass of the same command. Source: "
-                         + os.path.relpath(sq_out)}
+                         + os.path.relpath(sq_out)})
 
 
 def main():
@@ -79,6 +117,8 @@ def main():
     p.add_argument("--traffic-out", default=None)
     p.add_argument("--sq", default=None, help="SQ/GRBM pass dir (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)")
     p.add_argument("--stats", default=None, help="kernel_stats.csv of the trace pass of the same command")
+    p.add_argument("--clock-ghz", type=float, default=None, help="in-kernel clock from a stamp build (tools/gpu_clock.sh)")
+    p.add_argument("--post-out", default=None, help="write the post kernels' traffic here (profiles/post_traffic.json)")
     a = p.parse_args()
     (fe, nfe), (wr, nwr) = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")
     res = {}
@@ -102,8 +142,10 @@ def main():
                 t[key + "_hbm_bytes_per_launch"] = res[cls]["hbm_bytes_per_launch"]
                 t[key + "_dispatches"] = res[cls]["dispatches"]
         if a.sq and a.stats:
-            t.update(mfma_busy(a.sq, a.stats, os.path.join(os.path.dirname(a.out), "sq_counters.json")))
+            t.update(mfma_busy(a.sq, a.stats, os.path.join(os.path.dirname(a.out), "sq_counters.json"), a.clock_ghz))
         json.dump(t, open(a.traffic_out, "w"), indent=1)
+    if a.post_out and a.stats:
+        post_traffic(res, a.stats, a.post_out, os.path.relpath(a.out))
     for k, v in res.items():
         print("%-40s read %10.1f MB  write %10.1f MB" % (k, v["read_bytes_per_step"] / 1e6, v["write_bytes_per_step"] / 1e6))
 

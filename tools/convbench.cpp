@@ -51,7 +51,9 @@ int main(int argc, char** argv) {
   in.pad = pin; in.cs = cs_in; out.pad = pout; out.cs = cs_out;
   in.base = dev_random<float>(in.bytes() / 4, -1.f, 1.f, 1);
   CK(hipMalloc(&out.base, out.bytes()));
-  const int chunks = cs_in / 8, pairs = (chunks + 1) / 2, bco = conv_bco_for(cout), co_tiles = (cout + bco - 1) / bco;
+  // env CONVBENCH_BCO overrides the output-channel tile (timing of other tile families)
+  const int bco = getenv("CONVBENCH_BCO") ? atoi(getenv("CONVBENCH_BCO")) : conv_bco_for(cout);
+  const int chunks = cs_in / 8, pairs = (chunks + 1) / 2, co_tiles = (cout + bco - 1) / bco;
   float* wd = dev_random<float>((size_t)co_tiles * chunks * ks * ks * 2 * bco * 4, -0.05f, 0.05f, 2);
   _Float16* wx = dev_random<_Float16>((size_t)co_tiles * pairs * ks * ks * 4 * bco * 8, -8192.f, 8192.f, 3);
   const int wb = wino_bco_for(cout);

@@ -43,7 +43,7 @@
 //         are staged once as one run, a third per ky step, by loader waves, while
 //         DMA waves stream the weights (role split, see the union loop);
 //   1024  canonical K ranges (in-block): the chunk pairs are summed in S ranges,
-//         each from zero, and the range sums added in order -- the same bits as
+//         each from zero, and the range sums added in order -- the same bits as 2048;
 //   2048  split-K across blocks: each block writes one range's sum, x3_splitk_reduce
 //         adds them in range order.  S depends on the layer shape only
 //         (x3_canonical_ranges), so a frame gives the same bits at any batch size
@@ -355,33 +355,6 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
 #pragma unroll
       for (int kx = 0; kx < KS; ++kx) tap(sw, sx, SEGP, kx);
     };
-    // VAR 64: the next step's DMA pieces go out between the taps (a few before each
-    // tap's MFMA group) instead of all ahead of the step's MFMAs
-    constexpr int NPW = (WSLAB / 64 + NWAVES - 1) / NWAVES;     // pieces per wave and step
-    constexpr int PPT = (NPW + KS - 1) / KS;                    // ... per tap
-    auto issue_part = [&](int t, int buf, int kx) __attribute__((always_inline)) {
-      const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
-      f16x8* dst = smem + buf * BUF;
-#pragma unroll
-      for (int k = 0; k < PPT; ++k) {
-        const int j = kx * PPT + k;                             // this wave's j-th piece
-        const int q = j * NWAVES + wave_u;
-        if (j < NPW && ((WSLAB / 64) % NWAVES == 0 || q < WSLAB / 64))
-          __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
-                                           (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
-      }
-    };
-    auto compute_spread = [&](int buf, int t, bool nxt) __attribute__((always_inline)) {
-      const f16x8* sw = smem + buf * BUF + h * BCO + wave_m * WM * 32 + l32;
-      const f16x8* sx = smem + buf * BUF + WSLAB + h * SEGP;
-#pragma unroll
-      for (int kx = 0; kx < KS; ++kx) {
-        if (nxt) issue_part(t + 1, buf ^ 1, kx);
-        __builtin_amdgcn_sched_barrier(0);
-        tap(sw, sx, SEGP, kx);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
     // K ranges: [t0, t1) of this block (SPLIT: one range), range length R steps
     int t0 = 0, t1 = T, R = T;
     if constexpr (SPLIT || RANGED) {
@@ -399,16 +372,11 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     __syncthreads();
     for (int t = t0; t < t1; ++t) {
       const int buf = (t - t0) & 1;
-      if constexpr ((VAR & 64) != 0) {
-        if (t + 1 < t1) load_x(t + 1);
-        compute_spread(buf, t, t + 1 < t1);
-      } else {
-        if (t + 1 < t1) {
-          issue_w(t + 1, buf ^ 1);
-          load_x(t + 1);
-        }
-        compute(buf);
+      if (t + 1 < t1) {
+        issue_w(t + 1, buf ^ 1);
+        load_x(t + 1);
       }
+      compute(buf);
       if constexpr (RANGED) {
         // end of a range: its sum (from zero) joins the total, ranges in order
         if (t + 1 == t1 || (t + 1) % R == 0) {
@@ -615,11 +583,6 @@ static int x3_union_mode() {
   return m;
 }
 
-static bool x3_spread() {
-  static const bool v = getenv("ISLPOSE_X3_SPREAD") && getenv("ISLPOSE_X3_SPREAD")[0] == '1';
-  return v;
-}
-
 static int device_cus() {
   static const int n = [] {
     int dev = 0, cus = 0;
@@ -726,14 +689,6 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   }
   if constexpr (KS <= 3) {
     if (x3_big_tiles(c)) {
-      if (x3_spread()) {
-        switch (c.bco) {
-          case 128: return launch_t<KS, 2, 8, 2, 2, 64, 4>(c, s);
-          case 96: return launch_t<KS, 1, 16, 3, 1, 64, 4>(c, s);
-          case 64: return launch_t<KS, 2, 8, 1, 2, 64, 4>(c, s);
-          case 32: return launch_t<KS, 1, 16, 1, 1, 64, 4>(c, s);
-        }
-      }
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 0, 4>(c, s);   // 16 waves, 64co x 64px each
         case 96: return launch_t<KS, 1, 16, 3, 1, 0, 4>(c, s);   // 16 waves, 96co x 32px
@@ -749,7 +704,6 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   case BC:                                                                        \
     if (split) return launch_t<KS, WMS, WNS, WMM, WNN, 2048, 2>(c, s);            \
     if (ranged) return launch_t<KS, WMS, WNS, WMM, WNN, 1024, 2>(c, s);           \
-    if (x3_spread()) return launch_t<KS, WMS, WNS, WMM, WNN, 64, 2>(c, s);        \
     return launch_t<KS, WMS, WNS, WMM, WNN, 0, 2>(c, s);
     X3_CASE(128, 2, 2, 2, 2)
     X3_CASE(96, 1, 4, 3, 1)

@@ -3,6 +3,6 @@ export TMPDIR=/tmp
 O=gpurun_out/${1:-clk}; mkdir -p $O
 for s in "3 128 128 46 82 32" "3 384 128 46 82 32"; do
   echo "== $s" >> $O/c.txt
-  ISLPOSE_X3_RING=0 ISLPOSE_X3_UNION=4 timeout -k 10 120 tools/convbench $s 200 x3 4 >> $O/c.txt 2>&1 || { tail $O/c.txt; exit 1; }
+  ISLPOSE_X3_UNION=4 timeout -k 10 120 tools/convbench $s 200 x3 4 >> $O/c.txt 2>&1 || { tail $O/c.txt; exit 1; }
 done
 grep -E "==|round|clock|stamps" $O/c.txt

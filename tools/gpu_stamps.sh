@@ -1,11 +1,8 @@
-# s_memtime phase stamps of the row-union loop (ISLPOSE_X3_UNION=4, development build), per shape,
-# with the 3-buffer weight ring (default) and without (ISLPOSE_X3_RING=0).
+# s_memtime phase stamps of the row-union loop (ISLPOSE_X3_UNION=4, development build), per shape.
 export TMPDIR=/tmp
 O=gpurun_out/${1:-stamps}; mkdir -p $O
 for s in "3 128 128 46 82 32" "3 384 128 46 82 32"; do
-  for r in 1 0; do
-    echo "== $s union=4 ring=$r" >> $O/s.txt
-    ISLPOSE_X3_RING=$r ISLPOSE_X3_UNION=4 timeout -k 10 120 tools/convbench $s 10 x3 2 >> $O/s.txt 2>&1 || { tail $O/s.txt; exit 1; }
-  done
+  echo "== $s union=4" >> $O/s.txt
+  ISLPOSE_X3_UNION=4 timeout -k 10 120 tools/convbench $s 10 x3 2 >> $O/s.txt 2>&1 || { tail $O/s.txt; exit 1; }
 done
 cat $O/s.txt

@@ -42,6 +42,7 @@ METRIC = "frames/sec body_25 368×656 fwd+NMS+PAF at 1/8 MI355X; conv MFMA util 
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 matrix peak (spec) = 256 CU x 4 SIMD x 64 FLOP/clk x 2.4 GHz
 PEAK_FP16_MFMA_TFLOPS = 2516.6     # dense FP16/BF16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF, no sparsity)
 PEAK_HBM_GBPS = 8000.0             # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+MFMA_LOOP_CEILING_TF = 1549.0      # measured: bare x3 3x3 step loop, 32x32x16, all CUs (profiles/r02/mfma_shape/)
 KIND = {0: "maxpool2_kernel", 1: "conv_mfma_f32 (direct fp32)", 2: "wino_f23_mfma (Winograd F(2x2,3x3) fp32)",
         3: "conv_x3_f16 (split-fp16 x3, fp32-accurate)",
         4: "wino_x3_f16 (Winograd F(2x2,3x3), split-fp16 x3, fp32-accurate)"}
@@ -354,7 +355,13 @@ def gpu_main(args, rank, local, world):
                      "mfma_busy_pmc_at_stamp_clock": busy_s,
                      "stamp_clock_ghz": clk_s,
                      "frac_at_stamp_clock": round(achieved / (peak * clk_s / 2.4), 4) if clk_s else None,
-                     "pmc_source": "profiles/conv_traffic.json (tools/profile_round.sh + tools/pmc_summary.py)"},
+                     "pmc_source": "profiles/conv_traffic.json (tools/profile_round.sh + tools/pmc_summary.py)",
+                     # the bare x3 inner loop (LDS fragment reads + 3 MFMAs per product, no staging,
+                     # no barriers) on every CU: what the chip sustains with this MFMA shape under its
+                     # power limit (the clock settles at ~1.55 GHz)
+                     "mfma_loop_ceiling_tflops": MFMA_LOOP_CEILING_TF if key == "x3" else None,
+                     "frac_of_mfma_loop_ceiling": round(achieved / MFMA_LOOP_CEILING_TF, 4) if key == "x3" else None,
+                     "ceiling_source": "tools/mfma_shape_bench.hip step32, profiles/r02/mfma_shape/mfma_shape_bench.txt"},
         "post": post_fields(H, W, B, post_ms, pairs),
         "e2e": e2e,
         "cpu_baseline": None,

@@ -861,6 +861,19 @@ __device__ int uf_find(PT parent, int x) {
   }
 }
 
+// read-only walk to the root, for the final labelling pass: each pixel's owner then
+// stores the root, and nobody else writes that slot, so every parent ends as its
+// root.  (A halving find here could, racing with the owner, overwrite a stored
+// root with a mere ancestor.)
+template <typename PT>
+__device__ int uf_root(PT parent, int x) {
+  while (true) {
+    const int p = ld_parent(parent, x);
+    if (p == x) return x;
+    x = p;
+  }
+}
+
 // lock-free union: hook the larger root under the smaller with a CAS, so the
 // final root of every component is its smallest raster index (= label order).
 template <typename PT>
@@ -1005,8 +1018,89 @@ __device__ double np_sum(const double* a, int n) {
 }
 
 constexpr int CC_LDS_MAX = 36864;   // plane pixels whose parent array fits LDS (144 KB)
+constexpr int CC_CHUNK = 4096;      // pixels per block of the multi-block pre-pass (large planes)
 
-template <bool LDSP>
+// Adds map[p] into vals[root of p] for this thread's pixels p = p0, p0 + step, ...:
+// runs of equal roots are summed in a register and flushed with one atomic, so a
+// plane that is one big component (random weights) costs one atomic per thread,
+// not one per pixel on a single address.  Order-free (see the candidate pass).
+template <typename PT>
+__device__ __forceinline__ void cc_root_sums(PT parent, const double* map, double* vals, int p0, int p1, int step) {
+  int cur = -1;
+  double acc = 0.0;
+  for (int p = p0; p < p1; p += step) {
+    const int r = parent[p];
+    if (r < 0) continue;
+    if (r != cur) {
+      if (cur >= 0) atomicAdd(&vals[cur], acc);
+      cur = r;
+      acc = 0.0;
+    }
+    acc += map[p];
+  }
+  if (cur >= 0) atomicAdd(&vals[cur], acc);
+}
+
+// Multi-block pre-pass for planes above CC_LDS_MAX (hand crops of HD frames reach
+// 600 x 600 px): one block per (plane, CC_CHUNK pixels) for each phase, separated by
+// launches -- init (parents, zeroed sums), union, find + root sums.  One workgroup
+// per plane doing all of it serialised ~1.4 M global CAS round trips on dense maps.
+__global__ void __launch_bounds__(256) cc_init_kernel(const unsigned long long* __restrict__ mask, int h, int w,
+                                                      int words, int chunks, int* __restrict__ parent_all,
+                                                      double* __restrict__ vals_all) {
+  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  const int P = h * w;
+  const unsigned long long* mk = mask + (size_t)plane * h * words;
+  int* parent = parent_all + (size_t)plane * P;
+  double* vals = vals_all + (size_t)plane * P;
+  for (int p = c * CC_CHUNK + threadIdx.x; p < min(P, (c + 1) * CC_CHUNK); p += 256) {
+    const int y = p / w, x = p - y * w;
+    parent[p] = ((mk[(size_t)y * words + (x >> 6)] >> (x & 63)) & 1ull) ? p : -1;
+    vals[p] = 0.0;
+  }
+}
+
+__global__ void __launch_bounds__(256) cc_union_kernel(const unsigned long long* __restrict__ mask, int h, int w,
+                                                       int words, int chunks, int* __restrict__ parent_all) {
+  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  const int P = h * w;
+  const unsigned long long* mk = mask + (size_t)plane * h * words;
+  int* parent = parent_all + (size_t)plane * P;
+  auto bit = [&](int y, int x) -> bool { return (mk[(size_t)y * words + (x >> 6)] >> (x & 63)) & 1ull; };
+  for (int p = c * CC_CHUNK + threadIdx.x; p < min(P, (c + 1) * CC_CHUNK); p += 256) {
+    const int y = p / w, x = p - y * w;
+    if (!bit(y, x)) continue;
+    if (x > 0 && bit(y, x - 1)) uf_union(parent, p, p - 1);
+    if (y > 0) {
+      if (x > 0 && bit(y - 1, x - 1)) uf_union(parent, p, p - w - 1);
+      if (bit(y - 1, x)) uf_union(parent, p, p - w);
+      if (x + 1 < w && bit(y - 1, x + 1)) uf_union(parent, p, p - w + 1);
+    }
+  }
+}
+
+// labelling: every pixel's parent becomes its root (roots are final once every union
+// is done; uf_root), then, in the next launch, the root sums
+__global__ void __launch_bounds__(256) cc_find_kernel(int h, int w, int chunks, int* __restrict__ parent_all) {
+  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  const int P = h * w;
+  int* parent = parent_all + (size_t)plane * P;
+  for (int p = c * CC_CHUNK + threadIdx.x; p < min(P, (c + 1) * CC_CHUNK); p += 256)
+    if (ld_parent(parent, p) >= 0)
+      __hip_atomic_store(parent + p, uf_root(parent, p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ planes, int h, int w, int chunks,
+                                                     const int* __restrict__ parent_all, double* __restrict__ vals_all) {
+  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  const int P = h * w;
+  cc_root_sums(parent_all + (size_t)plane * P, planes + (size_t)plane * P, vals_all + (size_t)plane * P,
+               c * CC_CHUNK + threadIdx.x, min(P, (c + 1) * CC_CHUNK), 256);
+}
+
+// LDSP: parents in LDS (planes up to CC_LDS_MAX px).  PRE: parents (roots) and root
+// sums come from the multi-block pre-pass (global parents).
+template <bool LDSP, bool PRE>
 __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__ planes,
                                                       const unsigned long long* __restrict__ mask, int h, int w,
                                                       int words, int* __restrict__ parent_all,
@@ -1032,9 +1126,13 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
   __syncthreads();
   int local = 0;
   for (int p = tid; p < P; p += 256) {
-    const bool b = bit(p / w, p % w);
-    parent[p] = b ? p : -1;
-    local += b;
+    if constexpr (PRE) {
+      local += parent[p] >= 0;
+    } else {
+      const bool b = bit(p / w, p % w);
+      parent[p] = b ? p : -1;
+      local += b;
+    }
   }
   atomicAdd(&s_cnt, local);
   __syncthreads();
@@ -1042,25 +1140,28 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
     if (tid == 0) { out[plane * 2] = 0; out[plane * 2 + 1] = 0; }
     return;
   }
-  __threadfence_block();
-  __syncthreads();
-  // union over the 4 raster-earlier neighbours (8-connectivity)
-  for (int p = tid; p < P; p += 256) {
-    if (parent[p] < 0) continue;
-    const int y = p / w, x = p - y * w;
-    if (x > 0 && bit(y, x - 1)) uf_union(parent, p, p - 1);
-    if (y > 0) {
-      if (x > 0 && bit(y - 1, x - 1)) uf_union(parent, p, p - w - 1);
-      if (bit(y - 1, x)) uf_union(parent, p, p - w);
-      if (x + 1 < w && bit(y - 1, x + 1)) uf_union(parent, p, p - w + 1);
+  if constexpr (!PRE) {
+    __threadfence_block();
+    __syncthreads();
+    // union over the 4 raster-earlier neighbours (8-connectivity)
+    for (int p = tid; p < P; p += 256) {
+      if (parent[p] < 0) continue;
+      const int y = p / w, x = p - y * w;
+      if (x > 0 && bit(y, x - 1)) uf_union(parent, p, p - 1);
+      if (y > 0) {
+        if (x > 0 && bit(y - 1, x - 1)) uf_union(parent, p, p - w - 1);
+        if (bit(y - 1, x)) uf_union(parent, p, p - w);
+        if (x + 1 < w && bit(y - 1, x + 1)) uf_union(parent, p, p - w + 1);
+      }
     }
+    __threadfence();
+    __syncthreads();
+    for (int p = tid; p < P; p += 256)
+      if (ld_parent(parent, p) >= 0)
+        __hip_atomic_store(parent + p, uf_root(parent, p), __ATOMIC_RELAXED, UfScope<PT>::v);
+    __threadfence();
+    __syncthreads();
   }
-  __threadfence();
-  __syncthreads();
-  for (int p = tid; p < P; p += 256)
-    if (ld_parent(parent, p) >= 0) parent[p] = uf_find(parent, p);
-  __threadfence();
-  __syncthreads();
   // np.argmax over the components' np.sum (hand.py:68-69): only components whose sum
   // can be the maximum need numpy's exact pairwise order.  An order-free fp64 sum per
   // root (atomics; relative error < 1e-12 for these sizes) finds the maximum M; the
@@ -1071,15 +1172,16 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
   constexpr int MAXC = 64;
   __shared__ int s_cand[MAXC];
   __shared__ int s_ncand;
-  for (int p = tid; p < P; p += 256) vals[p] = 0.0;
-  __threadfence_block();
-  __syncthreads();
-  for (int p = tid; p < P; p += 256) {
-    const int r = parent[p];
-    if (r >= 0) atomicAdd(&vals[r], map[p]);
+  if constexpr (!PRE) {
+    for (int p = tid; p < P; p += 256) vals[p] = 0.0;
+    __threadfence_block();
+    __syncthreads();
+    // contiguous pixel runs per thread, so equal roots aggregate in a register
+    const int per = (P + 255) / 256;
+    cc_root_sums(parent, map, vals, tid * per, min(P, (tid + 1) * per), 1);
+    __threadfence();
+    __syncthreads();
   }
-  __threadfence();
-  __syncthreads();
   {
     double m = -INFINITY;
     for (int p = tid; p < P; p += 256)
@@ -1470,15 +1572,21 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
   if (h * w <= CC_LDS_MAX) {
     static bool attr = false;
     if (!attr) {
-      PHIP(hipFuncSetAttribute((const void*)hand_cc_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      PHIP(hipFuncSetAttribute((const void*)hand_cc_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                CC_LDS_MAX * 4));
       attr = true;
     }
-    hipLaunchKernelGGL(hand_cc_kernel<true>, dim3(n * nparts), dim3(256), (size_t)h * w * 4, s, (const double*)avg,
-                       mask, h, w, words, parent, vals, (long long*)d_peaks);
+    hipLaunchKernelGGL((hand_cc_kernel<true, false>), dim3(n * nparts), dim3(256), (size_t)h * w * 4, s,
+                       (const double*)avg, mask, h, w, words, parent, vals, (long long*)d_peaks);
   } else {
-    hipLaunchKernelGGL(hand_cc_kernel<false>, dim3(n * nparts), dim3(256), 0, s, (const double*)avg, mask, h, w,
-                       words, parent, vals, (long long*)d_peaks);
+    const int chunks = (int)((P + CC_CHUNK - 1) / CC_CHUNK);
+    const dim3 g(n * nparts * chunks);
+    hipLaunchKernelGGL(cc_init_kernel, g, dim3(256), 0, s, mask, h, w, words, chunks, parent, vals);
+    hipLaunchKernelGGL(cc_union_kernel, g, dim3(256), 0, s, mask, h, w, words, chunks, parent);
+    hipLaunchKernelGGL(cc_find_kernel, g, dim3(256), 0, s, h, w, chunks, parent);
+    hipLaunchKernelGGL(cc_sum_kernel, g, dim3(256), 0, s, (const double*)avg, h, w, chunks, parent, vals);
+    hipLaunchKernelGGL((hand_cc_kernel<false, true>), dim3(n * nparts), dim3(256), 0, s, (const double*)avg, mask,
+                       h, w, words, parent, vals, (long long*)d_peaks);
   }
   PHIP(hipGetLastError());
   return ISL_OK;

@@ -65,6 +65,29 @@ def synth_weights(kind: int, seed: int = 0) -> dict:
     return out
 
 
+HEAT_LAYER = {"body25": "Mconv7_stage1_L1", "coco": "Mconv7_stage6_L2"}
+
+
+def tame_heat_layer(weights: dict, heat: np.ndarray, model_type: str = "body25", gain: float = 0.05) -> dict:
+    """Synthetic weights whose heat output behaves like a trained net's.
+
+    Raw outputs of the seeded He-init weights put thousands of peaks on a frame
+    (SURVEY §8d).  Given the net's heat output on one calibration frame (low-res
+    [1, C, h, w], from any implementation of the net), the heat output layer is
+    rescaled per channel: heat_k = gain * (z_k - mean_k) / std_k, so a part map
+    crosses the 0.1 peak threshold where its field is ~0.1/gain standard deviations
+    high -- a handful of peaks per part, a few persons per frame.  The PAF layers are
+    untouched."""
+    z = np.asarray(heat)[0].reshape(heat.shape[1], -1).astype(np.float64)
+    m, s = z.mean(1), np.maximum(z.std(1), 1e-6)
+    a = gain / s
+    layer = HEAT_LAYER[model_type]
+    out = dict(weights)
+    out[layer + ".weight"] = (weights[layer + ".weight"] * a[:, None, None, None]).astype(np.float32)
+    out[layer + ".bias"] = ((weights[layer + ".bias"] - m) * a).astype(np.float32)
+    return out
+
+
 def synth_frames(n: int, h: int, w: int, seed: int = 0) -> np.ndarray:
     """uint8 [n, h, w, 3] BGR frames; frame i depends only on (seed, i)."""
     frames = np.empty((n, h, w, 3), np.uint8)

@@ -105,15 +105,20 @@ class ISLSignPos(object):
         """frames uint8 [n, H, W, 3] -> [(candidate, subset, all_hand_peaks)] * n, equal to
         call() per frame.  The body runs as one batch; every hand crop of the batch
         (util.handDetect boxes, in the reference's order) runs as one batch per scale."""
-        frames = np.ascontiguousarray(_as_numpy(frames), dtype=np.uint8)
         body, hand = self._estimators()
-        t = torch.from_numpy(frames).to("cuda:%d" % body.device)
+        if isinstance(frames, torch.Tensor) and frames.is_cuda:
+            # already resident (islpose.pipeline's prefetch: async H2D on a copy stream)
+            if frames.dtype != torch.uint8 or frames.ndim != 4 or frames.shape[3] != 3:
+                raise ValueError("frames: uint8 [n, H, W, 3] expected, got %s %s" % (frames.dtype, tuple(frames.shape)))
+            t = frames.contiguous()
+        else:
+            t = torch.from_numpy(np.ascontiguousarray(_as_numpy(frames), dtype=np.uint8)).to("cuda:%d" % body.device)
         res = body.estimate(t)
-        boxes, owner = [], []
+        boxes = []
         for i, (c, s) in enumerate(res):
-            for x, y, w, _is_left in util.handDetect(c, s, frames[i]):
+            # handDetect reads only the frame's shape (util.py:245)
+            for x, y, w, _is_left in util.handDetect(c, s, t[i]):
                 boxes.append((i, x, y, w))
-                owner.append(i)
         peaks = hand.estimate_crops(t, boxes)
         out = [(c, s, []) for (c, s) in res]
         for (i, x, y, _w), pk in zip(boxes, peaks):

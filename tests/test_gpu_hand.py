@@ -46,6 +46,29 @@ def test_hand_post_designed_batch(hest, h, w):
         assert np.array_equal(got[i], ref), i
 
 
+@pytest.mark.parametrize("h,w,dense", [(256, 256, False), (200, 330, False), (192, 192, True), (260, 240, True)])
+def test_hand_post_large_and_dense(hest, h, w, dense):
+    """Planes above the LDS parent array (> 36864 px: the multi-block union-find
+    pre-pass) and dense maps (random-weight-like: a few giant components, every pixel
+    over the threshold) against the oracle, bit for bit."""
+    n = 2
+    geoms = [g[1:] for g in scale_geometry(h, w, HAND_SCALES)]
+    rng = np.random.RandomState(h + w)
+    heats, per = [], []
+    for (nh, nw, vh, vw) in geoms:
+        if dense:
+            maps = [rng.uniform(0.02, 1.0, (22, nh // 8, nw // 8)).astype(np.float32) for _ in range(n)]
+        else:
+            maps = [synth.designed_hand_maps(nh // 8, nw // 8, seed=5 * i + nh, n_blobs=3) for i in range(n)]
+        per.append(maps)
+        heats.append(torch.from_numpy(np.stack(maps)).cuda())
+    got = hest.post_maps(h, w, geoms, heats)
+    for i in range(n):
+        it = iter([per[s][i] for s in range(4)])
+        ref = cpu_ref.hand_call(np.zeros((h, w, 3), np.uint8), lambda im: next(it)[None])
+        assert np.array_equal(got[i], ref), i
+
+
 def test_hand_estimate_end_to_end(hest):
     crops = synth.synth_frames(2, 96, 96, seed=11)
     t = torch.from_numpy(crops).cuda()

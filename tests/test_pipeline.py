@@ -147,3 +147,29 @@ def test_pipeline_gpu_matches_isl_sign_pos(tmp_path):
         ref = isl.call(np.ascontiguousarray(frames[i][:, :, ::-1]))
         with open(f['filepath']) as fh:
             assert fh.read() == pipeline.frame_json(*ref)
+
+
+@pytest.mark.gpu
+def test_pipeline_overlap_equals_sequential(tmp_path):
+    """The overlapped pipeline (prefetch thread + pinned ring + copy stream, GPU flip,
+    writer thread) writes what the sequential loop writes, over several videos and
+    ragged batches (5 frames, batch 2), and resumes the same way."""
+    base, rows = _videos(tmp_path, n_videos=3, T=5)
+    outs = {}
+    for ov in (False, True):
+        out = str(tmp_path / ("out%d" % ov))
+        model = FakeModel()
+        feats, ex = pipeline.extract_dataset(rows, pipeline.npy_decoder(base), model, out, batch=2, overlap=ov)
+        assert ex.frames_done == 15 and model.calls == [2, 2, 1] * 3
+        outs[ov] = feats
+        texts = []
+        for f in feats:
+            with open(f['filepath']) as fh:
+                texts.append(fh.read())
+        outs[ov] = ([{k: v for k, v in f.items() if k != 'filepath'} for f in feats], texts)
+    assert outs[True] == outs[False]
+    # resume under overlap: nothing recomputed
+    model = FakeModel()
+    feats, ex = pipeline.extract_dataset(rows, pipeline.npy_decoder(base), model, str(tmp_path / "out1"),
+                                         batch=2, overlap=True)
+    assert feats == [] and ex.frames_skipped == 15 and model.calls == []

@@ -7,6 +7,8 @@
   C4  body_25 4-scale pyramid (scale_search 0.5/1/1.5/2 -> nets 184x328 ... 736x1312),
       batch 16 frames per GPU (128 over 8 GPUs, sharded), post on designed maps.
 
+  C5  the video -> JSON pipeline (islpose.pipeline) on 1080x1920 RGB frames, body
+      (Mode R) + batched hand crops + per-frame JSON files, sequential vs overlapped.
   C6  translator head: the HIP sign classifier (csrc/sign.hip) on [B, 20, 156]
       windows -- latency of one window (the demo's per-frame call) and throughput
       of a batch of 4096 windows; plus translate_stream over a 64-frame clip
@@ -122,6 +124,57 @@ def c4(args):
             "conv_gflop_per_step": round(gf, 1), "conv_tflops_fp32_equiv_wall": round(gf / sec / 1e3, 1)}
 
 
+def c5(args):
+    """configs[4]: the extract_features_mp.py:122-132 pipeline on 1080x1920 RGB frames
+    (Mode R body net 184x327 -> 184x328, batched hand crops, per-frame JSON files),
+    sequential vs overlapped (prefetch + async H2D + GPU flip + writer thread)."""
+    import shutil
+    import tempfile
+    from islpose import pipeline, synth
+    from islpose.body import BodyEstimator
+    from src.body import Body
+    from src.hand import Hand
+    from src.ISL_Model_parameter import ISLSignPos
+    T, H, W = args.c5_frames, 1080, 1920
+    rgb = synth.synth_frames(T, H, W, seed=57)
+    # heat layer tamed on the GPU net's own output for frame 0 (a few persons per frame)
+    wb = synth.synth_weights(0)
+    cal = BodyEstimator(wb, "body25", scale_search=(0.5,))
+    _, _, heats = cal.run_scales(torch.from_numpy(np.ascontiguousarray(rgb[:1, ..., ::-1])).cuda(), keep_maps=True)
+    wb = synth.tame_heat_layer(wb, heats[0].cpu().numpy(), "body25", gain=0.05)
+    del cal
+    tw = lambda d: {k: torch.from_numpy(v) for k, v in d.items()}  # noqa: E731
+    isl = ISLSignPos(Body(tw(wb), "body25").model, Hand(tw(synth.synth_weights(2))).model)
+    clips = {"v%d.mp4" % k: rgb for k in range(args.c5_videos)}
+    rows = [{"Filepath": f, "type": "Greetings", "expression": "hello"} for f in clips]
+    res = {"config": "C5 video -> per-frame JSON, 1080x1920 RGB frames", "frames": T * len(rows),
+           "videos": len(rows), "batch": args.batch, "export": False,
+           "decode": "frames already decoded in host memory (pims/ffmpeg absent); the pipeline reads them as "
+                     "slices of the [T,H,W,3] array"}
+    for ov in (False, True):
+        out = tempfile.mkdtemp(prefix="c5_")
+        try:
+            # warm-up (arenas, hand scales) on the first video, then the timed pass over all
+            pipeline.extract_dataset(rows[:1], clips.__getitem__, isl, out, batch=args.batch, export=False, overlap=ov)
+            shutil.rmtree(out)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            feats, ex = pipeline.extract_dataset(rows, clips.__getitem__, isl, out, batch=args.batch,
+                                                 export=False, overlap=ov)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            hands = 0
+            for f in feats:
+                hands += len(f["all_hand_peaks"])
+        finally:
+            shutil.rmtree(out, ignore_errors=True)
+        key = "overlap" if ov else "sequential"
+        res[key + "_frames_per_s"] = round(ex.frames_done / dt, 2)
+        res[key + "_s"] = round(dt, 3)
+        res["hand_crops_per_frame"] = round(hands / max(len(feats), 1), 2)
+    return res
+
+
 def c6(args):
     from islpose import synth, translate
     from src.body import Body
@@ -159,14 +212,16 @@ def c6(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", choices=["c3", "c4", "c6", "all"], default="all")
+    ap.add_argument("--config", choices=["c3", "c4", "c5", "c6", "all"], default="all")
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--c5-frames", type=int, default=96, help="C5: frames per (synthetic 1080p) video")
+    ap.add_argument("--c5-videos", type=int, default=3)
     ap.add_argument("--raw-hand-maps", dest="designed_hands", action="store_false",
                     help="C3: run the hand post on the raw net maps instead of designed maps")
     a = ap.parse_args()
-    for name, fn in (("c3", c3), ("c4", c4), ("c6", c6)):
+    for name, fn in (("c3", c3), ("c4", c4), ("c5", c5), ("c6", c6)):
         if a.config in (name, "all"):
             print(json.dumps(fn(a)), flush=True)
 

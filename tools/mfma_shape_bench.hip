@@ -116,6 +116,121 @@ __global__ void __launch_bounds__(NT, 4) loop16(const f16x8* g, float* out, int 
   out[blockIdx.x * NT + threadIdx.x] = v;
 }
 
+// One 3x3 (pair, ky) step of the conv, both shapes, equal useful FLOPs per iteration:
+// 3 taps x 2 chunks x 3 terms = 18 fragment units of K = 8 per output tile.
+// step32: per tap A hi/lo x 2, B hi/lo x 2 reads, 4 tiles x 3 MFMAs (36 MFMAs, 24 reads).
+// step16: taps 0+1 as 3 full 16x16x32 MFMAs (hi/lo reuse kept), tap 2's 6 units packed
+// into 2 MFMAs whose second one is half zero (lanes 32-63 read a zeroed LDS region):
+// 16 tiles x 5 MFMAs = 80 (72 useful), 32 reads.
+constexpr int ZERO = LDS_UNITS;   // 64 zeroed units after the data
+__global__ void __launch_bounds__(NT, 4) step32(const f16x8* g, float* out, int iters, unsigned long long* clk) {
+  __shared__ f16x8 s[LDS_UNITS + 64];
+  for (int i = threadIdx.x; i < LDS_UNITS; i += NT) s[i] = g[(blockIdx.x * 131 + i) % (4 * LDS_UNITS)];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x16 acc[2][2] = {};
+  unsigned long long t0 = 0, r0 = 0;
+  if (threadIdx.x == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+  int off = (wave * 64 + lane) & (LDS_UNITS / 2 - 1);
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      f16x8 A[2][2], B[2][2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) {
+          A[m][hl] = s[(off + kx * 256 + m * 32 + hl * 1024) & (LDS_UNITS - 1)];
+          B[m][hl] = s[(off + kx * 8 + m * 32 + hl * 1024 + 2048 + 7) & (LDS_UNITS - 1)];
+        }
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], B[n][0], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], B[n][1], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][1], B[n][0], acc[m][n], 0, 0, 0);
+        }
+    }
+    off = (off + 64) & (LDS_UNITS / 2 - 1);
+  }
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - t0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v += acc[m][n][r];
+  out[blockIdx.x * NT + threadIdx.x] = v;
+}
+
+__global__ void __launch_bounds__(NT, 4) step16(const f16x8* g, float* out, int iters, unsigned long long* clk) {
+  __shared__ f16x8 s[LDS_UNITS + 64];
+  for (int i = threadIdx.x; i < LDS_UNITS; i += NT) s[i] = g[(blockIdx.x * 131 + i) % (4 * LDS_UNITS)];
+  if (threadIdx.x < 64) s[ZERO + threadIdx.x] = f16x8{};
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x4 acc[4][4] = {};
+  unsigned long long t0 = 0, r0 = 0;
+  if (threadIdx.x == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+  int off = (wave * 64 + lane) & (LDS_UNITS / 2 - 1);
+  const bool upper = lane >= 32;
+  for (int it = 0; it < iters; ++it) {
+    {  // taps 0 + 1: hh, hl, lh with fragment reuse
+      f16x8 A[4][2], B[4][2];
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) {
+          A[m][hl] = s[(off + m * 16 + hl * 1024) & (LDS_UNITS - 1)];
+          B[m][hl] = s[(off + m * 16 + hl * 1024 + 2048 + 7) & (LDS_UNITS - 1)];
+        }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[m][0], B[n][0], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[m][0], B[n][1], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[m][1], B[n][0], acc[m][n], 0, 0, 0);
+        }
+    }
+    {  // tap 2: [hh c0 c1 | hl c0 c1] and [lh c0 c1 | zero]
+      f16x8 A[4][2], B[4][2];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        A[m][0] = s[(off + 512 + m * 16) & (LDS_UNITS - 1)];
+        A[m][1] = s[upper ? ZERO + lane : (off + 512 + m * 16 + 1024) & (LDS_UNITS - 1)];
+        B[m][0] = s[(off + 8 + m * 16 + 2048 + 7) & (LDS_UNITS - 1)];
+        B[m][1] = s[(off + 8 + m * 16 + 3072 + 7) & (LDS_UNITS - 1)];
+      }
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[m][0], B[n][0], acc[m][n], 0, 0, 0);
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[m][1], B[n][1], acc[m][n], 0, 0, 0);
+        }
+    }
+    off = (off + 64) & (LDS_UNITS / 2 - 1);
+  }
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - t0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v += acc[m][n][r];
+  out[blockIdx.x * NT + threadIdx.x] = v;
+}
+
 int main(int argc, char** argv) {
   const int blocks = argc > 1 ? atoi(argv[1]) : 1024;
   const int iters = argc > 2 ? atoi(argv[2]) : 4000;
@@ -160,6 +275,27 @@ int main(int argc, char** argv) {
       printf("round %d %s: %.1f us/launch  %.1f TFLOP/s  in-kernel clock %.3f GHz\n", r,
              k == 0 ? "32x32x16" : "16x16x32", ms * 1e3 / 5, fl / (ms * 1e-3) / 1e12,
              c[1] ? (double)c[0] / c[1] * 0.1 : 0.0);
+    }
+  }
+  // the conv-step pair: useful FLOPs per iteration per wave = 3 taps x 4 tiles x 3 x 32x32x16
+  for (int r = 0; r < rounds; ++r) {
+    for (int k = 0; k < 2; ++k) {
+      const int n_it = iters / 3;
+      CK(hipEventRecord(e0, 0));
+      for (int rep = 0; rep < 5; ++rep) {
+        if (k == 0) hipLaunchKernelGGL(step32, dim3(blocks), dim3(NT), 0, 0, g, out, n_it, clk);
+        else hipLaunchKernelGGL(step16, dim3(blocks), dim3(NT), 0, 0, g, out, n_it, clk);
+      }
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      unsigned long long c[2];
+      CK(hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost));
+      const double fl = 5.0 * blocks * 16.0 * n_it * 36 * 32768.0;
+      printf("round %d step %s: %.1f us/launch  %.1f useful TFLOP/s  in-kernel clock %.3f GHz\n", r,
+             k == 0 ? "32x32x16 (36 MFMA)" : "16x16x32 (80 MFMA, 72 useful)", ms * 1e3 / 5,
+             fl / (ms * 1e-3) / 1e12, c[1] ? (double)c[0] / c[1] * 0.1 : 0.0);
     }
   }
   return 0;

@@ -954,18 +954,40 @@ __device__ __forceinline__ double np_leaf(const double* x, int len) {
   return res;
 }
 
-// Block-cooperative np.sum with numpy's exact association (same result as np_sum):
-// per 8192-element buffer, thread 0 lists the leaves of the split tree, the block
-// sums the leaves in parallel, thread 0 combines them in tree order.  Every thread
-// of the block must call it; the result is returned to all of them.
+// Block-cooperative np.sum with numpy's exact association (same result as np_sum).
+// A full 8192-element buffer always has the same tree -- 64 leaves of 128 elements,
+// paired level by level (n2 = n/2 is a multiple of 8 down to 128) -- so one wave
+// sums a buffer: a leaf per lane, then 6 shuffle levels, every wave on its own
+// buffer.  The partial last buffer takes the general path: thread 0 lists the
+// leaves of its split tree, the block sums them, thread 0 combines them in tree
+// order.  Buffers are added left to right.  Every thread of the block must call it;
+// the result is returned to all of them.
 __device__ double np_sum_block(const double* a, int n) {
-  constexpr int MAXL = 128;   // leaves of an 8192-element tree have 65..128 elements
+  constexpr int MAXL = 128;   // leaves of a < 8192-element tree have 65..128 elements
   __shared__ int s_loff[MAXL], s_llen[MAXL], s_nl;
   __shared__ double s_lsum[MAXL];
+  __shared__ double s_part[32];
   __shared__ double s_tot;
-  const int tid = threadIdx.x;
-  for (int i0 = 0; i0 < n; i0 += 8192) {
-    const int len0 = min(8192, n - i0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int nfull = n / 8192;
+  for (int g = 0; g < nfull; g += nw) {
+    const int b = g + wave;
+    if (b < nfull) {
+      double v = np_leaf(a + (size_t)b * 8192 + lane * 128, 128);
+#pragma unroll
+      for (int half = 32; half >= 1; half >>= 1) {
+        const double x0 = __shfl(v, 2 * lane, 64), x1 = __shfl(v, 2 * lane + 1, 64);
+        if (lane < half) v = x0 + x1;
+      }
+      if (lane == 0) s_part[wave] = v;
+    }
+    __syncthreads();
+    if (tid == 0)
+      for (int k = 0; k < nw && g + k < nfull; ++k) s_tot = g + k == 0 ? s_part[k] : s_tot + s_part[k];
+    __syncthreads();
+  }
+  const int i0 = nfull * 8192, len0 = n - i0;
+  if (len0 > 0) {
     if (tid == 0) {   // pre-order leaf list
       int st_off[32], st_len[32], sp = 0, nl = 0;
       st_off[0] = i0; st_len[0] = len0;
@@ -998,7 +1020,7 @@ __device__ double np_sum_block(const double* a, int n) {
         else if (f.state == 1) { f.left = ret; f.state = 2; st[++sp] = {f.len - n2, 0, 0.0}; }
         else { ret = f.left + ret; --sp; }
       }
-      s_tot = i0 == 0 ? ret : s_tot + ret;
+      s_tot = nfull == 0 ? ret : s_tot + ret;
     }
     __syncthreads();
   }
@@ -1018,17 +1040,27 @@ __device__ double np_sum(const double* a, int n) {
 }
 
 constexpr int CC_LDS_MAX = 36864;   // plane pixels whose parent array fits LDS (144 KB)
-constexpr int CC_CHUNK = 4096;      // pixels per block of the multi-block pre-pass (large planes)
+constexpr int CC_CHUNK = 4096;      // pixels per row chunk of the large-plane path
+constexpr int CC_WMAX = 8192;       // widest plane the large-plane path takes (LDS chunk parents)
+constexpr int CC_MAXC = 64;         // candidate components kept per plane
 
-// Adds map[p] into vals[root of p] for this thread's pixels p = p0, p0 + step, ...:
-// runs of equal roots are summed in a register and flushed with one atomic, so a
-// plane that is one big component (random weights) costs one atomic per thread,
-// not one per pixel on a single address.  Order-free (see the candidate pass).
+// per-plane results of the large-plane pre-pass
+struct CcStats {
+  int count;                        // foreground pixels
+  int ncand;                        // components whose approximate sum reaches the candidate bar
+  unsigned long long maxbits;       // largest approximate component sum (bits of a positive double)
+  int cand[CC_MAXC];                // their roots, unordered
+};
+
+// Adds map[p] into vals[root of p] for p in [p0, p1): runs of equal roots are summed
+// in a register and flushed with one atomic; the last flush of a wave whose lanes all
+// hold the same root (a plane that is one big component: random weights) is summed
+// across the wave first.  Order-free (see the candidate pass).
 template <typename PT>
-__device__ __forceinline__ void cc_root_sums(PT parent, const double* map, double* vals, int p0, int p1, int step) {
+__device__ __forceinline__ void cc_root_sums(PT parent, const double* map, double* vals, int p0, int p1) {
   int cur = -1;
   double acc = 0.0;
-  for (int p = p0; p < p1; p += step) {
+  for (int p = p0; p < p1; ++p) {
     const int r = parent[p];
     if (r < 0) continue;
     if (r != cur) {
@@ -1038,73 +1070,237 @@ __device__ __forceinline__ void cc_root_sums(PT parent, const double* map, doubl
     }
     acc += map[p];
   }
-  if (cur >= 0) atomicAdd(&vals[cur], acc);
-}
-
-// Multi-block pre-pass for planes above CC_LDS_MAX (hand crops of HD frames reach
-// 600 x 600 px): one block per (plane, CC_CHUNK pixels) for each phase, separated by
-// launches -- init (parents, zeroed sums), union, find + root sums.  One workgroup
-// per plane doing all of it serialised ~1.4 M global CAS round trips on dense maps.
-__global__ void __launch_bounds__(256) cc_init_kernel(const unsigned long long* __restrict__ mask, int h, int w,
-                                                      int words, int chunks, int* __restrict__ parent_all,
-                                                      double* __restrict__ vals_all) {
-  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
-  const int P = h * w;
-  const unsigned long long* mk = mask + (size_t)plane * h * words;
-  int* parent = parent_all + (size_t)plane * P;
-  double* vals = vals_all + (size_t)plane * P;
-  for (int p = c * CC_CHUNK + threadIdx.x; p < min(P, (c + 1) * CC_CHUNK); p += 256) {
-    const int y = p / w, x = p - y * w;
-    parent[p] = ((mk[(size_t)y * words + (x >> 6)] >> (x & 63)) & 1ull) ? p : -1;
-    vals[p] = 0.0;
+  if (__all(cur == __shfl(cur, 0, 64)) && cur >= 0) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&vals[cur], acc);
+  } else if (cur >= 0) {
+    atomicAdd(&vals[cur], acc);
   }
 }
 
-__global__ void __launch_bounds__(256) cc_union_kernel(const unsigned long long* __restrict__ mask, int h, int w,
-                                                       int words, int chunks, int* __restrict__ parent_all) {
+// Large-plane path (planes above CC_LDS_MAX: hand crops of HD frames reach 600 x 600
+// px), a sequence of multi-block launches over (plane, row chunk of <= CC_CHUNK px):
+//   cc_local  -- connected components of the chunk in LDS (the lock-free union-find at
+//                workgroup scope), labels written as global pixel indices;
+//   cc_merge  -- unions across chunk boundaries only (the chunk's first row with the
+//                row above), on the global parents: a few hundred global CAS per
+//                chunk instead of ~4 per pixel with dependent L2 round trips;
+//   cc_find   -- every parent becomes its root (smallest raster index of the component);
+//   cc_sum    -- approximate root sums and the foreground count;
+//   cc_stats  -- the largest approximate sum, then cc_cand the candidate roots;
+//   hand_cc_kernel<false, true> -- exact sums of the candidates and the argmax.
+__global__ void __launch_bounds__(256) cc_local_kernel(const unsigned long long* __restrict__ mask, int h, int w,
+                                                       int words, int rows, int chunks, int* __restrict__ parent_all,
+                                                       double* __restrict__ vals_all, CcStats* __restrict__ stats) {
+  __shared__ int s_lp[CC_WMAX > CC_CHUNK ? CC_WMAX : CC_CHUNK];
+  lds_int* lp = (lds_int*)s_lp;
   const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
-  const int P = h * w;
+  const int P = h * w, y0 = c * rows, y1 = min(h, y0 + rows), base = y0 * w, n = (y1 - y0) * w;
   const unsigned long long* mk = mask + (size_t)plane * h * words;
   int* parent = parent_all + (size_t)plane * P;
+  double* vals = vals_all + (size_t)plane * P;
   auto bit = [&](int y, int x) -> bool { return (mk[(size_t)y * words + (x >> 6)] >> (x & 63)) & 1ull; };
-  for (int p = c * CC_CHUNK + threadIdx.x; p < min(P, (c + 1) * CC_CHUNK); p += 256) {
-    const int y = p / w, x = p - y * w;
-    if (!bit(y, x)) continue;
-    if (x > 0 && bit(y, x - 1)) uf_union(parent, p, p - 1);
-    if (y > 0) {
-      if (x > 0 && bit(y - 1, x - 1)) uf_union(parent, p, p - w - 1);
-      if (bit(y - 1, x)) uf_union(parent, p, p - w);
-      if (x + 1 < w && bit(y - 1, x + 1)) uf_union(parent, p, p - w + 1);
+  if (c == 0 && threadIdx.x == 0) { stats[plane].count = 0; stats[plane].ncand = 0; stats[plane].maxbits = 0; }
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const int y = y0 + i / w, x = i % w;
+    lp[i] = bit(y, x) ? i : -1;
+    vals[base + i] = 0.0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 256) {
+    if (lp[i] < 0) continue;
+    const int yl = i / w, x = i - yl * w, y = y0 + yl;
+    if (x > 0 && bit(y, x - 1)) uf_union(lp, i, i - 1);
+    if (yl > 0) {
+      if (x > 0 && bit(y - 1, x - 1)) uf_union(lp, i, i - w - 1);
+      if (bit(y - 1, x)) uf_union(lp, i, i - w);
+      if (x + 1 < w && bit(y - 1, x + 1)) uf_union(lp, i, i - w + 1);
     }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 256)
+    if (ld_parent(lp, i) >= 0) __hip_atomic_store(lp + i, uf_root(lp, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += 256) parent[base + i] = lp[i] >= 0 ? base + lp[i] : -1;
+}
+
+__global__ void __launch_bounds__(256) cc_merge_kernel(const unsigned long long* __restrict__ mask, int h, int w,
+                                                       int words, int rows, int chunks, int* __restrict__ parent_all) {
+  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  if (c == 0) return;
+  const int y = c * rows;
+  const unsigned long long* mk = mask + (size_t)plane * h * words;
+  int* parent = parent_all + (size_t)plane * h * w;
+  auto bit = [&](int yy, int x) -> bool { return (mk[(size_t)yy * words + (x >> 6)] >> (x & 63)) & 1ull; };
+  for (int x = threadIdx.x; x < w; x += 256) {
+    if (!bit(y, x)) continue;
+    const int p = y * w + x;
+    if (x > 0 && bit(y - 1, x - 1)) uf_union(parent, p, p - w - 1);
+    if (bit(y - 1, x)) uf_union(parent, p, p - w);
+    if (x + 1 < w && bit(y - 1, x + 1)) uf_union(parent, p, p - w + 1);
   }
 }
 
 // labelling: every pixel's parent becomes its root (roots are final once every union
-// is done; uf_root), then, in the next launch, the root sums
-__global__ void __launch_bounds__(256) cc_find_kernel(int h, int w, int chunks, int* __restrict__ parent_all) {
+// is done; uf_root)
+__global__ void __launch_bounds__(256) cc_find_kernel(int h, int w, int rows, int chunks, int* __restrict__ parent_all) {
   const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
-  const int P = h * w;
+  const int P = h * w, p0 = c * rows * w, p1 = min(P, p0 + rows * w);
   int* parent = parent_all + (size_t)plane * P;
-  for (int p = c * CC_CHUNK + threadIdx.x; p < min(P, (c + 1) * CC_CHUNK); p += 256)
+  for (int p = p0 + threadIdx.x; p < p1; p += 256)
     if (ld_parent(parent, p) >= 0)
       __hip_atomic_store(parent + p, uf_root(parent, p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ planes, int h, int w, int chunks,
-                                                     const int* __restrict__ parent_all, double* __restrict__ vals_all) {
+__global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ planes, int h, int w, int rows,
+                                                     int chunks, const int* __restrict__ parent_all,
+                                                     double* __restrict__ vals_all, CcStats* __restrict__ stats) {
+  __shared__ int s_cnt;
   const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
-  const int P = h * w;
-  cc_root_sums(parent_all + (size_t)plane * P, planes + (size_t)plane * P, vals_all + (size_t)plane * P,
-               c * CC_CHUNK + threadIdx.x, min(P, (c + 1) * CC_CHUNK), 256);
+  const int P = h * w, p0 = c * rows * w, p1 = min(P, p0 + rows * w);
+  const int* parent = parent_all + (size_t)plane * P;
+  const int per = (p1 - p0 + 255) / 256;                    // a contiguous run per thread
+  const int a = min(p1, p0 + threadIdx.x * per), b = min(p1, a + per);
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  int cnt = 0;
+  for (int p = a; p < b; ++p) cnt += parent[p] >= 0;
+  cc_root_sums(parent, planes + (size_t)plane * P, vals_all + (size_t)plane * P, a, b);
+  atomicAdd(&s_cnt, cnt);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_cnt) atomicAdd(&stats[plane].count, s_cnt);
+}
+
+__global__ void __launch_bounds__(256) cc_stats_kernel(int h, int w, int rows, int chunks,
+                                                       const int* __restrict__ parent_all,
+                                                       const double* __restrict__ vals_all, CcStats* __restrict__ stats) {
+  __shared__ double s_m[4];
+  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  const int P = h * w, p0 = c * rows * w, p1 = min(P, p0 + rows * w);
+  const int* parent = parent_all + (size_t)plane * P;
+  const double* vals = vals_all + (size_t)plane * P;
+  double m = 0.0;                                           // sums are of values > thre > 0
+  for (int p = p0 + threadIdx.x; p < p1; p += 256)
+    if (parent[p] == p) m = fmax(m, vals[p]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmax(fmax(s_m[0], s_m[1]), fmax(s_m[2], s_m[3]));
+    if (m > 0.0) atomicMax(&stats[plane].maxbits, (unsigned long long)__double_as_longlong(m));
+  }
+}
+
+__global__ void __launch_bounds__(256) cc_cand_kernel(int h, int w, int rows, int chunks,
+                                                      const int* __restrict__ parent_all,
+                                                      const double* __restrict__ vals_all, CcStats* __restrict__ stats) {
+  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  const int P = h * w, p0 = c * rows * w, p1 = min(P, p0 + rows * w);
+  const int* parent = parent_all + (size_t)plane * P;
+  const double* vals = vals_all + (size_t)plane * P;
+  CcStats& st = stats[plane];
+  if (st.count == 0) return;
+  const double thr_c = __longlong_as_double((long long)st.maxbits) * (1.0 - 1e-9);
+  for (int p = p0 + threadIdx.x; p < p1; p += 256)
+    if (parent[p] == p && vals[p] >= thr_c) {
+      const int slot = atomicAdd(&st.ncand, 1);
+      if (slot < CC_MAXC) st.cand[slot] = p;
+    }
+}
+
+constexpr int CC_NT = 1024;   // threads per plane (one workgroup per (crop, part))
+constexpr int CC_NW = CC_NT / 64;
+constexpr int CC_RUN = 8;     // consecutive pixels per thread and round of the per-plane passes
+
+__device__ __forceinline__ double cc_block_max(double v, double* s_d) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s_d[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = s_d[0];
+#pragma unroll
+  for (int k = 1; k < CC_NW; ++k) r = fmax(r, s_d[k]);
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ int cc_block_sum(int v, int* s_i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) s_i[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int r = 0;
+#pragma unroll
+  for (int k = 0; k < CC_NW; ++k) r += s_i[k];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ int cc_block_min(int v, int* s_i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) s_i[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int r = s_i[0];
+#pragma unroll
+  for (int k = 1; k < CC_NW; ++k) r = min(r, s_i[k]);
+  __syncthreads();
+  return r;
+}
+
+// (value, index) with the larger value, the smaller index on ties (first max)
+__device__ __forceinline__ void cc_pick(double& v, int& i, double v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+}
+
+__device__ __forceinline__ int cc_block_argmax(double v, int i, double* s_d, int* s_i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cc_pick(v, i, __shfl_xor(v, o, 64), __shfl_xor(i, o, 64));
+  if ((threadIdx.x & 63) == 0) { s_d[threadIdx.x >> 6] = v; s_i[threadIdx.x >> 6] = i; }
+  __syncthreads();
+  double bv = s_d[0];
+  int bi = s_i[0];
+#pragma unroll
+  for (int k = 1; k < CC_NW; ++k) cc_pick(bv, bi, s_d[k], s_i[k]);
+  __syncthreads();
+  return bi;
+}
+
+// inclusive prefix sum of v over the CC_NT-thread block; total = the block's sum
+__device__ __forceinline__ int cc_block_scan(int v, int* s_i, int& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(v, d, 64);
+    if (lane >= d) v += y;
+  }
+  if (lane == 63) s_i[wave] = v;
+  __syncthreads();
+  int off = 0;
+  total = 0;
+#pragma unroll
+  for (int k = 0; k < CC_NW; ++k) {
+    const int t = s_i[k];
+    off += k < wave ? t : 0;
+    total += t;
+  }
+  __syncthreads();
+  return v + off;
 }
 
 // LDSP: parents in LDS (planes up to CC_LDS_MAX px).  PRE: parents (roots) and root
-// sums come from the multi-block pre-pass (global parents).
+// sums come from the multi-block pre-pass (global parents).  The per-plane passes
+// walk CC_RUN consecutive pixels per thread and round with 1024 threads: a plane of a
+// 600 px crop is ~44 rounds per pass, not the ~1400 dependent rounds of a
+// 256-thread, one-pixel-per-round loop.
 template <bool LDSP, bool PRE>
-__global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__ planes,
-                                                      const unsigned long long* __restrict__ mask, int h, int w,
-                                                      int words, int* __restrict__ parent_all,
-                                                      double* __restrict__ vals_all, long long* __restrict__ out) {
+__global__ void __launch_bounds__(CC_NT) hand_cc_kernel(const double* __restrict__ planes,
+                                                        const unsigned long long* __restrict__ mask, int h, int w,
+                                                        int words, int* __restrict__ parent_all,
+                                                        double* __restrict__ vals_all, const CcStats* __restrict__ stats,
+                                                        long long* __restrict__ out) {
   extern __shared__ int s_dyn[];
   const int plane = blockIdx.x;   // crop * 21 + part
   const int P = h * w, tid = threadIdx.x;
@@ -1116,27 +1312,30 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
   else parent = parent_all + (size_t)plane * P;
   double* vals = vals_all + (size_t)plane * P;
   auto bit = [&](int y, int x) -> bool { return (mk[(size_t)y * words + (x >> 6)] >> (x & 63)) & 1ull; };
-  __shared__ int s_cnt;
-  __shared__ int s_scan[256];
+  __shared__ int s_i[CC_NW];
+  __shared__ double s_d[CC_NW];
+  constexpr int MAXC = CC_MAXC;
+  __shared__ int s_cand[MAXC];
+  __shared__ int s_ncand;
   __shared__ double s_best_sum;
   __shared__ int s_best_root;
-  __shared__ double s_red_v[256];
-  __shared__ int s_red_i[256];
-  if (tid == 0) s_cnt = 0;
-  __syncthreads();
   int local = 0;
-  for (int p = tid; p < P; p += 256) {
-    if constexpr (PRE) {
-      local += parent[p] >= 0;
-    } else {
-      const bool b = bit(p / w, p % w);
-      parent[p] = b ? p : -1;
-      local += b;
+  if constexpr (PRE) {
+    local = tid == 0 ? stats[plane].count : 0;
+  } else {
+    for (int q = tid * CC_RUN; q < P; q += CC_NT * CC_RUN) {
+#pragma unroll
+      for (int k = 0; k < CC_RUN; ++k) {
+        const int p = q + k;
+        if (p >= P) break;
+        const int y = p / w;
+        const bool b = bit(y, p - y * w);
+        parent[p] = b ? p : -1;
+        local += b;
+      }
     }
   }
-  atomicAdd(&s_cnt, local);
-  __syncthreads();
-  if (s_cnt == 0) {                     // np.sum(binary) == 0 -> [0, 0]
+  if (cc_block_sum(local, s_i) == 0) {     // np.sum(binary) == 0 -> [0, 0]
     if (tid == 0) { out[plane * 2] = 0; out[plane * 2 + 1] = 0; }
     return;
   }
@@ -1144,7 +1343,7 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
     __threadfence_block();
     __syncthreads();
     // union over the 4 raster-earlier neighbours (8-connectivity)
-    for (int p = tid; p < P; p += 256) {
+    for (int p = tid; p < P; p += CC_NT) {
       if (parent[p] < 0) continue;
       const int y = p / w, x = p - y * w;
       if (x > 0 && bit(y, x - 1)) uf_union(parent, p, p - 1);
@@ -1156,7 +1355,7 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
     }
     __threadfence();
     __syncthreads();
-    for (int p = tid; p < P; p += 256)
+    for (int p = tid; p < P; p += CC_NT)
       if (ld_parent(parent, p) >= 0)
         __hip_atomic_store(parent + p, uf_root(parent, p), __ATOMIC_RELAXED, UfScope<PT>::v);
     __threadfence();
@@ -1164,76 +1363,68 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
   }
   // np.argmax over the components' np.sum (hand.py:68-69): only components whose sum
   // can be the maximum need numpy's exact pairwise order.  An order-free fp64 sum per
-  // root (atomics; relative error < 1e-12 for these sizes) finds the maximum M; the
-  // components with approx >= M*(1-1e-9) -- in practice one -- are the candidates, and
-  // only they are summed exactly, in label (= root raster) order, first max kept.
-  // (Random weights give hundreds of components per plane: one exact pass per
-  // component made this kernel 7 ms per crop.)  Sums are of values > thre > 0.
-  constexpr int MAXC = 64;
-  __shared__ int s_cand[MAXC];
-  __shared__ int s_ncand;
+  // root (register-aggregated atomics; relative error < 1e-12 for these sizes) finds
+  // the maximum M; the components with approx >= M*(1-1e-9) -- in practice one -- are
+  // the candidates, and only they are summed exactly, in label (= root raster) order,
+  // first max kept.  Sums are of values > thre > 0.
   if constexpr (!PRE) {
-    for (int p = tid; p < P; p += 256) vals[p] = 0.0;
+    for (int p = tid; p < P; p += CC_NT) vals[p] = 0.0;
     __threadfence_block();
     __syncthreads();
-    // contiguous pixel runs per thread, so equal roots aggregate in a register
-    const int per = (P + 255) / 256;
-    cc_root_sums(parent, map, vals, tid * per, min(P, (tid + 1) * per), 1);
+    const int per = (P + CC_NT - 1) / CC_NT;
+    cc_root_sums(parent, map, vals, tid * per, min(P, (tid + 1) * per));
     __threadfence();
     __syncthreads();
   }
-  {
+  if constexpr (PRE) {
+    if (tid == 0) s_ncand = stats[plane].ncand;
+    if (tid < MAXC) s_cand[tid] = stats[plane].cand[tid];
+  } else {
     double m = -INFINITY;
-    for (int p = tid; p < P; p += 256)
-      if (parent[p] == p) m = fmax(m, vals[p]);
-    s_red_v[tid] = m;
+    for (int q = tid * CC_RUN; q < P; q += CC_NT * CC_RUN) {
+#pragma unroll
+      for (int k = 0; k < CC_RUN; ++k) {
+        const int p = q + k;
+        if (p < P && parent[p] == p) m = fmax(m, vals[p]);
+      }
+    }
+    const double thr_c = cc_block_max(m, s_d) * (1.0 - 1e-9);
+    if (tid == 0) s_ncand = 0;
     __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-      if (tid < off) s_red_v[tid] = fmax(s_red_v[tid], s_red_v[tid + off]);
-      __syncthreads();
+    for (int q = tid * CC_RUN; q < P; q += CC_NT * CC_RUN) {
+#pragma unroll
+      for (int k = 0; k < CC_RUN; ++k) {
+        const int p = q + k;
+        if (p < P && parent[p] == p && vals[p] >= thr_c) {
+          const int slot = atomicAdd(&s_ncand, 1);
+          if (slot < MAXC) s_cand[slot] = p;
+        }
+      }
     }
   }
-  const double thr_c = s_red_v[0] * (1.0 - 1e-9);
-  if (tid == 0) s_ncand = 0;
   __syncthreads();
-  for (int r0 = 0; r0 < P;) {   // candidate roots in raster order
-    int cand = 0x7fffffff;
-    for (int p = r0 + tid; p < P; p += 256)
-      if (parent[p] == p && vals[p] >= thr_c) { cand = p; break; }
-    s_scan[tid] = cand;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-      if (tid < off) s_scan[tid] = min(s_scan[tid], s_scan[tid + off]);
-      __syncthreads();
-    }
-    const int root = s_scan[0];
-    __syncthreads();
-    if (root == 0x7fffffff) break;
-    if (tid == 0) {
-      if (s_ncand < MAXC) s_cand[s_ncand] = root;
-      ++s_ncand;
-    }
-    __syncthreads();
-    r0 = root + 1;
-  }
   const bool all_roots = s_ncand > MAXC;   // pathological ties: every component, exactly
-  if (tid == 0) { s_best_root = -1; s_best_sum = 0.0; }
+  if (tid == 0) {
+    if (!all_roots)                        // label order = root raster order
+      for (int i = 1; i < s_ncand; ++i) {
+        const int v = s_cand[i];
+        int j = i - 1;
+        while (j >= 0 && s_cand[j] > v) { s_cand[j + 1] = s_cand[j]; --j; }
+        s_cand[j + 1] = v;
+      }
+    s_best_root = -1;
+    s_best_sum = 0.0;
+  }
   __syncthreads();
-  for (int ci = 0, r0 = 0; all_roots ? r0 < P : ci < s_ncand; ++ci) {
+  const int ncand = s_ncand;
+  for (int ci = 0, r0 = 0; all_roots ? r0 < P : ci < ncand; ++ci) {
     int root;
     if (all_roots) {
       // next root (parent[r] == r) at or after r0, found cooperatively
       int cand = 0x7fffffff;
-      for (int p = r0 + tid; p < P; p += 256)
+      for (int p = r0 + tid; p < P; p += CC_NT)
         if (parent[p] == p) { cand = p; break; }
-      s_scan[tid] = cand;
-      __syncthreads();
-      for (int off = 128; off > 0; off >>= 1) {
-        if (tid < off) s_scan[tid] = min(s_scan[tid], s_scan[tid + off]);
-        __syncthreads();
-      }
-      root = s_scan[0];
-      __syncthreads();
+      root = cc_block_min(cand, s_i);
       if (root == 0x7fffffff) break;
       r0 = root + 1;
     } else {
@@ -1241,20 +1432,17 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
     }
     // compact this component's values in raster order
     int base = 0;
-    for (int c0 = root; c0 < P; c0 += 256) {
-      const int p = c0 + tid;
-      const int f = (p < P && parent[p] == root) ? 1 : 0;
-      s_scan[tid] = f;
-      __syncthreads();
-      for (int off = 1; off < 256; off <<= 1) {
-        const int v = tid >= off ? s_scan[tid - off] : 0;
-        __syncthreads();
-        s_scan[tid] += v;
-        __syncthreads();
-      }
-      if (f) vals[base + s_scan[tid] - 1] = map[p];
-      base += s_scan[255];
-      __syncthreads();
+    for (int c0 = root; c0 < P; c0 += CC_NT * CC_RUN) {
+      const int q0 = c0 + tid * CC_RUN;
+      int cnt = 0;
+#pragma unroll
+      for (int k = 0; k < CC_RUN; ++k) cnt += (q0 + k < P && parent[q0 + k] == root) ? 1 : 0;
+      int total;
+      int o = base + cc_block_scan(cnt, s_i, total) - cnt;
+#pragma unroll
+      for (int k = 0; k < CC_RUN; ++k)
+        if (q0 + k < P && parent[q0 + k] == root) vals[o++] = map[q0 + k];
+      base += total;
     }
     __threadfence_block();
     __syncthreads();
@@ -1266,25 +1454,17 @@ __global__ void __launch_bounds__(256) hand_cc_kernel(const double* __restrict__
   const int best = s_best_root;
   double bv = -INFINITY;
   int bi = 0x7fffffff;
-  for (int p = tid; p < P; p += 256) {
-    const double v = parent[p] == best ? map[p] : 0.0;
-    if (v > bv || (v == bv && p < bi)) { bv = v; bi = p; }
-  }
-  s_red_v[tid] = bv;
-  s_red_i[tid] = bi;
-  __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (tid < off) {
-      const double v2 = s_red_v[tid + off];
-      const int i2 = s_red_i[tid + off];
-      if (v2 > s_red_v[tid] || (v2 == s_red_v[tid] && i2 < s_red_i[tid])) { s_red_v[tid] = v2; s_red_i[tid] = i2; }
+  for (int q = tid * CC_RUN; q < P; q += CC_NT * CC_RUN) {
+#pragma unroll
+    for (int k = 0; k < CC_RUN; ++k) {
+      const int p = q + k;
+      if (p < P) cc_pick(bv, bi, parent[p] == best ? map[p] : 0.0, p);
     }
-    __syncthreads();
   }
+  const int pbest = cc_block_argmax(bv, bi, s_d, s_i);
   if (tid == 0) {
-    const int p = s_red_i[0];
-    out[plane * 2] = p % w;       // [x, y]
-    out[plane * 2 + 1] = p / w;
+    out[plane * 2] = pbest % w;       // [x, y]
+    out[plane * 2 + 1] = pbest / w;
   }
 }
 
@@ -1537,13 +1717,16 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t avg_bytes = (size_t)n * nparts * P * 8, mask_bytes = (size_t)n * nparts * h * words * 8;
   const size_t par_bytes = (size_t)n * nparts * P * 4, val_bytes = (size_t)n * nparts * P * 8;
-  char* base = (char*)net_scratch(net, up(avg_bytes) + up(mid_bytes) + up(mask_bytes) + up(par_bytes) + up(val_bytes));
+  const size_t st_bytes = (size_t)n * nparts * sizeof(CcStats);
+  char* base = (char*)net_scratch(net, up(avg_bytes) + up(mid_bytes) + up(mask_bytes) + up(par_bytes) + up(val_bytes) +
+                                           up(st_bytes));
   if (!base) return ISL_E_HIP;
   double* avg = (double*)base;
   float* mid = (float*)(base + up(avg_bytes));
   unsigned long long* mask = (unsigned long long*)((char*)mid + up(mid_bytes));
   int* parent = (int*)((char*)mask + up(mask_bytes));
   double* vals = (double*)((char*)parent + up(par_bytes));
+  CcStats* stats = (CcStats*)((char*)vals + up(val_bytes));
   PHIP(hipMemsetAsync(avg, 0, avg_bytes, s));
   const float div_f = (float)nscales;
   for (int si = 0; si < nscales; ++si) {
@@ -1576,17 +1759,20 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
                                CC_LDS_MAX * 4));
       attr = true;
     }
-    hipLaunchKernelGGL((hand_cc_kernel<true, false>), dim3(n * nparts), dim3(256), (size_t)h * w * 4, s,
-                       (const double*)avg, mask, h, w, words, parent, vals, (long long*)d_peaks);
+    hipLaunchKernelGGL((hand_cc_kernel<true, false>), dim3(n * nparts), dim3(CC_NT), (size_t)h * w * 4, s,
+                       (const double*)avg, mask, h, w, words, parent, vals, nullptr, (long long*)d_peaks);
   } else {
-    const int chunks = (int)((P + CC_CHUNK - 1) / CC_CHUNK);
+    if (w > CC_WMAX) return post_fail(ISL_E_ARG, "isl_hand_post: crop wider than 8192 px");
+    const int rows = std::max(1, CC_CHUNK / w), chunks = (h + rows - 1) / rows;
     const dim3 g(n * nparts * chunks);
-    hipLaunchKernelGGL(cc_init_kernel, g, dim3(256), 0, s, mask, h, w, words, chunks, parent, vals);
-    hipLaunchKernelGGL(cc_union_kernel, g, dim3(256), 0, s, mask, h, w, words, chunks, parent);
-    hipLaunchKernelGGL(cc_find_kernel, g, dim3(256), 0, s, h, w, chunks, parent);
-    hipLaunchKernelGGL(cc_sum_kernel, g, dim3(256), 0, s, (const double*)avg, h, w, chunks, parent, vals);
-    hipLaunchKernelGGL((hand_cc_kernel<false, true>), dim3(n * nparts), dim3(256), 0, s, (const double*)avg, mask,
-                       h, w, words, parent, vals, (long long*)d_peaks);
+    hipLaunchKernelGGL(cc_local_kernel, g, dim3(256), 0, s, mask, h, w, words, rows, chunks, parent, vals, stats);
+    hipLaunchKernelGGL(cc_merge_kernel, g, dim3(256), 0, s, mask, h, w, words, rows, chunks, parent);
+    hipLaunchKernelGGL(cc_find_kernel, g, dim3(256), 0, s, h, w, rows, chunks, parent);
+    hipLaunchKernelGGL(cc_sum_kernel, g, dim3(256), 0, s, (const double*)avg, h, w, rows, chunks, parent, vals, stats);
+    hipLaunchKernelGGL(cc_stats_kernel, g, dim3(256), 0, s, h, w, rows, chunks, parent, vals, stats);
+    hipLaunchKernelGGL(cc_cand_kernel, g, dim3(256), 0, s, h, w, rows, chunks, parent, vals, stats);
+    hipLaunchKernelGGL((hand_cc_kernel<false, true>), dim3(n * nparts), dim3(CC_NT), 0, s, (const double*)avg, mask,
+                       h, w, words, parent, vals, stats, (long long*)d_peaks);
   }
   PHIP(hipGetLastError());
   return ISL_OK;

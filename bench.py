@@ -445,6 +445,7 @@ def cpu_baseline(args, mult, nh, nw):
     t_fwd, t_post = [], []
     torch.set_num_threads(share)
     for i in range(args.cpu_frames):
+        print("cpu_baseline: frame %d/%d" % (i + 1, args.cpu_frames), file=sys.stderr, flush=True)
         t0 = time.perf_counter()
         im, _, _ = cpu_ref.net_input(frames[i], mult)
         fwd(im)
@@ -455,7 +456,10 @@ def cpu_baseline(args, mult, nh, nw):
         t_fwd.append(t1 - t0)
         t_post.append(t2 - t1)
     fwd_by_threads = {share: med(t_fwd)}
-    if affinity > share:
+    # every affinity core too, unless the affinity set is far larger than the CPU share
+    # (the GPU box: 256 visible, 16 granted -- 256 torch threads there ran > 3 minutes)
+    oversubscribed = affinity > 2 * share
+    if share < affinity and not oversubscribed:
         torch.set_num_threads(affinity)
         t_all = []
         for i in range(min(3, args.cpu_frames)):
@@ -472,7 +476,9 @@ def cpu_baseline(args, mult, nh, nw):
             "fwd_s_by_threads": {str(k): round(v, 4) for k, v in fwd_by_threads.items()},
             "threads_basis": "forward timed with torch.set_num_threads(t) for t in {min(affinity, OMP_NUM_THREADS=%s), "
                              "len(sched_getaffinity)=%d}; the faster is used (cores). The post is numpy/scipy, one thread"
-                             % (omp or "unset", affinity),
+                             % (omp or "unset", affinity) +
+                             ("; all-affinity timing skipped: %d visible cores > 2x the %d-CPU share (oversubscribed)"
+                              % (affinity, share) if oversubscribed else ""),
             "sample": "%d frames %dx%d (scale %.2f, net %dx%d), median of frames 2..N: fwd %.3f s + post %.3f s per frame"
                       % (args.cpu_frames, args.height, args.width, args.scale, nh, nw,
                          fwd_by_threads[cores], med(t_post))}

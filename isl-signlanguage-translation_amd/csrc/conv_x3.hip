@@ -621,6 +621,30 @@ static bool x3_big_tiles(const ConvLaunch& c) {
   return (long long)c.n * px_tiles * ((c.cout + c.bco - 1) / c.bco) >= device_cus();
 }
 
+// 7x7 layers on 256-pixel tiles (8 waves of 64co x 64px, 156 KiB of LDS) or on
+// 128-pixel tiles (8 waves of 64co x 32px): one block per CU either way (a step's
+// weight slab is 56 KiB).  The 256-pixel block does twice the work for ~1.72x the
+// time of a 128-pixel block (half the weight bytes per MFMA), so the choice is per
+// launch, by grid quantisation: rounds of one block per CU, a 256-pixel block costing
+// X3_WIDE7_COST 128-pixel blocks (measured over 92^2 / 69^2 / 46x82 grids at batch
+// 13-64, tools/gpu_wide7.sh).  Both pack the weights for 128-channel tiles.
+constexpr double X3_WIDE7_COST = 1.74;
+
+static int x3_wide7_mode() {   // ISLPOSE_X3_WIDE7: 0 never, 1 always (A/B), default by the estimate
+  static const int m = getenv("ISLPOSE_X3_WIDE7") ? atoi(getenv("ISLPOSE_X3_WIDE7")) : 2;
+  return m;
+}
+
+static bool x3_wide7(const ConvLaunch& c) {
+  if (c.ks != 7 || c.bco != 128 || x3_small_tiles() || x3_canonical_ranges(c) > 1) return false;
+  const int mode = x3_wide7_mode();
+  if (mode != 2) return mode == 1;
+  const long long HW = (long long)c.H * c.W, co = (c.cout + 127) / 128, cus = device_cus();
+  const int t1 = tile_pixels(c, 128, x3_segmax(128)), t2 = tile_pixels(c, 256, x3_segmax(256));
+  const long long b1 = c.n * ((HW + t1 - 1) / t1) * co, b2 = c.n * ((HW + t2 - 1) / t2) * co;
+  return (double)((b2 + cus - 1) / cus) * X3_WIDE7_COST < (double)((b1 + cus - 1) / cus);
+}
+
 // Row-union staging (VAR 512) when the longest union run of any 512-pixel tile fits.
 // longest row-union run (pixels) over the 512-pixel tiles of a layer
 static int x3_union_run(const ConvLaunch& c) {
@@ -640,8 +664,9 @@ static bool x3_union(const ConvLaunch& c) {
 }
 
 // K-range plan of a launch on the 128-pixel family: S ranges, computed across S blocks
-// per tile (split-K, partials through the workspace) when the plain grid cannot
-// half-fill the CUs, else in one block.  With isl_net_set_split_k(net, 2) (latency
+// per tile (split-K, partials through the workspace) when the plain grid has fewer
+// blocks than CUs, else in one block (tools/gpu_across.sh: across wins 10-50 % at
+// 64-160 blocks, in-block wins 20-70 % at 256-1024 -- same bits either way).  With isl_net_set_split_k(net, 2) (latency
 // mode) layers without canonical ranges also split when their grid is that small --
 // an adaptive S that depends on the batch, so those layers' bits then do too.
 struct X3Ranges {
@@ -651,13 +676,14 @@ struct X3Ranges {
 
 static X3Ranges x3_ranges(const ConvLaunch& c) {
   X3Ranges r;
-  if (x3_big_tiles(c)) return r;
+  if (x3_big_tiles(c) || x3_wide7(c)) return r;
   const int tpx = tile_pixels(c, 128, x3_segmax(128));
   const long long blocks = (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * ((c.cout + c.bco - 1) / c.bco);
   const int cus = device_cus(), pairs = (c.cin_chunks + 1) / 2;
   r.S = x3_canonical_ranges(c);
   if (r.S > 1) {
-    r.across_blocks = 2 * blocks <= cus;
+    static const int force = getenv("ISLPOSE_X3_ACROSS") ? atoi(getenv("ISLPOSE_X3_ACROSS")) : -1;   // A/B
+    r.across_blocks = force >= 0 ? force == 1 : blocks < cus;
     return r;
   }
   if (c.allow_split == 2 && 2 * blocks <= cus && pairs >= 4) {
@@ -697,6 +723,15 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
       }
     }
   }
+  if constexpr (KS == 7) {
+    // 128-channel 7x7 tiles without K ranges: 8 waves of 64co x 64px on 256 pixels, or
+    // of 64co x 32px on 128 pixels (one block per CU either way: the 56 KiB weight
+    // slabs; 8 waves measured 2-6 % over 4 waves of 64co x 64px / x 128px)
+    if (c.ksplit <= 1 && c.bco == 128) {
+      if (x3_wide7(c)) return launch_t<KS, 2, 4, 2, 2, 0, 1>(c, s);
+      return launch_t<KS, 2, 4, 2, 1, 0, 1>(c, s);
+    }
+  }
   const bool ranged = c.ksplit > 1 && !c.ws;      // launch_conv_x3: in-block ranges
   const bool split = c.ksplit > 1 && c.ws;        // across blocks
   switch (c.bco) {
@@ -718,7 +753,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
 bool x3_fits(const ConvLaunch& c) { return c.in_pad >= c.ks / 2; }
 
 double conv_x3_mfma_flops(const ConvLaunch& c) {
-  const int BPX = x3_big_tiles(c) ? 512 : 128;
+  const int BPX = x3_big_tiles(c) ? 512 : x3_wide7(c) ? 256 : 128;
   const double co = (double)((c.cout + c.bco - 1) / c.bco) * c.bco;
   const double px = std::ceil((double)c.H * c.W / tile_pixels(c, BPX, x3_segmax(BPX))) * BPX;
   return 3.0 * 2.0 * co * (((c.cin_chunks + 1) / 2) * 16.0) * c.ks * c.ks * px * c.n;

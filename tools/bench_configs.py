@@ -151,7 +151,7 @@ def c5(args):
            "videos": len(rows), "batch": args.batch, "export": False,
            "decode": "frames already decoded in host memory (pims/ffmpeg absent); the pipeline reads them as "
                      "slices of the [T,H,W,3] array"}
-    for ov in (False, True):
+    for ov in ((True,) if args.c5_overlap_only else (False, True)):
         out = tempfile.mkdtemp(prefix="c5_")
         try:
             # warm-up (arenas, hand scales) on the first video, then the timed pass over all
@@ -218,6 +218,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c5-frames", type=int, default=96, help="C5: frames per (synthetic 1080p) video")
     ap.add_argument("--c5-videos", type=int, default=3)
+    ap.add_argument("--c5-overlap-only", action="store_true")
     ap.add_argument("--raw-hand-maps", dest="designed_hands", action="store_false",
                     help="C3: run the hand post on the raw net maps instead of designed maps")
     a = ap.parse_args()

@@ -70,6 +70,13 @@ int main(int argc, char** argv) {
   L.out = out.base; L.out_pad = pout; L.out_cs = cs_out; L.out_coff = 0;
   L.bias = bias; L.slope = slope; L.n = n; L.H = H; L.W = W; L.ks = ks; L.cin_chunks = chunks; L.cout = cout;
   L.act = ACT_PRELU; L.wx3 = wx; L.wscale_inv = 1.f / 16384.f; L.range_flag = flag;
+  // CONVBENCH_SPLIT=1|2: the net's K-range mode (canonical ranges / latency split), with a workspace
+  if (getenv("CONVBENCH_SPLIT")) {
+    L.allow_split = atoi(getenv("CONVBENCH_SPLIT"));
+    L.bco = bco;
+    L.ws_floats = x3_splitk_ws_floats(L);
+    if (L.ws_floats) CK(hipMalloc(&L.ws, L.ws_floats * sizeof(float)));
+  }
   // ISLPOSE_X3_UNION=4: s_memtime stamps of block 0 (16 waves x K steps x 4 points)
   const int T = pairs * ks;
   unsigned long long* dbg = nullptr;

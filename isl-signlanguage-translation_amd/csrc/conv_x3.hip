@@ -79,6 +79,7 @@ struct X3Args {
   int nfr;                      // frames (split-K partial-sum layout)
   float* ws;                    // split-K partial sums [ksplit][nfr][cout/8][H*W][8]
   unsigned long long* dbg;      // VAR 16384 (development): s_memtime stamps of block 0
+  int hpool;                    // ConvLaunch::hpool: out is the [n][chunk][H][W/2][8] pair-max buffer
 };
 
 // input segment capacity in pixels for a BPX-pixel tile (host: tile_pixels)
@@ -431,7 +432,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   // epilogue: x 2^-s, bias + activation, range check, masked float4 stores.  Bias and
   // PReLU slopes come from LDS (staged once), so no global load -- and no vmcnt(0)
   // behind the stores issued so far -- sits between the output stores.
-  const int Wo = a.W + 2 * a.out_pad;
+  const int Wo = a.hpool ? a.W / 2 : a.W + 2 * a.out_pad;
   float* out_f = a.out + (size_t)n * a.out_fs;
   bool bad = false;
   float* ebias = (float*)smem;                  // [BCO] bias, [BCO] slope
@@ -445,7 +446,8 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     const int m = m0 + (wave_n * WN + wn) * 32 + l32;
     if (m > mlast) continue;
     const int y = m / a.W, x = m - y * a.W;
-    float* op = out_f + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8;
+    float* op = a.hpool ? out_f + (size_t)(y * Wo + (x >> 1)) * 8
+                        : out_f + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8;
 #pragma unroll
     for (int wm = 0; wm < WM; ++wm) {
       const int cob = co_t * BCO + (wave_m * WM + wm) * 32 + 4 * h;
@@ -466,6 +468,14 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) bad |= !(__builtin_fabsf(v[e]) < 65504.f);
+        if (a.hpool) {
+          // pixels m, m+1 (x even, x+1: W even, tiles start on even pixels) sit in lanes
+          // l, l^1: take the pair's max, the even lane stores it
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = fmaxf(v[e], __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v[e]), 0xB1, 0xF, 0xF, false)));
+          if (x & 1) continue;
+        }
         float* oc = op + (size_t)(co >> 3) * a.out_chs + (co & 7);
         if (co + 3 < a.cout) {
           *(f32x4*)oc = v;
@@ -559,6 +569,16 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   a.nfr = c.n;
   a.ws = c.ws;
   a.dbg = c.dbg;
+  a.hpool = c.hpool;
+  if (c.hpool) {
+    if ((c.W & 1) || c.out_pad || c.out_coff || SPLIT) {
+      set_error("conv_x3: pair-max epilogue needs an even width, an unpadded output and no split-K");
+      return hipErrorInvalidValue;
+    }
+    a.out_chs = (long long)c.H * (c.W / 2) * 8;
+    a.out_fs = a.out_chs * (c.out_cs / 8);
+    a.out = c.out;
+  }
   const long long nb = (long long)c.n * a.px_tiles * a.co_tiles * (SPLIT ? a.ksplit : 1);
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
@@ -751,6 +771,10 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
 }
 
 bool x3_fits(const ConvLaunch& c) { return c.in_pad >= c.ks / 2; }
+
+bool x3_hpool_ok(const ConvLaunch& c) {
+  return x3_fits(c) && !(c.W & 1) && !(x3_ranges(c).S > 1 && x3_ranges(c).across_blocks);
+}
 
 double conv_x3_mfma_flops(const ConvLaunch& c) {
   const int BPX = x3_big_tiles(c) ? 512 : x3_wide7(c) ? 256 : 128;

@@ -47,6 +47,10 @@ struct ConvLaunch {
   int ksplit = 1;              // set by launch_conv_x3
   int allow_split = 0;         // the net's split-K switch (isl_net_set_split_k)
   unsigned long long* dbg = nullptr;   // development stamps (tools/convbench), never set by the runtime
+  // Half of a following 2x2 max-pool (conv_x3 only, even W): the epilogue writes the
+  // max of each horizontal pixel pair into `out` as an unpadded [n][chunk][H][W/2][8]
+  // buffer (out_pad 0); launch_vpool2 then takes the max of row pairs.
+  int hpool = 0;
 };
 
 // Pixels per tile of the flattened-raster conv kernels: BPX, or fewer when the
@@ -72,6 +76,8 @@ hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
 // launch_conv; x3_fits() says whether the input segment of a pixel tile fits.
 hipError_t launch_conv_x3(const ConvLaunch& c, hipStream_t s);
 bool x3_fits(const ConvLaunch& c);
+// whether launch_conv_x3 can run c with hpool (even W, not split across blocks)
+bool x3_hpool_ok(const ConvLaunch& c);
 double conv_x3_mfma_flops(const ConvLaunch& c);
 // floats of split-K workspace launch_conv_x3 would use for c (0 = no split)
 size_t x3_splitk_ws_floats(const ConvLaunch& c);
@@ -85,6 +91,9 @@ double conv_mfma_flops(const ConvLaunch& c);
 double wino_mfma_flops(const ConvLaunch& c);
 
 hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s);
+// second half of a fused 2x2 max-pool: row pairs of a horizontally pooled buffer
+// (ConvLaunch::hpool, [n][chunk][H][W/2][8]) into the padded next buffer
+hipError_t launch_vpool2(const Act& half, const Act& out, int C, hipStream_t s);
 hipError_t launch_pack_nchw(const float* x, int n, int C, int h, int w, const Act& out, hipStream_t s);
 hipError_t launch_unpack_nchw(const Act& in, int coff, int C, float* y, hipStream_t s);
 // Pre-processing of a batch of images described by a device table of entries

@@ -44,6 +44,41 @@ hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s) 
   return hipGetLastError();
 }
 
+// Second half of a fused 2x2 max-pool: the producing conv's epilogue already took the
+// max of each horizontal pixel pair (ConvLaunch::hpool) into an unpadded
+// [n][chunk][H][W/2][8] buffer; here each output pixel is the max of its two rows
+// (floor mode: an odd last row is dropped, as MaxPool2d(2, 2) does).  Reads half the
+// bytes maxpool2_kernel reads, and the conv wrote half the bytes.
+__global__ void vpool2_kernel(const float* __restrict__ in, int iH, int iW2, float* __restrict__ out, int op,
+                              int oH, int oW, int chunks, int in_chunks, int out_chunks) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= oH * oW * 2) return;
+  const int plane = blockIdx.y, f = plane / chunks, k = plane - f * chunks;
+  const int half = idx & 1, px = idx >> 1;
+  const int y = px / oW, x = px - y * oW;
+  const int oWp = oW + 2 * op;
+  const size_t ich = (size_t)iH * iW2 * 8, och = (size_t)(oH + 2 * op) * oWp * 8;
+  const float* p = in + ((size_t)f * in_chunks + k) * ich + (size_t)(2 * y * iW2 + x) * 8 + 4 * half;
+  const f32x4 a = *(const f32x4*)p, c = *(const f32x4*)(p + (size_t)iW2 * 8);
+  f32x4 m;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) m[e] = fmaxf(a[e], c[e]);
+  *(f32x4*)(out + ((size_t)f * out_chunks + k) * och + (size_t)((y + op) * oWp + x + op) * 8 + 4 * half) = m;
+}
+
+hipError_t launch_vpool2(const Act& in, const Act& out, int C, hipStream_t s) {
+  const int chunks = (C + 7) / 8;
+  const long long per_plane = (long long)out.H * out.W * 2;
+  if (per_plane > 0x7fffffffLL || (long long)out.n * chunks > 65535 || in.pad != 0 || out.W != in.W ||
+      out.H != in.H / 2) {
+    set_error("vpool2: bad geometry");
+    return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(vpool2_kernel, dim3((unsigned)((per_plane + 255) / 256), out.n * chunks), dim3(256), 0, s,
+                     in.base, in.H, in.W, out.base, out.pad, out.H, out.W, chunks, in.cs / 8, out.cs / 8);
+  return hipGetLastError();
+}
+
 // NCHW float (module seam input) -> chunked padded buffer, channels >= C zero-filled.
 __global__ void pack_nchw_kernel(const float* __restrict__ x, int n, int C, int h, int w,
                                  float* __restrict__ out, int op, int ocs) {

@@ -167,12 +167,14 @@ static std::vector<ConvLayer> hand_layers() {  // model.py:331-392
 
 struct BufSpec {
   int level, cs, pad;
+  int half = 0;   // W/2 wide (the pair-max buffer of a fused pool, ConvLaunch::hpool)
 };
 
 struct Op {
   int type;  // 0 conv, 1 maxpool
   int layer;
   int in, in_coff, out, out_coff, C;
+  int hbuf = -1;  // maxpool: the pair-max buffer its producing conv may write instead of `in`
 };
 
 struct OutRef {
@@ -239,8 +241,8 @@ static int round8(int c) { return (c + 7) / 8 * 8; }
 
 struct Builder {
   isl_net* net;
-  int buf(int level, int cs, int pad) {
-    net->bufs.push_back({level, cs, pad});
+  int buf(int level, int cs, int pad, int half = 0) {
+    net->bufs.push_back({level, cs, pad, half});
     return (int)net->bufs.size() - 1;
   }
   int L(const std::string& name) {
@@ -264,7 +266,13 @@ struct Builder {
     c.wbco = c.k == 3 ? wino_bco_for(c.cout) : 0;
     net->ops.push_back({0, li, in, in_coff, out, out_coff, 0});
   }
-  void pool(int in, int out, int C) { net->ops.push_back({1, -1, in, 0, out, 0, C}); }
+  // 2x2 max-pool of `in` (channels [0, C)) into `out`; when the producing conv can (x3,
+  // even width) it writes pair maxima into a separate half-width buffer instead and
+  // the pool takes the row pairs (run_ops)
+  void pool(int in, int out, int C) {
+    const int hb = buf(net->bufs[in].level, net->bufs[in].cs, 0, 1);
+    net->ops.push_back({1, -1, in, 0, out, 0, C, hb});
+  }
 
   // shared VGG front; returns the level-3 buffer written by the last front conv
   void front(int X, bool hand, int out_buf, int out_coff, int pad3) {
@@ -616,7 +624,7 @@ static int plan(isl_net* net, int n, int h, int w) {
     ar.n_cap = n;
     for (const BufSpec& b : net->bufs) {
       Act a;
-      a.n = n; a.H = lh0[b.level]; a.W = lw0[b.level]; a.pad = b.pad; a.cs = b.cs;
+      a.n = n; a.H = lh0[b.level]; a.W = b.half ? lw0[b.level] / 2 : lw0[b.level]; a.pad = b.pad; a.cs = b.cs;
       ar.offs.push_back(ar.bytes);
       ar.bytes += (a.bytes() + 255) / 256 * 256;
     }
@@ -640,7 +648,7 @@ static int plan(isl_net* net, int n, int h, int w) {
   for (size_t i = 0; i < net->bufs.size(); ++i) {
     const BufSpec& b = net->bufs[i];
     Act& a = net->act[i];
-    a.n = n; a.H = lh[b.level]; a.W = lw[b.level]; a.pad = b.pad; a.cs = b.cs;
+    a.n = n; a.H = lh[b.level]; a.W = b.half ? lw[b.level] / 2 : lw[b.level]; a.pad = b.pad; a.cs = b.cs;
     a.base = (float*)((char*)ar.base + ar.offs[i]);
   }
   net->arena = ar.base;
@@ -669,6 +677,13 @@ static bool x3_wino_enabled() {
   return on;
 }
 
+// ISLPOSE_FUSED_POOL=0: the plain conv + maxpool2 path (A/B; read per run, so a test
+// can compare both in one process)
+static bool fused_pool_enabled() {
+  const char* e = getenv("ISLPOSE_FUSED_POOL");
+  return !(e && e[0] == '0');
+}
+
 static int run_ops(isl_net* net, hipStream_t s) {
   isl_net::TimedRun* tr = nullptr;
   if (net->timing) {
@@ -678,12 +693,16 @@ static int run_ops(isl_net* net, hipStream_t s) {
     for (hipEvent_t& e : tr->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipEventRecord(tr->ev[0], s));
   }
+  bool fused = false;   // the previous conv wrote the pair-max buffer of this pool
+  const bool fuse_pools = fused_pool_enabled();
   for (size_t k = 0; k < net->ops.size(); ++k) {
     const Op& op = net->ops[k];
     const Act& in = net->act[op.in];
     const Act& out = net->act[op.out];
     if (op.type == 1) {
-      HIP_OK(launch_maxpool2(in, out, op.C, s));
+      if (fused) HIP_OK(launch_vpool2(net->act[op.hbuf], out, op.C, s));
+      else HIP_OK(launch_maxpool2(in, out, op.C, s));
+      fused = false;
       if (tr) {
         tr->kind.push_back(0); tr->flops.push_back(0.0); tr->mfma_flops.push_back(0.0);
         HIP_OK(hipEventRecord(tr->ev[k + 1], s));
@@ -710,6 +729,14 @@ static int run_ops(isl_net* net, hipStream_t s) {
       kind = 4; mf = wino_x3_mfma_flops(L);
     } else if (net->algo == ISL_ALGO_X3 && x3_fits(L)) {
       L.allow_split = net->split_k;
+      // the next op pools this conv's output: write pair maxima to its half-width buffer
+      if (k + 1 < net->ops.size() && net->ops[k + 1].type == 1 && net->ops[k + 1].in == op.out && op.out_coff == 0 &&
+          net->ops[k + 1].C == c.cout && fuse_pools && x3_hpool_ok(L)) {
+        const Act& hb = net->act[net->ops[k + 1].hbuf];
+        L.out = hb.base; L.out_pad = 0; L.out_cs = hb.cs; L.out_coff = 0;
+        L.hpool = 1;
+        fused = true;
+      }
       const size_t need = x3_splitk_ws_floats(L);
       if (need > net->ks_floats) {
         // grow-only; hipFree waits for the queued work that may still read the old one

@@ -63,6 +63,19 @@ def test_body25_forward_algo_vs_oracle(net25, w25, algo):
     assert ep < TOL and eh < TOL, (ep, eh)
 
 
+@pytest.mark.parametrize("n,h,w", [(2, 184, 328), (1, 368, 656), (2, 50, 70), (3, 96, 136)])
+def test_fused_pool_bit_identical(net25, n, h, w, monkeypatch):
+    """conv1_2 / conv2_2 / conv3_4 writing horizontal pair maxima (ConvLaunch::hpool) +
+    the row-pair pool == conv + maxpool2, bit for bit (max is exact); odd widths
+    (50x70's 25x35 level) take the plain path."""
+    x = torch.from_numpy(_inputs(n, h, w, seed=h + w)).cuda()
+    paf0, heat0 = net25.forward(x)
+    monkeypatch.setenv("ISLPOSE_FUSED_POOL", "0")
+    paf1, heat1 = net25.forward(x)
+    torch.cuda.synchronize()
+    assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
+
+
 def test_body25_forward_lds_dma_staging(net25, w25, monkeypatch):
     """The LDS-DMA staging variant of the conv kernel gives the same results."""
     x = torch.from_numpy(_inputs(2, 50, 70, seed=9)).cuda()

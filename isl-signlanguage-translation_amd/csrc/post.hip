@@ -261,6 +261,8 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
   __shared__ float s_low[FUSED ? NMS_SRC_ROWS : 1][FUSED ? NMS_SRC_COLS : 1];
   __shared__ float4 s_tb[FUSED ? NMS_IR : 1];
   __shared__ int s_live;
+  __shared__ double s_cmax[NMS_VC];   // max |in| of every window column (word liveness)
+  __shared__ int s_wlive[3];
   double (*s_g)[NMS_VC] = s_v;
   const int y0 = by * NMS_TY, x0 = bx * NMS_TX;
   const int tid = threadIdx.x;
@@ -279,6 +281,7 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
         in[r] = (double)src[(size_t)reflect_idx(y0 - 1 - NMS_R + r, H) * W + xx];
         amax = fmax(amax, fabs(in[r]));
       }
+      s_cmax[tid] = amax;
       // Early out, exact: every g of the tile is a positive-weight average (weights sum
       // to 1) of these inputs, so |g| <= max|in| * (1 + 1e-13) in fp64.  When that stays
       // below the threshold no pixel can pass `g > thre` and the tile's mask is zero.
@@ -344,6 +347,7 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
         in[r] = (double)v;
         vmax = fmax(vmax, fabs(in[r]));
       }
+      s_cmax[tid] = vmax;
       if (vmax >= thre * (1.0 - 1e-9)) s_live = 1;   // the exact blur bound, as unfused
     }
     __syncthreads();
@@ -355,7 +359,22 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
     }
     return;
   }
-  if (tid < NMS_VC) {
+  // Word liveness, the same exact bound per 64-column mask word: word w's outputs (tile
+  // columns 64w..64w+63) read g on columns 64w..64w+65 (NMS ring), i.e. window columns
+  // 64w..64w+89 of every input row; when those stay below the threshold the word is
+  // zero and neither its vertical nor its horizontal pass runs.
+  if (tid < 3) {
+    double mx = 0.0;
+    for (int t = 64 * tid; t <= 64 * tid + 89 && t < NMS_VC; ++t) mx = fmax(mx, s_cmax[t]);
+    s_wlive[tid] = mx >= thre * (1.0 - 1e-9);
+  }
+  __syncthreads();
+  const bool wl0 = s_wlive[0], wl1 = s_wlive[1], wl2 = s_wlive[2];
+  // window column t is needed by a live word
+  auto col_needed = [&](int t) {
+    return (wl0 && t <= 89) || (wl1 && t >= 64 && t <= 153) || (wl2 && t >= 128);
+  };
+  if (tid < NMS_VC && col_needed(tid)) {
 #pragma unroll
     for (int r = 0; r < NMS_VR; ++r) {
       double o = in[r + NMS_R] * kGauss[0];
@@ -368,8 +387,12 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
   // axis 1, same recurrence along the row
   {
     constexpr int SEGS = (NMS_GC + NMS_SEG - 1) / NMS_SEG;   // 14 runs per row, 252 threads
-    const bool act = tid < NMS_VR * SEGS;
     const int r = tid / SEGS, c0 = (tid - r * SEGS) * NMS_SEG;
+    // g columns c0..c0+13 overlap a live word's g range [64w, 64w+65]; the run's other
+    // columns may read v never computed -- their g is never read
+    const int c1 = c0 + NMS_SEG - 1;
+    const bool act = tid < NMS_VR * SEGS &&
+                     ((wl0 && c0 <= 65) || (wl1 && c1 >= 64 && c0 <= 129) || (wl2 && c1 >= 128));
     double v[NMS_SEG + 2 * NMS_R];
     if (act) {
 #pragma unroll
@@ -392,7 +415,7 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
     const int ty = it / 3, wd = it - ty * 3;
     const int y = y0 + ty, cx = wd * 64 + lane, x = x0 + cx;
     bool pk = false;
-    if (y < H && x < W) {
+    if (y < H && x < W && s_wlive[wd]) {
       const double g = s_g[ty + 1][cx + 1];
       if (mode_hand) {
         pk = g > thre;                                  // hand.py:62 binary map
@@ -1482,6 +1505,7 @@ __global__ void init_records_kernel(char* result, isl_layout lay, int n, int nli
 // ---------------------------------------------------------------------------
 
 static inline long long al8(long long x) { return (x + 7) / 8 * 8; }
+
 
 }  // namespace isl
 

@@ -96,11 +96,15 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr int BPX = WAVES_N * WN * 32;
   constexpr int P = KS / 2;
   constexpr int SEGMAX = x3_segmax(BPX);
-  constexpr int WSLAB = KS * 2 * 2 * BCO;        // 16-byte units: [kx][hi|lo][h][BCO]
+  // VAR 4096 (1x1 layers, 256-channel tiles): two chunk pairs per K step
+  constexpr int PPS = (VAR & 4096) ? 2 : 1;
+  static_assert(PPS == 1 || KS == 1, "two pairs per step: 1x1 layers only");
+  constexpr int WSLAB1 = KS * 2 * 2 * BCO;       // one pair: [kx][hi|lo][h][BCO]
+  constexpr int WSLAB = PPS * WSLAB1;            // 16-byte units per step
   constexpr int SEGP = SEGMAX + 1;               // + one dummy slot idle staging items write to
-  constexpr int XSLAB = 2 * 2 * SEGP;            // 16-byte units: [hi|lo][h][px]
+  constexpr int XSLAB = 2 * 2 * PPS * SEGP;      // 16-byte units: [hi|lo][chunk of the step][px]
   constexpr int BUF = WSLAB + XSLAB;
-  constexpr int IT = (2 * SEGMAX + NT - 1) / NT; // staging items (h, px) per thread
+  constexpr int IT = (2 * PPS * SEGMAX + NT - 1) / NT; // staging items (chunk, px) per thread
   static_assert(WSLAB % 64 == 0, "weight slab is whole 1 KiB DMA pieces");
   static_assert(BPX <= SEGMAX, "segment must hold a tile");
   constexpr bool UNION = (VAR & 512) != 0;
@@ -112,6 +116,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr bool SPLIT = (VAR & 2048) != 0;
   constexpr bool STAMP = (VAR & 16384) != 0;
   static_assert(!(UNION && (RANGED || SPLIT)), "K ranges run on the generic loop");
+  static_assert(PPS == 1 || !(UNION || RANGED || SPLIT), "two pairs per step: plain generic loop only");
   __shared__ f16x8 smem[SMEM];
 
   // XCD-aware tile order (conv.hip): co-tiles of a pixel tile, then neighbouring
@@ -156,7 +161,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     rel[wn] = (y + a.in_pad) * Wi + x + a.in_pad - La;
   }
 
-  const int T = a.pairs * KS;
+  const int T = a.pairs / PPS * KS;              // K steps (PPS == 2: the host checks pairs is even)
 
   f32x16 acc[WM][WN];
 #pragma unroll
@@ -298,13 +303,13 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   } else {
     // Generic loop: one step = (pair, ky); weights by LDS-DMA one step ahead, the
     // input row run register-staged one step ahead.
-    int ih[IT], ipx[IT];                 // staging items: tid + i*NT -> (chunk half, pixel)
+    int ih[IT], ipx[IT];                 // staging items: tid + i*NT -> (chunk of the step, pixel)
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
       const int it = tid + i * NT;
-      ih[i] = it >= seg ? 1 : 0;
+      ih[i] = min(it / seg, 2 * PPS - 1);
       ipx[i] = it - ih[i] * seg;
-      if (it >= 2 * seg) ipx[i] = -1;   // idle
+      if (it >= 2 * PPS * seg) ipx[i] = -1;   // idle
     }
     f32x4 raw[IT][2];
     auto load_x = [&](int t) __attribute__((always_inline)) {
@@ -312,7 +317,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       const long long row = (long long)(La + (ky - P) * Wi - P);
 #pragma unroll
       for (int i = 0; i < IT; ++i) {
-        const int c = 2 * c2 + ih[i];
+        const int c = 2 * PPS * c2 + ih[i];
         if (ipx[i] >= 0 && c < a.cin_chunks) {
           const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + ipx[i]) * 8;
           raw[i][0] = *(const f32x4*)src;
@@ -335,8 +340,8 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
           hi[j] = (_Float16)x;
           lo[j] = (_Float16)(x - (float)hi[j]);
         }
-        s[(0 * 2 + ih[i]) * SEGP + ipx[i]] = hi;
-        s[(1 * 2 + ih[i]) * SEGP + ipx[i]] = lo;
+        s[(0 * 2 * PPS + ih[i]) * SEGP + ipx[i]] = hi;
+        s[(1 * 2 * PPS + ih[i]) * SEGP + ipx[i]] = lo;
       }
     };
     auto issue_w = [&](int t, int buf) __attribute__((always_inline)) {
@@ -351,10 +356,13 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       }
     };
     auto compute = [&](int buf) __attribute__((always_inline)) {
-      const f16x8* sw = smem + buf * BUF + h * BCO + wave_m * WM * 32 + l32;
-      const f16x8* sx = smem + buf * BUF + WSLAB + h * SEGP;
 #pragma unroll
-      for (int kx = 0; kx < KS; ++kx) tap(sw, sx, SEGP, kx);
+      for (int pp = 0; pp < PPS; ++pp) {
+        const f16x8* sw = smem + buf * BUF + pp * WSLAB1 + h * BCO + wave_m * WM * 32 + l32;
+        const f16x8* sx = smem + buf * BUF + WSLAB + (2 * pp + h) * SEGP;
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) tap(sw, sx, PPS * SEGP, kx);
+      }
     };
     // K ranges: [t0, t1) of this block (SPLIT: one range), range length R steps
     int t0 = 0, t1 = T, R = T;
@@ -549,6 +557,7 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   if ((SPLIT || RANGED) && c.ksplit < 2) { set_error("conv_x3: K ranges without a range count"); return hipErrorInvalidValue; }
   if (SPLIT && !c.ws) { set_error("conv_x3: split-K without workspace"); return hipErrorInvalidValue; }
   if ((VAR & 16384) && !c.dbg) { set_error("conv_x3: stamp build without a stamp buffer"); return hipErrorInvalidValue; }
+  if ((VAR & 4096) && ((c.cin_chunks + 1) / 2) % 2) { set_error("conv_x3: two pairs per step needs an even pair count"); return hipErrorInvalidValue; }
   X3Args a;
   a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
   a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
@@ -635,10 +644,28 @@ static int x3_canonical_ranges(const ConvLaunch& c) {
 // family's register budget).  512-pixel tiles are used only when they fill the
 // chip: a layer with fewer such blocks than CUs runs ~2x faster on the 128-pixel,
 // 4-wave family (tools/gpu_tiles.sh).
+static int x3_big_bpx(const ConvLaunch& c) { return c.ks == 1 && c.bco == 256 ? 256 : 512; }
+
 static bool x3_big_tiles(const ConvLaunch& c) {
   if (c.ks > 3 || x3_small_tiles() || x3_canonical_ranges(c) > 1) return false;
-  const long long px_tiles = (c.H * c.W + tile_pixels(c, 512, x3_segmax(512)) - 1) / tile_pixels(c, 512, x3_segmax(512));
+  const int bpx = x3_big_bpx(c), tpx = tile_pixels(c, bpx, x3_segmax(bpx));
+  const long long px_tiles = (c.H * c.W + tpx - 1) / tpx;
   return (long long)c.n * px_tiles * ((c.cout + c.bco - 1) / c.bco) >= device_cus();
+}
+
+// 1x1 layers with 256k output channels and an even number of chunk pairs (Mconv6 of
+// every stage: 384/288 -> 512/256) also pack their split filters for 256-channel
+// tiles.  On big grids they run 16 waves of 64co x 64px over 256 pixels with two chunk
+// pairs per K step (VAR 4096: 24 MFMAs per wave between barriers instead of 12, and
+// the input read for half as many channel tiles): +7-12 % (tools/gpu_k1.sh).  Small
+// grids (K ranges, the 128-pixel family) keep the 128-channel packing: 256-channel
+// tiles there halve the blocks and lost 30 %.
+bool x3_wide1_layer(int ks, int cout, int cin_phys) {
+  return ks == 1 && cout % 256 == 0 && ((cin_phys / 8 + 1) / 2) % 2 == 0;
+}
+
+bool x3_wide1(const ConvLaunch& c) {
+  return c.bco == 256 && x3_wide1_layer(c.ks, c.cout, c.cin_chunks * 8) && x3_big_tiles(c);
 }
 
 // 7x7 layers on 256-pixel tiles (8 waves of 64co x 64px, 156 KiB of LDS) or on
@@ -733,6 +760,9 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
       }
     }
   }
+  if constexpr (KS == 1) {
+    if (c.bco == 256 && x3_big_tiles(c)) return launch_t<KS, 4, 4, 2, 2, 4096, 1>(c, s);
+  }
   if constexpr (KS <= 3) {
     if (x3_big_tiles(c)) {
       switch (c.bco) {
@@ -777,7 +807,7 @@ bool x3_hpool_ok(const ConvLaunch& c) {
 }
 
 double conv_x3_mfma_flops(const ConvLaunch& c) {
-  const int BPX = x3_big_tiles(c) ? 512 : x3_wide7(c) ? 256 : 128;
+  const int BPX = x3_big_tiles(c) ? x3_big_bpx(c) : x3_wide7(c) ? 256 : 128;
   const double co = (double)((c.cout + c.bco - 1) / c.bco) * c.bco;
   const double px = std::ceil((double)c.H * c.W / tile_pixels(c, BPX, x3_segmax(BPX))) * BPX;
   return 3.0 * 2.0 * co * (((c.cin_chunks + 1) / 2) * 16.0) * c.ks * c.ks * px * c.n;

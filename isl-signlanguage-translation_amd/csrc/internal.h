@@ -74,6 +74,10 @@ int wino_bco_for(int cout);
 hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
 // Split-fp16 (3 x fp16 MFMA = fp32-accurate) direct convolution: same tiles as
 // launch_conv; x3_fits() says whether the input segment of a pixel tile fits.
+// 1x1 layers with x3_wide1_layer() also carry filters packed for 256-channel tiles,
+// used for a launch when x3_wide1(c with bco 256) says its grid is big enough.
+bool x3_wide1_layer(int ks, int cout, int cin_phys);
+bool x3_wide1(const ConvLaunch& c);
 hipError_t launch_conv_x3(const ConvLaunch& c, hipStream_t s);
 bool x3_fits(const ConvLaunch& c);
 // whether launch_conv_x3 can run c with hpool (even W, not split across blocks)

@@ -54,10 +54,12 @@ struct ConvLayer {
   bool has_w = false, has_b = false, has_s = false;
   std::vector<Seg> cmap;
   int cin_phys = 0, bco = 0;
+  bool x3_wide = false;          // 1x1 layer with a second split-fp16 packing for 256-channel tiles
   int wbco = 0;                  // Winograd tile (3x3 layers), 0 = direct only
   float *d_w = nullptr, *d_b = nullptr, *d_s = nullptr;
   float* d_wu = nullptr;         // Winograd-transformed filters
-  void* d_wx3 = nullptr;         // split-fp16 filters (conv_x3.hip)
+  void* d_wx3 = nullptr;         // split-fp16 filters (conv_x3.hip), tiles of bco channels
+  void* d_wx3w = nullptr;        // the same for 256-channel tiles (x3_wide layers; per launch, x3_wide1)
   float x3_inv = 1.f;            // 2^-s of the split weights
   void* d_wux3 = nullptr;        // split-fp16 Winograd filters (wino_x3.hip), 3x3 only
   float wx3_inv = 1.f;
@@ -263,6 +265,7 @@ struct Builder {
     c.cmap = cmap;
     c.cin_phys = cin_phys;
     c.bco = conv_bco_for(c.cout);
+    c.x3_wide = x3_wide1_layer(c.k, c.cout, c.cin_phys);
     c.wbco = c.k == 3 ? wino_bco_for(c.cout) : 0;
     net->ops.push_back({0, li, in, in_coff, out, out_coff, 0});
   }
@@ -456,8 +459,8 @@ static std::vector<float> pack_wino(const ConvLayer& c) {
 // Split-fp16 filters for conv_x3.hip: w * 2^s = hi + lo (both fp16, round to
 // nearest), 2^s chosen per layer so that max|w| * 2^s lies in [2^13, 2^14);
 // layout [co_tile][chunk pair][ky][kx][hi|lo][h][BCO][8], h = chunk of the pair.
-static std::vector<_Float16> pack_x3(const ConvLayer& c, float* inv_scale) {
-  const int ks = c.k, bco = c.bco, chunks = c.cin_phys / 8, pairs = (chunks + 1) / 2;
+static std::vector<_Float16> pack_x3(const ConvLayer& c, int bco, float* inv_scale) {
+  const int ks = c.k, chunks = c.cin_phys / 8, pairs = (chunks + 1) / 2;
   const int co_tiles = (c.cout + bco - 1) / bco;
   std::vector<int> p2l(pairs * 16, -1);
   for (const Seg& s : c.cmap)
@@ -547,8 +550,9 @@ static int upload_params(isl_net* net) {
     if (!c.has_w || !c.has_b || (c.act == ACT_PRELU && !c.has_s))
       return fail(ISL_E_STATE, "parameter missing for layer " + c.name);
     std::vector<float> wp = pack_weights(c);
-    const int co_tiles = (c.cout + c.bco - 1) / c.bco;
-    std::vector<float> bp((size_t)co_tiles * c.bco, 0.f), sp((size_t)co_tiles * c.bco, 0.f);
+    // bias / slopes padded for every tile width (c.bco; 256 for x3_wide layers)
+    const int wpad = std::max((c.cout + c.bco - 1) / c.bco * c.bco, (c.cout + 255) / 256 * 256);
+    std::vector<float> bp((size_t)wpad, 0.f), sp((size_t)wpad, 0.f);
     std::copy(c.b.begin(), c.b.end(), bp.begin());
     if (c.act == ACT_PRELU) std::copy(c.s.begin(), c.s.end(), sp.begin());
     if (!c.d_w) HIP_OK(hipMalloc(&c.d_w, wp.size() * sizeof(float)));
@@ -558,9 +562,15 @@ static int upload_params(isl_net* net) {
     HIP_OK(hipMemcpy(c.d_b, bp.data(), bp.size() * sizeof(float), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(c.d_s, sp.data(), sp.size() * sizeof(float), hipMemcpyHostToDevice));
     {
-      std::vector<_Float16> xp = pack_x3(c, &c.x3_inv);
+      std::vector<_Float16> xp = pack_x3(c, c.bco, &c.x3_inv);
       if (!c.d_wx3) HIP_OK(hipMalloc(&c.d_wx3, xp.size() * sizeof(_Float16)));
       HIP_OK(hipMemcpy(c.d_wx3, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
+    if (c.x3_wide) {
+      float inv = 1.f;
+      std::vector<_Float16> xp = pack_x3(c, 256, &inv);
+      if (!c.d_wx3w) HIP_OK(hipMalloc(&c.d_wx3w, xp.size() * sizeof(_Float16)));
+      HIP_OK(hipMemcpy(c.d_wx3w, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
     if (c.k == 3 && c.cout % 4 == 0) {
       std::vector<_Float16> up = pack_wino_x3(c, &c.wx3_inv);
@@ -729,6 +739,11 @@ static int run_ops(isl_net* net, hipStream_t s) {
       kind = 4; mf = wino_x3_mfma_flops(L);
     } else if (net->algo == ISL_ALGO_X3 && x3_fits(L)) {
       L.allow_split = net->split_k;
+      if (c.x3_wide) {   // 256-channel tiles, two pairs per step, where the grid is big enough
+        ConvLaunch Lw = L;
+        Lw.bco = 256;
+        if (x3_wide1(Lw)) { L.bco = 256; L.wx3 = c.d_wx3w; }
+      }
       // the next op pools this conv's output: write pair maxima to its half-width buffer
       if (k + 1 < net->ops.size() && net->ops[k + 1].type == 1 && net->ops[k + 1].in == op.out && op.out_coff == 0 &&
           net->ops[k + 1].C == c.cout && fuse_pools && x3_hpool_ok(L)) {
@@ -844,6 +859,7 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_s) (void)hipFree(c.d_s);
     if (c.d_wu) (void)hipFree(c.d_wu);
     if (c.d_wx3) (void)hipFree(c.d_wx3);
+    if (c.d_wx3w) (void)hipFree(c.d_wx3w);
     if (c.d_wux3) (void)hipFree(c.d_wux3);
   }
   if (net->d_flag) (void)hipFree(net->d_flag);

@@ -60,8 +60,8 @@ int main(int argc, char** argv) {
   float* wu = wb ? dev_random<float>((size_t)(cout / wb) * chunks * 16 * 2 * wb * 4, -0.05f, 0.05f, 4) : nullptr;
   const int wxt = (cout + 63) / 64;
   _Float16* wux = dev_random<_Float16>((size_t)wxt * pairs * 16 * 4 * 64 * 8, -8192.f, 8192.f, 7);
-  float* bias = dev_random<float>(co_tiles * 128 + 128, -0.05f, 0.05f, 5);
-  float* slope = dev_random<float>(co_tiles * 128 + 128, 0.05f, 0.25f, 6);
+  float* bias = dev_random<float>(co_tiles * 256 + 256, -0.05f, 0.05f, 5);
+  float* slope = dev_random<float>(co_tiles * 256 + 256, 0.05f, 0.25f, 6);
   int* flag;
   CK(hipMalloc(&flag, 4));
   CK(hipMemset(flag, 0, 4));

@@ -124,28 +124,42 @@ class BodyEstimator:
                 raise rt.IslError("body post: frame %d status %d" % (f, st))
         return need
 
-    def decode(self, host, lay, caps, n):
+    def decode(self, host, lay, caps, n, details=True):
+        """Per-frame result records -> FrameResult.  candidate rows are the peaks of parts
+        0..nparts-1 in order, ids consecutive (body.py:101-107, 183); all_peaks,
+        connection_all and special_k are built only with details (the reference's
+        __call__ returns candidate and subset)."""
         out = []
         nparts, nl = self.njoint - 1, NLIMBS[self.kind]
         mpk, mcn, rw = caps["max_peaks"], caps["max_conns"], self.njoint + 1
+        slot = np.arange(mpk)
         for f in range(n):
             rec = host[f * lay.record_bytes:(f + 1) * lay.record_bytes]
             npk = rec[lay.n_peaks:lay.n_peaks + 128].view(np.int32)[:nparts]
-            ncn = rec[lay.n_conns:lay.n_conns + 128].view(np.int32)[:nl]
             nrows = int(rec[lay.n_rows:lay.n_rows + 4].view(np.int32)[0])
             pk = rec[lay.peaks:lay.peaks + nparts * mpk * 24].view(np.float64).reshape(nparts, mpk, 3)
-            cn = rec[lay.conns:lay.conns + nl * mcn * 40].view(np.float64).reshape(nl, mcn, 5)
+            sel = pk[slot[None, :] < npk[:, None]]               # [N, 3] (x, y, score), part-major
+            if len(sel):
+                candidate = np.empty((len(sel), 4), np.float64)
+                candidate[:, :3] = sel
+                candidate[:, 3] = np.arange(len(sel), dtype=np.float64)
+            else:
+                candidate = np.array([])
             sb = rec[lay.subset:lay.subset + caps["max_rows"] * rw * 8].view(np.float64).reshape(-1, rw)
-            all_peaks, rows, pid = [], [], 0
+            subset = sb[:nrows].copy()
+            if not details:
+                out.append(FrameResult(candidate, subset, None, None, None))
+                continue
+            ncn = rec[lay.n_conns:lay.n_conns + 128].view(np.int32)[:nl]
+            cn = rec[lay.conns:lay.conns + nl * mcn * 40].view(np.float64).reshape(nl, mcn, 5)
+            all_peaks, pid = [], 0
             for p in range(nparts):
                 lst = []
                 for i in range(int(npk[p])):
-                    x, y, s = pk[p, i]
-                    lst.append((np.int64(x), np.int64(y), np.float64(s), pid))
-                    rows.append((x, y, s, float(pid)))
+                    x, y, sc = pk[p, i]
+                    lst.append((np.int64(x), np.int64(y), np.float64(sc), pid))
                     pid += 1
                 all_peaks.append(lst)
-            candidate = np.array(rows, np.float64) if rows else np.array([])
             conn_all, special = [], []
             for k in range(nl):
                 if ncn[k] < 0:
@@ -153,7 +167,6 @@ class BodyEstimator:
                     conn_all.append([])
                 else:
                     conn_all.append(cn[k, :ncn[k]].copy())
-            subset = sb[:nrows].copy()
             out.append(FrameResult(candidate, subset, all_peaks, conn_all, special))
         return out
 
@@ -173,7 +186,7 @@ class BodyEstimator:
             with self.net.algo_scope("direct"):
                 geoms, pafs, heats = self.run_scales(t)
                 host, lay, caps = self.post(n, H, W, geoms, pafs, heats)
-        res = self.decode(host, lay, caps, n)
+        res = self.decode(host, lay, caps, n, details)
         if details:
             return res
         out = [(r.candidate, r.subset) for r in res]
@@ -183,5 +196,5 @@ class BodyEstimator:
         """Post-processing only, on caller low-res maps (NCHW cuda tensors per scale)."""
         n = pafs[0].shape[0]
         host, lay, caps = self.post(n, H, W, geoms, pafs, heats)
-        res = self.decode(host, lay, caps, n)
+        res = self.decode(host, lay, caps, n, details)
         return res if details else [(r.candidate, r.subset) for r in res]

@@ -49,7 +49,10 @@
 //         (x3_canonical_ranges), so a frame gives the same bits at any batch size
 //         whether its ranges ran in one block (large grids) or across blocks (small
 //         grids: batch-1 frames).
+//   4096  two chunk pairs per K step (1x1 layers on 256-channel tiles, x3_wide1);
 //   16384 development only: s_memtime stamps of the union loop (tools/convbench).
+// conv_x3_rgb: the 3-channel first layers (conv1_1) with K packed as the 27 real
+// (ky, kx, c) values instead of 9 taps x 16 channels.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -496,6 +499,168 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     }
   }
   if (bad) atomicOr(a.range_flag, 1);
+}
+
+// ---------------------------------------------------------------------------
+// conv1_1 of every net: 3 input channels, 3x3, 64 outputs.  Through the generic
+// kernel a pixel costs 9 pair-taps of K = 16 for 27 real products (5.3x the work);
+// here K is the 27 real (ky, kx, c) values padded to 32 -- two MFMA K-steps --
+// from an im2col tile of 512 pixels x 32 k in LDS (fp16 hi | lo, 64 KiB), built
+// straight from the padded input.  Weights [kk][hi|lo][h][64][8], k = 16 kk + 8 h
+// + j = 9 ky + 3 kx + c (host: pack_x3_rgb), scaled by 2^s as pack_x3.  The layer
+// is then bound by its 64-channel fp32 output write.  8 waves, 64co x 64px each.
+// ---------------------------------------------------------------------------
+constexpr int RGB_BPX = 512, RGB_BCO = 64, RGB_NT = 512;
+
+__global__ void __launch_bounds__(RGB_NT, 1) conv_x3_rgb(X3Args a) {
+  __shared__ f16x8 s_x[2][4][RGB_BPX];          // [hi|lo][k chunk q][px]
+  __shared__ f16x8 s_w[2][2][2][RGB_BCO];        // [kk][hi|lo][h][co]
+  __shared__ float s_b[2 * RGB_BCO];             // bias, PReLU slope
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, l32 = lane & 31;
+  int bid = blockIdx.x;
+  {
+    const int nb = a.nblocks, q = nb >> 3, r = nb & 7, xcd = bid & 7, k = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int pt = bid % a.px_tiles, n = bid / a.px_tiles;
+  const int HW = a.H * a.W, m0 = pt * RGB_BPX, mlast = min(m0 + RGB_BPX, HW) - 1;
+  const int Wi = a.W + 2 * a.in_pad;
+  const float* in_f = a.in + (size_t)n * a.in_fs;
+  for (int i = tid; i < 2 * 2 * 2 * RGB_BCO; i += RGB_NT) (&s_w[0][0][0][0])[i] = a.wpk[i];
+  for (int i = tid; i < RGB_BCO; i += RGB_NT) {
+    s_b[i] = a.bias[i];
+    s_b[RGB_BCO + i] = a.act == ACT_PRELU ? a.slope[i] : 0.f;
+  }
+  _Float16* sxh = (_Float16*)&s_x[0][0][0];
+  auto put = [&](int hl, int k, int px, _Float16 v) __attribute__((always_inline)) {
+    sxh[(((size_t)hl * 4 + (k >> 3)) * RGB_BPX + px) * 8 + (k & 7)] = v;
+  };
+  // im2col: task (px, ky) reads the 3 input pixels kx = 0..2 of kernel row ky
+  for (int task = tid; task < 3 * RGB_BPX; task += RGB_NT) {
+    const int ky = task / RGB_BPX, px = task - ky * RGB_BPX;
+    const int m = min(m0 + px, mlast);
+    const int y = m / a.W, x = m - y * a.W;
+    const float* src = in_f + (size_t)((y + ky - 1 + a.in_pad) * Wi + x - 1 + a.in_pad) * 8;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const f32x4 v = *(const f32x4*)(src + kx * 8);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int k = 9 * ky + 3 * kx + c;
+        const _Float16 hi = (_Float16)v[c];
+        put(0, k, px, hi);
+        put(1, k, px, (_Float16)(v[c] - (float)hi));
+      }
+    }
+  }
+  for (int px = tid; px < RGB_BPX; px += RGB_NT)
+#pragma unroll
+    for (int k = 27; k < 32; ++k) {
+      put(0, k, px, (_Float16)0.f);
+      put(1, k, px, (_Float16)0.f);
+    }
+  __syncthreads();
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int wm = 0; wm < 2; ++wm)
+#pragma unroll
+    for (int wn = 0; wn < 2; ++wn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[wm][wn][r] = 0.f;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    f16x8 A[2][2], B[2][2];
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) {
+#pragma unroll
+      for (int wm = 0; wm < 2; ++wm) A[wm][hl] = s_w[kk][hl][h][wm * 32 + l32];
+#pragma unroll
+      for (int wn = 0; wn < 2; ++wn) B[wn][hl] = s_x[hl][2 * kk + h][wave * 64 + wn * 32 + l32];
+    }
+#pragma unroll
+    for (int wm = 0; wm < 2; ++wm)
+#pragma unroll
+      for (int wn = 0; wn < 2; ++wn) {
+        acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][0], acc[wm][wn], 0, 0, 0);
+        acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][0], B[wn][1], acc[wm][wn], 0, 0, 0);
+        acc[wm][wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[wn][0], acc[wm][wn], 0, 0, 0);
+      }
+  }
+  // epilogue (as conv_x3_f16's): x 2^-s, bias, activation, range check, float4 stores
+  const int Wo = a.W + 2 * a.out_pad;
+  float* out_f = a.out + (size_t)n * a.out_fs;
+  bool bad = false;
+#pragma unroll
+  for (int wn = 0; wn < 2; ++wn) {
+    const int m = m0 + wave * 64 + wn * 32 + l32;
+    if (m > mlast) continue;
+    const int y = m / a.W, x = m - y * a.W;
+    float* op = out_f + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8;
+#pragma unroll
+    for (int wm = 0; wm < 2; ++wm) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = wm * 32 + 4 * h + 8 * q;
+        if (co >= a.cout) continue;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[wm][wn][4 * q + e] * a.wscale_inv + s_b[co + e];
+          if (a.act == ACT_RELU) v[e] = v[e] > 0.f ? v[e] : 0.f;
+          else if (a.act == ACT_PRELU) v[e] = v[e] >= 0.f ? v[e] : v[e] * s_b[RGB_BCO + co + e];
+          bad |= !(__builtin_fabsf(v[e]) < 65504.f);
+        }
+        float* oc = op + (size_t)(co >> 3) * a.out_chs + (co & 7);
+        if (co + 3 < a.cout) {
+          *(f32x4*)oc = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (co + e < a.cout) oc[e] = v[e];
+        }
+      }
+    }
+  }
+  if (bad) atomicOr(a.range_flag, 1);
+}
+
+bool x3_rgb_fits(const ConvLaunch& c) {
+  return c.ks == 3 && c.cin_chunks == 1 && c.cout <= RGB_BCO && c.in_pad >= 1 && !c.hpool;
+}
+
+hipError_t launch_conv_x3_rgb(const ConvLaunch& c, hipStream_t s) {
+  if (!x3_rgb_fits(c) || !c.wx3 || !c.range_flag || ((c.in_cs | c.out_cs | c.out_coff | c.in_coff) & 7)) {
+    set_error("conv_x3_rgb: needs a 3x3 layer with one input chunk, <= 64 outputs and rgb-packed weights");
+    return hipErrorInvalidValue;
+  }
+  X3Args a{};
+  a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
+  a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
+  a.in_fs = a.in_chs * (c.in_cs / 8);
+  a.out_fs = a.out_chs * (c.out_cs / 8);
+  a.in = c.in + (c.in_coff / 8) * a.in_chs;
+  a.out = c.out + (c.out_coff / 8) * a.out_chs;
+  a.wpk = (const f16x8*)c.wx3; a.bias = c.bias; a.slope = c.slope;
+  a.range_flag = c.range_flag;
+  a.wscale_inv = c.wscale_inv;
+  a.in_pad = c.in_pad; a.out_pad = c.out_pad;
+  a.H = c.H; a.W = c.W; a.cin_chunks = 1; a.pairs = 1; a.cout = c.cout;
+  a.co_tiles = 1;
+  a.px_tiles = (c.H * c.W + RGB_BPX - 1) / RGB_BPX;
+  a.tpx = RGB_BPX;
+  a.act = c.act;
+  a.ksplit = 1;
+  a.nfr = c.n;
+  const long long nb = (long long)c.n * a.px_tiles;
+  if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3_rgb: bad grid"); return hipErrorInvalidValue; }
+  a.nblocks = (int)nb;
+  hipLaunchKernelGGL(conv_x3_rgb, dim3(a.nblocks), dim3(RGB_NT), 0, s, a);
+  return hipGetLastError();
+}
+
+double conv_x3_rgb_mfma_flops(const ConvLaunch& c) {
+  return 3.0 * 2.0 * RGB_BCO * 32.0 * (double)((c.H * c.W + RGB_BPX - 1) / RGB_BPX) * RGB_BPX * c.n;
 }
 
 // Split-K reduction: the ranges' sums added in range order (the order of the in-block

@@ -78,6 +78,11 @@ hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
 // used for a launch when x3_wide1(c with bco 256) says its grid is big enough.
 bool x3_wide1_layer(int ks, int cout, int cin_phys);
 bool x3_wide1(const ConvLaunch& c);
+// conv1_1 (3 input channels in one chunk, 3x3, <= 64 outputs): K packed as the 27
+// real (ky, kx, c) values; c.wx3 then holds the pack_x3_rgb filters [kk][hi|lo][h][64][8].
+bool x3_rgb_fits(const ConvLaunch& c);
+hipError_t launch_conv_x3_rgb(const ConvLaunch& c, hipStream_t s);
+double conv_x3_rgb_mfma_flops(const ConvLaunch& c);
 hipError_t launch_conv_x3(const ConvLaunch& c, hipStream_t s);
 bool x3_fits(const ConvLaunch& c);
 // whether launch_conv_x3 can run c with hpool (even W, not split across blocks)

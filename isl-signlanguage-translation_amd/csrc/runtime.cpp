@@ -60,6 +60,7 @@ struct ConvLayer {
   float* d_wu = nullptr;         // Winograd-transformed filters
   void* d_wx3 = nullptr;         // split-fp16 filters (conv_x3.hip), tiles of bco channels
   void* d_wx3w = nullptr;        // the same for 256-channel tiles (x3_wide layers; per launch, x3_wide1)
+  void* d_wrgb = nullptr;        // conv1_1: filters with K packed as the 27 real (ky, kx, c) values
   float x3_inv = 1.f;            // 2^-s of the split weights
   void* d_wux3 = nullptr;        // split-fp16 Winograd filters (wino_x3.hip), 3x3 only
   float wx3_inv = 1.f;
@@ -494,6 +495,35 @@ static std::vector<_Float16> pack_x3(const ConvLayer& c, int bco, float* inv_sca
   return out;
 }
 
+// conv1_1 filters for conv_x3_rgb: K = 9 ky + 3 kx + c (27 real, padded to 32),
+// k = 16 kk + 8 h + j, layout [kk][hi|lo][h][64][8]; the same 2^s as pack_x3.
+static bool rgb_layer(const ConvLayer& c) {
+  return c.k == 3 && c.cin == 3 && c.cin_phys == 8 && c.cout <= 64 && c.cmap.size() == 1 && c.cmap[0].phys == 0 &&
+         c.cmap[0].logical == 0 && c.cmap[0].len == 3;
+}
+
+static std::vector<_Float16> pack_x3_rgb(const ConvLayer& c) {
+  float mx = 0.f;
+  for (float v : c.w) mx = std::max(mx, std::fabs(v));
+  int e = 0;
+  if (mx > 0.f) {
+    std::frexp(mx, &e);
+    e = 14 - e;
+  }
+  const float scale = std::ldexp(1.f, e);
+  std::vector<_Float16> out((size_t)2 * 2 * 2 * 64 * 8, (_Float16)0.f);
+  for (int k = 0; k < 27; ++k) {
+    const int ky = k / 9, kx = (k % 9) / 3, ci = k % 3, kk = k / 16, h = (k % 16) / 8, j = k % 8;
+    for (int co = 0; co < c.cout; ++co) {
+      const float w = c.w[(((size_t)co * 3 + ci) * 3 + ky) * 3 + kx] * scale;
+      const _Float16 hi = (_Float16)w;
+      out[((((size_t)kk * 2 + 0) * 2 + h) * 64 + co) * 8 + j] = hi;
+      out[((((size_t)kk * 2 + 1) * 2 + h) * 64 + co) * 8 + j] = (_Float16)(w - (float)hi);
+    }
+  }
+  return out;
+}
+
 // Split-fp16 Winograd filters for wino_x3.hip: U = G g G^T (double) per (co,
 // physical ci), scaled by a per-layer 2^s (max|U| * 2^s in [2^13, 2^14)), split
 // hi + lo; layout [co_tile][pair][xi][hi|lo][h][64][8], h = chunk of the pair.
@@ -565,6 +595,11 @@ static int upload_params(isl_net* net) {
       std::vector<_Float16> xp = pack_x3(c, c.bco, &c.x3_inv);
       if (!c.d_wx3) HIP_OK(hipMalloc(&c.d_wx3, xp.size() * sizeof(_Float16)));
       HIP_OK(hipMemcpy(c.d_wx3, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
+    if (rgb_layer(c)) {
+      std::vector<_Float16> rp = pack_x3_rgb(c);
+      if (!c.d_wrgb) HIP_OK(hipMalloc(&c.d_wrgb, rp.size() * sizeof(_Float16)));
+      HIP_OK(hipMemcpy(c.d_wrgb, rp.data(), rp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
     if (c.x3_wide) {
       float inv = 1.f;
@@ -687,6 +722,12 @@ static bool x3_wino_enabled() {
   return on;
 }
 
+// ISLPOSE_RGB_CONV=0: conv1_1 on the generic split-fp16 kernel (A/B; read per launch)
+static bool rgb_kernel_enabled() {
+  const char* e = getenv("ISLPOSE_RGB_CONV");
+  return !(e && e[0] == '0');
+}
+
 // ISLPOSE_FUSED_POOL=0: the plain conv + maxpool2 path (A/B; read per run, so a test
 // can compare both in one process)
 static bool fused_pool_enabled() {
@@ -763,8 +804,14 @@ static int run_ops(isl_net* net, hipStream_t s) {
       }
       L.ws = net->d_ks;
       L.ws_floats = net->ks_floats;
-      HIP_OK(launch_conv_x3(L, s));
-      kind = 3; mf = conv_x3_mfma_flops(L);
+      if (c.d_wrgb && x3_rgb_fits(L) && rgb_kernel_enabled()) {
+        L.wx3 = c.d_wrgb;
+        HIP_OK(launch_conv_x3_rgb(L, s));
+        kind = 3; mf = conv_x3_rgb_mfma_flops(L);
+      } else {
+        HIP_OK(launch_conv_x3(L, s));
+        kind = 3; mf = conv_x3_mfma_flops(L);
+      }
     } else {
       HIP_OK(launch_conv(L, s));
       mf = conv_mfma_flops(L);
@@ -860,6 +907,7 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_wu) (void)hipFree(c.d_wu);
     if (c.d_wx3) (void)hipFree(c.d_wx3);
     if (c.d_wx3w) (void)hipFree(c.d_wx3w);
+    if (c.d_wrgb) (void)hipFree(c.d_wrgb);
     if (c.d_wux3) (void)hipFree(c.d_wux3);
   }
   if (net->d_flag) (void)hipFree(net->d_flag);

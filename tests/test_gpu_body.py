@@ -76,6 +76,23 @@ def test_fused_pool_bit_identical(net25, n, h, w, monkeypatch):
     assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
 
 
+@pytest.mark.parametrize("n,h,w", [(2, 184, 328), (1, 50, 70)])
+def test_rgb_first_layer_kernel(net25, w25, n, h, w, monkeypatch):
+    """conv1_1 through conv_x3_rgb (K = the 27 real (ky, kx, c) products) against the
+    generic split-fp16 kernel (ISLPOSE_RGB_CONV=0) and the oracle: the same fp32-accurate
+    sums in another order, so within 1e-5 of each other and the 1e-4 bar vs the oracle."""
+    x = _inputs(n, h, w, seed=5 * h + w)
+    xt = torch.from_numpy(x).cuda()
+    paf1, heat1 = net25.forward(xt)
+    monkeypatch.setenv("ISLPOSE_RGB_CONV", "0")
+    paf0, heat0 = net25.forward(xt)
+    torch.cuda.synchronize()
+    assert _rel(paf1.cpu().numpy(), paf0.cpu().numpy()) < 1e-5
+    assert _rel(heat1.cpu().numpy(), heat0.cpu().numpy()) < 1e-5
+    rp, rh = cpu_ref.make_net_fn("body25", w25)(x)
+    assert _rel(paf1.cpu().numpy(), rp) < TOL and _rel(heat1.cpu().numpy(), rh) < TOL
+
+
 def test_body25_forward_lds_dma_staging(net25, w25, monkeypatch):
     """The LDS-DMA staging variant of the conv kernel gives the same results."""
     x = torch.from_numpy(_inputs(2, 50, 70, seed=9)).cuda()

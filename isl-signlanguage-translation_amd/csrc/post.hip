@@ -1277,6 +1277,106 @@ __global__ void __launch_bounds__(256) cc_cand_kernel(int h, int w, int rows, in
     }
 }
 
+// Fast finish for planes with at most CC_KFAST candidate components (in practice one):
+// per (plane, chunk) the candidates' pixel counts and first maxima (cc_count), then
+// their values compacted in raster order into `vals` (cc_scatter, each chunk at the
+// prefix of the counts before it), so the per-plane kernel only runs numpy's
+// pairwise sums and reduces the chunk maxima.
+constexpr int CC_KFAST = 4;
+struct CcChunk {
+  int count[CC_KFAST];
+  int besti[CC_KFAST];
+  double bestv[CC_KFAST];
+};
+
+__device__ __forceinline__ void cc_pick2(double& v, int& i, double v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+}
+
+__global__ void __launch_bounds__(256) cc_count_kernel(const double* __restrict__ planes, int h, int w, int rows,
+                                                       int chunks, const int* __restrict__ parent_all,
+                                                       const CcStats* __restrict__ stats, CcChunk* __restrict__ ck) {
+  __shared__ int s_c[4];
+  __shared__ double s_v[4];
+  __shared__ int s_i[4];
+  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  const int nk = stats[plane].ncand;
+  if (stats[plane].count == 0 || nk < 1 || nk > CC_KFAST) return;
+  const int P = h * w, p0 = c * rows * w, p1 = min(P, p0 + rows * w);
+  const int* parent = parent_all + (size_t)plane * P;
+  const double* map = planes + (size_t)plane * P;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  CcChunk& out = ck[(size_t)plane * chunks + c];
+  for (int k = 0; k < nk; ++k) {
+    const int root = stats[plane].cand[k];
+    int cnt = 0, bi = 0x7fffffff;
+    double bv = -1.0;
+    for (int p = p0 + threadIdx.x; p < p1; p += 256)
+      if (parent[p] == root) {
+        ++cnt;
+        cc_pick2(bv, bi, map[p], p);
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      cnt += __shfl_xor(cnt, o, 64);
+      cc_pick2(bv, bi, __shfl_xor(bv, o, 64), __shfl_xor(bi, o, 64));
+    }
+    if (lane == 0) { s_c[wave] = cnt; s_v[wave] = bv; s_i[wave] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      double v = -1.0;
+      int i = 0x7fffffff;
+      for (int q = 0; q < 4; ++q) { t += s_c[q]; cc_pick2(v, i, s_v[q], s_i[q]); }
+      out.count[k] = t; out.bestv[k] = v; out.besti[k] = i;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) cc_scatter_kernel(const double* __restrict__ planes, int h, int w, int rows,
+                                                         int chunks, const int* __restrict__ parent_all,
+                                                         const CcStats* __restrict__ stats,
+                                                         const CcChunk* __restrict__ ck, double* __restrict__ vals_all) {
+  __shared__ int s_w[4], s_base;
+  const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
+  const int nk = stats[plane].ncand;
+  if (stats[plane].count == 0 || nk < 1 || nk > CC_KFAST) return;
+  const int P = h * w, p0 = c * rows * w, p1 = min(P, p0 + rows * w);
+  const int* parent = parent_all + (size_t)plane * P;
+  const double* map = planes + (size_t)plane * P;
+  double* vals = vals_all + (size_t)plane * P;
+  const CcChunk* pc = ck + (size_t)plane * chunks;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int per = (p1 - p0 + 255) / 256;
+  const int a = min(p1, p0 + threadIdx.x * per), b = min(p1, a + per);
+  for (int k = 0; k < nk; ++k) {
+    const int root = stats[plane].cand[k];
+    if (threadIdx.x == 0) {   // region of candidate k, then this chunk's place in it
+      int base = 0;
+      for (int q = 0; q < k; ++q)
+        for (int cc = 0; cc < chunks; ++cc) base += pc[cc].count[q];
+      for (int cc = 0; cc < c; ++cc) base += pc[cc].count[k];
+      s_base = base;
+    }
+    int cnt = 0;
+    for (int p = a; p < b; ++p) cnt += parent[p] == root;
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int o = s_base + incl - cnt;
+    for (int q = 0; q < wave; ++q) o += s_w[q];
+    for (int p = a; p < b; ++p)
+      if (parent[p] == root) vals[o++] = map[p];
+    __syncthreads();
+  }
+}
+
 constexpr int CC_NT = 1024;   // threads per plane (one workgroup per (crop, part))
 constexpr int CC_NW = CC_NT / 64;
 constexpr int CC_RUN = 8;     // consecutive pixels per thread and round of the per-plane passes
@@ -1367,6 +1467,7 @@ __global__ void __launch_bounds__(CC_NT) hand_cc_kernel(const double* __restrict
                                                         const unsigned long long* __restrict__ mask, int h, int w,
                                                         int words, int* __restrict__ parent_all,
                                                         double* __restrict__ vals_all, const CcStats* __restrict__ stats,
+                                                        const CcChunk* __restrict__ ck, int chunks,
                                                         long long* __restrict__ out) {
   extern __shared__ int s_dyn[];
   const int plane = blockIdx.x;   // crop * 21 + part
@@ -1405,6 +1506,44 @@ __global__ void __launch_bounds__(CC_NT) hand_cc_kernel(const double* __restrict
   if (cc_block_sum(local, s_i) == 0) {     // np.sum(binary) == 0 -> [0, 0]
     if (tid == 0) { out[plane * 2] = 0; out[plane * 2 + 1] = 0; }
     return;
+  }
+  if constexpr (PRE) {
+    const int nk = stats[plane].ncand;
+    if (nk >= 1 && nk <= CC_KFAST) {
+      // fast finish: the candidates' values are compacted (cc_scatter), their chunk
+      // maxima known (cc_count); exact sums in label (root) order, first max kept
+      const CcChunk* pc = ck + (size_t)plane * chunks;
+      int order[CC_KFAST], tot[CC_KFAST], base[CC_KFAST];
+      for (int k = 0; k < nk; ++k) order[k] = k;
+      for (int i = 1; i < nk; ++i)
+        for (int j = i; j > 0 && stats[plane].cand[order[j - 1]] > stats[plane].cand[order[j]]; --j) {
+          const int t = order[j]; order[j] = order[j - 1]; order[j - 1] = t;
+        }
+      for (int k = 0, acc = 0; k < nk; ++k) {
+        int t = 0;
+        for (int c = tid; c < chunks; c += CC_NT) t += pc[c].count[k];
+        tot[k] = cc_block_sum(t, s_i);
+        base[k] = acc;
+        acc += tot[k];
+      }
+      int bestk = -1;
+      double bestsum = 0.0;
+      for (int q = 0; q < nk; ++q) {
+        const int k = order[q];
+        const double sum = np_sum_block(vals + base[k], tot[k]);
+        if (bestk < 0 || sum > bestsum) { bestsum = sum; bestk = k; }   // first max
+      }
+      double bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int c = tid; c < chunks; c += CC_NT)
+        if (pc[c].count[bestk] > 0) cc_pick(bv, bi, pc[c].bestv[bestk], pc[c].besti[bestk]);
+      const int pbest = cc_block_argmax(bv, bi, s_d, s_i);
+      if (tid == 0) {
+        out[plane * 2] = pbest % w;
+        out[plane * 2 + 1] = pbest / w;
+      }
+      return;
+    }
   }
   if constexpr (!PRE) {
     __threadfence_block();
@@ -1786,8 +1925,10 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
   const size_t avg_bytes = (size_t)n * nparts * P * 8, mask_bytes = (size_t)n * nparts * h * words * 8;
   const size_t par_bytes = (size_t)n * nparts * P * 4, val_bytes = (size_t)n * nparts * P * 8;
   const size_t st_bytes = (size_t)n * nparts * sizeof(CcStats);
+  const int cc_rows = std::max(1, CC_CHUNK / w), cc_chunks = (h + cc_rows - 1) / cc_rows;
+  const size_t ck_bytes = (size_t)n * nparts * cc_chunks * sizeof(CcChunk);
   char* base = (char*)net_scratch(net, up(avg_bytes) + up(mid_bytes) + up(mask_bytes) + up(par_bytes) + up(val_bytes) +
-                                           up(st_bytes));
+                                           up(st_bytes) + up(ck_bytes));
   if (!base) return ISL_E_HIP;
   double* avg = (double*)base;
   float* mid = (float*)(base + up(avg_bytes));
@@ -1795,6 +1936,7 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
   int* parent = (int*)((char*)mask + up(mask_bytes));
   double* vals = (double*)((char*)parent + up(par_bytes));
   CcStats* stats = (CcStats*)((char*)vals + up(val_bytes));
+  CcChunk* cks = (CcChunk*)((char*)stats + up(st_bytes));
   PHIP(hipMemsetAsync(avg, 0, avg_bytes, s));
   const float div_f = (float)nscales;
   for (int si = 0; si < nscales; ++si) {
@@ -1828,10 +1970,10 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
       attr = true;
     }
     hipLaunchKernelGGL((hand_cc_kernel<true, false>), dim3(n * nparts), dim3(CC_NT), (size_t)h * w * 4, s,
-                       (const double*)avg, mask, h, w, words, parent, vals, nullptr, (long long*)d_peaks);
+                       (const double*)avg, mask, h, w, words, parent, vals, nullptr, nullptr, 0, (long long*)d_peaks);
   } else {
     if (w > CC_WMAX) return post_fail(ISL_E_ARG, "isl_hand_post: crop wider than 8192 px");
-    const int rows = std::max(1, CC_CHUNK / w), chunks = (h + rows - 1) / rows;
+    const int rows = cc_rows, chunks = cc_chunks;
     const dim3 g(n * nparts * chunks);
     hipLaunchKernelGGL(cc_local_kernel, g, dim3(256), 0, s, mask, h, w, words, rows, chunks, parent, vals, stats);
     hipLaunchKernelGGL(cc_merge_kernel, g, dim3(256), 0, s, mask, h, w, words, rows, chunks, parent);
@@ -1839,8 +1981,11 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
     hipLaunchKernelGGL(cc_sum_kernel, g, dim3(256), 0, s, (const double*)avg, h, w, rows, chunks, parent, vals, stats);
     hipLaunchKernelGGL(cc_stats_kernel, g, dim3(256), 0, s, h, w, rows, chunks, parent, vals, stats);
     hipLaunchKernelGGL(cc_cand_kernel, g, dim3(256), 0, s, h, w, rows, chunks, parent, vals, stats);
+    hipLaunchKernelGGL(cc_count_kernel, g, dim3(256), 0, s, (const double*)avg, h, w, rows, chunks, parent, stats, cks);
+    hipLaunchKernelGGL(cc_scatter_kernel, g, dim3(256), 0, s, (const double*)avg, h, w, rows, chunks, parent, stats, cks,
+                       vals);
     hipLaunchKernelGGL((hand_cc_kernel<false, true>), dim3(n * nparts), dim3(CC_NT), 0, s, (const double*)avg, mask,
-                       h, w, words, parent, vals, stats, (long long*)d_peaks);
+                       h, w, words, parent, vals, stats, cks, chunks, (long long*)d_peaks);
   }
   PHIP(hipGetLastError());
   return ISL_OK;

@@ -86,10 +86,21 @@ def rank_env():
 
 
 def init_group(world):
-    """Host-side (gloo) group for the barrier and the timing reductions only."""
+    """Host-side (gloo) group for the barrier and the timing reductions only.  gloo
+    prints its connection lines on the process's stdout: they go to stderr here, so
+    rank 0's stdout carries only the JSON line."""
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.distributed.init_process_group("gloo")
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            torch.distributed.init_process_group("gloo")
+            torch.distributed.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         assert torch.distributed.get_world_size() == world
 
 
@@ -161,6 +172,10 @@ def gpu_main(args, rank, local, world):
     from islpose import synth
     from islpose.body import BodyEstimator, scale_geometry
 
+    # one GPU per rank; more ranks than visible GPUs share them round-robin (a rehearsal
+    # of the multi-rank path on a smaller box -- the line then says so in "ranks")
+    ndev = torch.cuda.device_count()
+    local = local % ndev if ndev > 0 else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     B, H, W = args.batch, args.height, args.width
@@ -272,7 +287,7 @@ def gpu_main(args, rank, local, world):
     post_ms = float(np.mean([post_window_ms(r, m) for r, m in ev]))
     e2e = e2e_rate(args, lanes[0].est, frames_h, maps, dev) if args.e2e_steps > 0 else None
     g = gather_floats([elapsed, net_ms, post_ms, B * args.steps / elapsed, lo, hi,
-                       e2e["frames_per_s"] if e2e else 0.0], world)
+                       e2e["frames_per_s"] if e2e else 0.0, local], world)
     elapsed, net_ms, post_ms = float(g[:, 0].max()), float(g[:, 1].max()), float(g[:, 2].max())
     if rank != 0:
         return
@@ -328,6 +343,8 @@ def gpu_main(args, rank, local, world):
         "ranks": {"world_observed": torch.distributed.get_world_size() if world > 1 else 1,
                   "per_rank_frames_per_s": [round(float(v), 2) for v in g[:, 3]],
                   "frame_shards": [[int(a), int(b)] for a, b in g[:, 4:6]],
+                  "rank_devices": [int(d) for d in g[:, 7]],
+                  "devices_shared": bool(len(set(int(d) for d in g[:, 7])) < world),
                   "timing_collectives": "gloo (host): barrier + all_gather of per-rank times; no data-path collective"},
         "roofline": {"bound": "mfma", "kernel": KIND[dom],
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

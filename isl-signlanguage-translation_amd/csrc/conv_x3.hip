@@ -949,6 +949,27 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   }
   const bool ranged = c.ksplit > 1 && !c.ws;      // launch_conv_x3: in-block ranges
   const bool split = c.ksplit > 1 && c.ws;        // across blocks
+  // 128- / 96-channel tiles of the 128-pixel family: 8 waves of 64co x 32px / 12 waves of
+  // 32co x 32px rather than 4 waves of 64co x 64px / 96co x 32px.  These grids are small
+  // (Mode R's 23x41 stages: one block per CU at batch 32), and two or three waves per
+  // SIMD hide the staging: -8 to -22 % on the 23x41 3x3 stage layers, -12 to -31 % on
+  // their 1x1 layers, -5 to -14 % on the hand's 23^2 7x7 layers, -20 % on its 23^2 c512
+  // layers (tools/gpu_s8.sh, gpu_s8b.sh).  ISLPOSE_X3_S8=0: the 4-wave layouts (A/B).
+  static const int more = getenv("ISLPOSE_X3_S8") ? atoi(getenv("ISLPOSE_X3_S8")) : 1;
+  if (more) {
+    {
+      switch (c.bco) {
+        case 128:   // 8 waves of 64co x 32px
+          if (split) return launch_t<KS, 2, 4, 2, 1, 2048, 2>(c, s);
+          if (ranged) return launch_t<KS, 2, 4, 2, 1, 1024, 2>(c, s);
+          return launch_t<KS, 2, 4, 2, 1, 0, 2>(c, s);
+        case 96:    // 12 waves of 32co x 32px
+          if (split) return launch_t<KS, 3, 4, 1, 1, 2048, 2>(c, s);
+          if (ranged) return launch_t<KS, 3, 4, 1, 1, 1024, 2>(c, s);
+          return launch_t<KS, 3, 4, 1, 1, 0, 2>(c, s);
+      }
+    }
+  }
   switch (c.bco) {
 #define X3_CASE(BC, WMS, WNS, WMM, WNN)                                           \
   case BC:                                                                        \

@@ -8,8 +8,12 @@ OUT      := $(PKG)/islpose/libislpose.so
 # operation order bit-for-bit, which forbids fused multiply-adds.
 HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -Iinclude -I$(CSRC) \
             -Wall -Wno-unused-function -Wno-unused-variable -Wno-unused-lambda-capture
-SRCS     := $(CSRC)/conv.hip $(CSRC)/conv_x3.hip $(CSRC)/wino.hip $(CSRC)/wino_x3.hip $(CSRC)/ops.hip $(CSRC)/post.hip $(CSRC)/sign.hip $(CSRC)/runtime.cpp
+SRCS     := $(CSRC)/conv.hip $(CSRC)/conv_x3.hip $(CSRC)/wino.hip $(CSRC)/ops.hip $(CSRC)/post.hip $(CSRC)/sign.hip $(CSRC)/runtime.cpp
 OBJS     := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
+# development objects (tools/convbench): the product sources plus the rejected split-fp16
+# Winograd kernel and the s_memtime stamp variant, compiled with -DISLPOSE_DEV
+DEV_SRCS := $(SRCS) $(CSRC)/wino_x3.hip
+DEV_OBJS := $(patsubst $(CSRC)/%,build_dev/%.o,$(DEV_SRCS))
 
 all: $(OUT)
 
@@ -20,11 +24,15 @@ build/%.o: $(CSRC)/% $(CSRC)/internal.h include/islpose.h
 $(OUT): $(OBJS)
 	$(HIPCC) $(HIPFLAGS) -shared -Wl,-z,defs -o $@ $(OBJS)
 
+build_dev/%.o: $(CSRC)/% $(CSRC)/internal.h include/islpose.h
+	@mkdir -p build_dev
+	$(HIPCC) $(HIPFLAGS) -DISLPOSE_DEV -x hip -c $< -o $@
+
 clean:
-	rm -rf build $(OUT)
+	rm -rf build build_dev $(OUT)
 
 .PHONY: all clean
 
 # development microbenchmark of the conv kernels (not part of the library)
-tools/convbench: tools/convbench.cpp $(OBJS)
-	$(HIPCC) $(HIPFLAGS) -x hip tools/convbench.cpp -x none $(filter-out build/runtime.cpp.o build/post.hip.o build/ops.hip.o,$(OBJS)) build/runtime.cpp.o build/post.hip.o build/ops.hip.o -o $@
+tools/convbench: tools/convbench.cpp $(DEV_OBJS)
+	$(HIPCC) $(HIPFLAGS) -DISLPOSE_DEV -x hip tools/convbench.cpp -x none $(DEV_OBJS) -o $@

@@ -50,7 +50,8 @@
 //         whether its ranges ran in one block (large grids) or across blocks (small
 //         grids: batch-1 frames).
 //   4096  two chunk pairs per K step (1x1 layers on 256-channel tiles, x3_wide1);
-//   16384 development only: s_memtime stamps of the union loop (tools/convbench).
+//   16384 development only: s_memtime stamps of the union loop (tools/convbench;
+//         compiled only with -DISLPOSE_DEV, never into libislpose.so).
 // conv_x3_rgb: the 3-channel first layers (conv1_1) with K packed as the 27 real
 // (ky, kx, c) values instead of 9 taps x 16 channels.
 #include <algorithm>
@@ -911,12 +912,14 @@ template <int KS>
 static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   if constexpr (KS == 3) {
     if (x3_big_tiles(c) && x3_union(c)) {
-      if (x3_union_mode() == 4 && c.dbg) {
+#ifdef ISLPOSE_DEV
+      if (x3_union_mode() == 4 && c.dbg) {   // development build only (tools/convbench)
         switch (c.bco) {
           case 128: return launch_t<KS, 2, 8, 2, 2, 512 | 16384, 4>(c, s);
           case 96: return launch_t<KS, 1, 16, 3, 1, 512 | 16384, 4>(c, s);
         }
       }
+#endif
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 512, 4>(c, s);
         case 96: return launch_t<KS, 1, 16, 3, 1, 512, 4>(c, s);

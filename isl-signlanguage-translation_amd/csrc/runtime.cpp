@@ -524,6 +524,7 @@ static std::vector<_Float16> pack_x3_rgb(const ConvLayer& c) {
   return out;
 }
 
+#ifdef ISLPOSE_DEV
 // Split-fp16 Winograd filters for wino_x3.hip: U = G g G^T (double) per (co,
 // physical ci), scaled by a per-layer 2^s (max|U| * 2^s in [2^13, 2^14)), split
 // hi + lo; layout [co_tile][pair][xi][hi|lo][h][64][8], h = chunk of the pair.
@@ -574,6 +575,7 @@ static std::vector<_Float16> pack_wino_x3(const ConvLayer& c, float* inv_scale) 
     }
   return out;
 }
+#endif
 
 static int upload_params(isl_net* net) {
   for (ConvLayer& c : net->layers) {
@@ -607,11 +609,13 @@ static int upload_params(isl_net* net) {
       if (!c.d_wx3w) HIP_OK(hipMalloc(&c.d_wx3w, xp.size() * sizeof(_Float16)));
       HIP_OK(hipMemcpy(c.d_wx3w, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
+#ifdef ISLPOSE_DEV
     if (c.k == 3 && c.cout % 4 == 0) {
       std::vector<_Float16> up = pack_wino_x3(c, &c.wx3_inv);
       if (!c.d_wux3) HIP_OK(hipMalloc(&c.d_wux3, up.size() * sizeof(_Float16)));
       HIP_OK(hipMemcpy(c.d_wux3, up.data(), up.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
+#endif
     if (c.wbco) {
       std::vector<float> up = pack_wino(c);
       if (!c.d_wu) HIP_OK(hipMalloc(&c.d_wu, up.size() * sizeof(float)));
@@ -711,6 +715,7 @@ static int default_algo() {
   return ISL_ALGO_X3;
 }
 
+#ifdef ISLPOSE_DEV
 // ISL_ALGO_X3 runs 3x3 layers on the direct split-fp16 kernel; ISLPOSE_X3_WINO=1
 // selects the split-fp16 Winograd kernel instead.  It is fp32-accurate (rel err
 // 3e-6) but measured 1.3-1.8x SLOWER (r01): its V transform + split costs ~184
@@ -721,6 +726,7 @@ static bool x3_wino_enabled() {
   static const bool on = getenv("ISLPOSE_X3_WINO") && getenv("ISLPOSE_X3_WINO")[0] == '1';
   return on;
 }
+#endif
 
 // ISLPOSE_RGB_CONV=0: conv1_1 on the generic split-fp16 kernel (A/B; read per launch)
 static bool rgb_kernel_enabled() {
@@ -774,10 +780,12 @@ static int run_ops(isl_net* net, hipStream_t s) {
       L.wpk = c.d_wu; L.bco = c.wbco;
       HIP_OK(launch_wino(L, s));
       kind = 2; mf = wino_mfma_flops(L);
+#ifdef ISLPOSE_DEV
     } else if (net->algo == ISL_ALGO_X3 && c.d_wux3 && x3_wino_enabled()) {
       L.wx3 = c.d_wux3; L.wscale_inv = c.wx3_inv;
       HIP_OK(launch_wino_x3(L, s));
       kind = 4; mf = wino_x3_mfma_flops(L);
+#endif
     } else if (net->algo == ISL_ALGO_X3 && x3_fits(L)) {
       L.allow_split = net->split_k;
       if (c.x3_wide) {   // 256-channel tiles, two pairs per step, where the grid is big enough

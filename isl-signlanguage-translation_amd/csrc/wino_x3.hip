@@ -33,6 +33,7 @@
 // Work item of a thread (its wave's (h, row-half) are uniform): one tile, one
 // chunk (8 channels), one row half hf: 3 input rows x 4 columns -> V rows
 // 2hf, 2hf+1 (8 of the 16 xi).
+#ifdef ISLPOSE_DEV   // measured 1.3-1.8x slower than conv_x3: development builds only
 #include <cmath>
 #include <type_traits>
 
@@ -301,3 +302,4 @@ double wino_x3_mfma_flops(const ConvLaunch& c) {
 }
 
 }  // namespace isl
+#endif  // ISLPOSE_DEV

@@ -7,7 +7,7 @@ resident in HBM:
                           FP16 matrix cores by default, fp32-accurate)
     isl_body_post        (x8 cubic resize, fp64 blur + NMS, peak lists, PAF line
                           integrals, greedy matching, person assembly)
-    + async D2H of the per-frame result records.
+    + async D2H of the per-frame result records (copy stream, overlapping the next step).
 The post stage is fed designed pose maps (3 persons per frame) so that its cost
 is that of real footage (raw outputs of random weights produce ~4k peaks, see
 SURVEY.md §8d); the network still runs in full every step.
@@ -70,6 +70,8 @@ def parse(argv=None):
                    help="conv arithmetic: split-fp16 x3 on the FP16 matrix cores (default), Winograd or direct fp32")
     p.add_argument("--cpu-frames", type=int, default=6, help="frames for the CPU baseline sample (0 = skip)")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-op-timing", action="store_true",
+                   help="A/B only: no per-op HIP events in the timed region (roofline fields then absent)")
     p.add_argument("--e2e-steps", type=int, default=3,
                    help="batches timed through the caller path (host frames in, Python results out); 0 = skip")
     p.add_argument("--split-k", action="store_true",
@@ -215,29 +217,42 @@ def gpu_main(args, rank, local, world):
             self.hp = (ctypes.c_void_p * 1)(self.heat.data_ptr())
             self.stream = main_stream if S == 1 else torch.cuda.Stream(dev)
             self.sh = rt.stream_handle(self.stream)
+            # D2H of the records on a copy stream: it overlaps the next step's preprocess and
+            # net; the next post (which rewrites d_res) waits for it, and the timed region's
+            # closing device synchronize includes it
+            self.cs = torch.cuda.Stream(dev)
+            self.copied = None
 
     lanes = [Lane(s) for s in range(S)]
     ev = []
 
     def step(timed):
-        ref = torch.cuda.Event(enable_timing=True)
-        ref.record(main_stream)
+        # timed: stage events (net / post windows) on this step; timing events are kept
+        # off the other steps, like the per-op events (each costs a dispatch gap)
+        def mark(stream):
+            e = torch.cuda.Event(enable_timing=timed)
+            e.record(stream)
+            return e
+        ref = mark(main_stream)
         marks = []
         for ln in lanes:
-            ln.stream.wait_event(ref)
+            if ln.stream is not main_stream:
+                ln.stream.wait_event(ref)
             ln.net.preprocess(ln.frames, mult, stream=ln.stream)
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(ln.stream)
+            e0 = mark(ln.stream) if timed else None
             ln.net.run(stream=ln.stream)
-            e1.record(ln.stream)
+            e1 = mark(ln.stream) if timed else None
+            if ln.copied is not None:
+                ln.stream.wait_event(ln.copied)
             rt.check(L.isl_body_post(ln.net.h, ln.b, H, W, 1, ln.g, ln.pp, ln.hp, ctypes.byref(ln.caps),
                                      rt.ptr(ln.d_res), ln.sh), "post")
-            e2 = torch.cuda.Event(enable_timing=True)
-            e2.record(ln.stream)
+            e2 = mark(ln.stream)
             marks.append((e0, e1, e2))
-            with torch.cuda.stream(ln.stream):
+            ln.cs.wait_event(e2)
+            with torch.cuda.stream(ln.cs):
                 ln.h_res.copy_(ln.d_res, non_blocking=True)
+            ln.copied = torch.cuda.Event()
+            ln.copied.record(ln.cs)
         for ln in lanes:
             if ln.stream is not main_stream:
                 main_stream.wait_stream(ln.stream)
@@ -268,14 +283,20 @@ def gpu_main(args, rank, local, world):
             npk = host[o:o + 128].view(np.int32)
             pairs += sum(int(npk[a]) * int(npk[b]) for a, b in synth.BODY25_LIMBS)
         assert ln.net.range_ok(), "split-fp16 range exceeded in warmup"
-    for ln in lanes:
-        ln.net.set_timing(True)      # per-op HIP events on each lane's stream, inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    for i in range(args.steps):
+        # per-op HIP events (each lane's stream) on the last timed step only: an event
+        # between every launch costs ~8 us of dispatch gap (1.8 % of the step when every
+        # step carried them, tools/gpu_optiming.sh); one instrumented step of K still gives
+        # the per-launch averages of every kernel, inside the timed region
+        last = i == args.steps - 1
+        if last and not args.no_op_timing:
+            for ln in lanes:
+                ln.net.set_timing(True)
+        step(last)
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -293,6 +314,11 @@ def gpu_main(args, rank, local, world):
         return
     total_frames = B * world * args.steps
     fps = total_frames / elapsed
+    if args.no_op_timing:
+        print(json.dumps({"metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 3), "op_timing": False}))
+        return
     # per-kind sums over all lanes and timed steps (HIP events around every launch)
     kinds = {}
     for o in ops:
@@ -360,7 +386,8 @@ def gpu_main(args, rank, local, world):
                      "launches": dk["launches"], "avg_launch_us": round(dk["ms"] * 1e3 / dk["launches"], 2),
                      "algorithmic_gflop_per_launch": round(dk["flops"] / dk["launches"] / 1e9, 3),
                      "all_convs_tflops": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2),
-                     "ms_per_step_by_kind": {KIND[k]: round(v["ms"] / args.steps, 3) for k, v in kinds.items()},
+                     "ms_per_step_by_kind": {KIND[k]: round(v["ms"] / max(1, ops[0]["n_runs"]), 3) for k, v in kinds.items()},
+                     "op_timing": "per-op HIP events on the last of the %d timed steps (lane streams)" % args.steps,
                      "net_ms_per_step": round(net_ms, 3),
                      # PMC (profiles/conv_traffic.json, from tools/profile_round.sh): MFMA pipe busy
                      # fraction of the conv kernels' wall cycles, and the DVFS clock they ran at

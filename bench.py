@@ -338,7 +338,7 @@ def gpu_main(args, rank, local, world):
     executed = dk["mfma_flops"] / sec / 1e12                   # what the matrix cores ran (tile padding included)
     conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3, 4))
     conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3, 4))
-    traffic = mfma_busy = clk = busy_s = clk_s = None
+    traffic = mfma_busy = clk = busy_s = clk_s = stage_busy = stage_busy_s = None
     prof = os.path.join(REPO, "profiles", "conv_traffic.json")
     if os.path.exists(prof):
         pj = json.load(open(prof))
@@ -346,6 +346,8 @@ def gpu_main(args, rank, local, world):
         traffic = pj.get(key + "_hbm_bytes_per_launch")
         mfma_busy, clk = pj.get(key + "_mfma_busy_frac"), pj.get(key + "_effective_clock_ghz")
         busy_s, clk_s = pj.get(key + "_mfma_busy_frac_at_stamp_clock"), pj.get(key + "_stamp_clock_ghz")
+        stage_busy = pj.get("conv_stage_mfma_busy_frac")
+        stage_busy_s = pj.get("conv_stage_mfma_busy_frac_at_stamp_clock")
     out = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -390,8 +392,11 @@ def gpu_main(args, rank, local, world):
                      "op_timing": "per-op HIP events on the last of the %d timed steps (lane streams)" % args.steps,
                      "net_ms_per_step": round(net_ms, 3),
                      # PMC (profiles/conv_traffic.json, from tools/profile_round.sh): MFMA pipe busy
-                     # fraction of the conv kernels' wall cycles, and the DVFS clock they ran at
+                     # fraction of the dominant kernel's wall cycles, and the DVFS clock it ran at; the
+                     # conv stage adds conv1_1's write-bound conv_x3_rgb
                      "mfma_busy_pmc": mfma_busy,
+                     "conv_stage_mfma_busy_pmc": stage_busy,
+                     "conv_stage_mfma_busy_pmc_at_stamp_clock": stage_busy_s,
                      "effective_clock_ghz": clk,
                      "frac_at_effective_clock": round(achieved / (peak * clk / 2.4), 4) if clk else None,
                      # the GRBM-based clock reads high on sub-10 ms dispatches (MI355X_MICROARCH.md DVFS item 6);

@@ -83,28 +83,39 @@ def mfma_busy(sq_dir, stats_csv, sq_out, clock_ghz=None):
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        k = "conv_x3_f16" if "conv_x3" in n else n.split("(")[0].replace("void ", "").replace("isl::", "")
+        k = n.split("(")[0].replace("void ", "").replace("isl::", "").split("<")[0]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r.get("Dispatch_Id", ""))
+        if "conv_x3" in n:   # the whole conv stage: conv_x3_f16 + conv1_1's conv_x3_rgb
+            acc["conv_stage"][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp["conv_stage"].add(r.get("Dispatch_Id", ""))
     json.dump({"note": "raw SQ/GRBM counter sums per kernel class over the profiled bench run",
                "kernels": {k: dict(v, dispatches=len(disp[k])) for k, v in acc.items()}}, open(sq_out, "w"), indent=1)
     x = acc.get("conv_x3_f16")
     if not x or not x.get("GRBM_GUI_ACTIVE"):
         return {}
-    wall_ns = sum(float(r["TotalDurationNs"]) for r in csv.DictReader(open(stats_csv)) if "conv_x3" in r["Name"])
+    stats = list(csv.DictReader(open(stats_csv)))
+    wall_ns = sum(float(r["TotalDurationNs"]) for r in stats if "conv_x3_f16" in r["Name"])
     active = x["GRBM_GUI_ACTIVE"] / 8
-    extra = {}
+    cs = acc["conv_stage"]
+    stage_wall = sum(float(r["TotalDurationNs"]) for r in stats if "conv_x3" in r["Name"])
+    extra = {"conv_stage_mfma_busy_frac": round(cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (cs["GRBM_GUI_ACTIVE"] / 8), 4),
+             "conv_stage_note": "all conv kernels of the net (conv_x3_f16 + conv1_1's conv_x3_rgb, which is bound by "
+                                "its 64-channel output write): MFMA busy / GRBM cycles, as x3_mfma_busy_frac"}
+    if clock_ghz:
+        extra["conv_stage_mfma_busy_frac_at_stamp_clock"] = round(
+            cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (stage_wall * clock_ghz), 4)
     if clock_ghz:
         # GRBM_GUI_ACTIVE / 8 / wall reads high on sub-10 ms dispatches (MI355X_MICROARCH.md, DVFS item 6):
         # the in-kernel clock of a stamp build (s_memtime / s_memrealtime) is the one to divide by
-        extra = {"x3_mfma_busy_frac_at_stamp_clock": round(x["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (wall_ns * clock_ghz), 4),
-                 "x3_stamp_clock_ghz": clock_ghz}
+        extra.update({"x3_mfma_busy_frac_at_stamp_clock": round(x["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (wall_ns * clock_ghz), 4),
+                      "x3_stamp_clock_ghz": clock_ghz})
     return dict(extra, **{"x3_mfma_busy_frac": round(x["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / active, 4),
             "x3_effective_clock_ghz": round(active / wall_ns, 3),
             "mfma_note": "SQ_VALU_MFMA_BUSY_CYCLES (32 cycles per 32x32x16 MFMA, summed over 1024 SIMDs) / 1024 / "
-                         "(GRBM_GUI_ACTIVE / 8 XCDs): the fraction of the conv kernels' cycles the MFMA pipes were "
+                         "(GRBM_GUI_ACTIVE / 8 XCDs): the fraction of conv_x3_f16's cycles the MFMA pipes were "
                          "busy, at the clock the chip actually ran (DVFS); effective clock = GRBM_GUI_ACTIVE / 8 / "
-                         "summed conv_x3 duration of the trace pass of the same command. Source: "
+                         "summed conv_x3_f16 duration of the trace pass of the same command. Source: "
                          + os.path.relpath(sq_out)})
 
 

@@ -738,6 +738,7 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   a.H = c.H; a.W = c.W; a.cin_chunks = c.cin_chunks; a.pairs = (c.cin_chunks + 1) / 2; a.cout = c.cout;
   a.co_tiles = (c.cout + BCO - 1) / BCO;
   a.tpx = tile_pixels(c, BPX, SEGCAP);
+  if (c.hpool && (a.tpx & 1)) --a.tpx;          // pair-max epilogue: tiles start on even pixels
   a.px_tiles = (c.H * c.W + a.tpx - 1) / a.tpx;
   a.act = c.act;
   a.ksplit = (SPLIT || RANGED) ? c.ksplit : 1;
@@ -810,7 +811,19 @@ static int x3_canonical_ranges(const ConvLaunch& c) {
 // family's register budget).  512-pixel tiles are used only when they fill the
 // chip: a layer with fewer such blocks than CUs runs ~2x faster on the 128-pixel,
 // 4-wave family (tools/gpu_tiles.sh).
-static int x3_big_bpx(const ConvLaunch& c) { return c.ks == 1 && c.bco == 256 ? 256 : 512; }
+static bool x3_union(const ConvLaunch& c);
+
+// 64-channel 3x3 layers off the row union (full-resolution conv1_2 / hand conv1_2: 12 K
+// steps) run 256-pixel blocks of 8 waves (64co x 32px each), two blocks per CU, so that one
+// block's prologue and epilogue overlap the other's K loop: -4 to -5 % against the 16-wave
+// 512-pixel block (tools/gpu_mid.sh; the 128-channel layers stay on 512 pixels, where every
+// 256-pixel shape lost 4-7 %).  ISLPOSE_X3_HALF64=0: the 512-pixel block (A/B).
+static bool x3_half64(const ConvLaunch& c) {
+  static const bool on = !(getenv("ISLPOSE_X3_HALF64") && getenv("ISLPOSE_X3_HALF64")[0] == '0');
+  return on && c.ks == 3 && c.bco == 64 && !x3_union(c);
+}
+
+static int x3_big_bpx(const ConvLaunch& c) { return (c.ks == 1 && c.bco == 256) || x3_half64(c) ? 256 : 512; }
 
 static bool x3_big_tiles(const ConvLaunch& c) {
   if (c.ks > 3 || x3_small_tiles() || x3_canonical_ranges(c) > 1) return false;
@@ -872,7 +885,7 @@ static int x3_union_run(const ConvLaunch& c) {
 }
 
 static bool x3_union(const ConvLaunch& c) {
-  if (x3_union_mode() == 0 || c.ks != 3) return false;
+  if (x3_union_mode() == 0 || c.ks != 3 || x3_small_tiles() || x3_canonical_ranges(c) > 1) return false;
   return x3_union_run(c) <= x3_segu_max();
 }
 
@@ -933,6 +946,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   }
   if constexpr (KS <= 3) {
     if (x3_big_tiles(c)) {
+      if (x3_half64(c)) return launch_t<KS, 1, 8, 2, 1, 0, 2>(c, s);   // 8 waves of 64co x 32px, 256 px
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 0, 4>(c, s);   // 16 waves, 64co x 64px each
         case 96: return launch_t<KS, 1, 16, 3, 1, 0, 4>(c, s);   // 16 waves, 96co x 32px

@@ -52,6 +52,8 @@
 //   4096  two chunk pairs per K step (1x1 layers on 256-channel tiles, x3_wide1);
 //   16384 development only: s_memtime stamps of the union loop (tools/convbench;
 //         compiled only with -DISLPOSE_DEV, never into libislpose.so).
+//   32768 pooled input (ConvLaunch::vin): the input is the pair-max buffer of the 2x2
+//         pool before this layer; staging takes the row-pair max (x3_vin_ok).
 // conv_x3_rgb: the 3-channel first layers (conv1_1) with K packed as the 27 real
 // (ky, kx, c) values instead of 9 taps x 16 channels.
 #include <algorithm>
@@ -84,7 +86,31 @@ struct X3Args {
   float* ws;                    // split-K partial sums [ksplit][nfr][cout/8][H*W][8]
   unsigned long long* dbg;      // VAR 16384 (development): s_memtime stamps of block 0
   int hpool;                    // ConvLaunch::hpool: out is the [n][chunk][H][W/2][8] pair-max buffer
+  int vin;                      // ConvLaunch::vin: in is the [n][chunk][2H][W][8] pair-max buffer of a pool
 };
+
+// u / d for 0 <= u < 2^20, d >= 1, through the fp32 reciprocal r = 1/d: (u + 0.5) / d sits
+// >= 0.5 / d away from an integer, and (u + 0.5) * r (two roundings, relative error < 2^-23)
+// is off by < 2^20 / d * 2^-23 = 0.125 / d, so the truncation is exact
+__device__ __forceinline__ int x3_div(int u, float r) { return (int)(((float)u + 0.5f) * r); }
+
+// VIN: the staged input pixel at padded position (yy, xx) of chunk plane `src` (the pair-max
+// buffer [2H][W][8] of the pool this layer reads): max of rows 2(yy-pad), 2(yy-pad)+1,
+// zero on the ring -- the values maxpool2_kernel / vpool2_kernel would have stored
+__device__ __forceinline__ void x3_vin_load(const float* src, int yy, int xx, const X3Args& a, float4& lo4,
+                                            float4& hi4) {
+  const int y = yy - a.in_pad, x = xx - a.in_pad;
+  if (y < 0 || y >= a.H || x < 0 || x >= a.W) {
+    lo4 = hi4 = float4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
+  const float* p0 = src + ((size_t)(2 * y) * a.W + x) * 8;
+  const float* p1 = p0 + (size_t)a.W * 8;
+  const float4 a0 = *(const float4*)p0, a1 = *(const float4*)(p0 + 4);
+  const float4 b0 = *(const float4*)p1, b1 = *(const float4*)(p1 + 4);
+  lo4 = float4{fmaxf(a0.x, b0.x), fmaxf(a0.y, b0.y), fmaxf(a0.z, b0.z), fmaxf(a0.w, b0.w)};
+  hi4 = float4{fmaxf(a1.x, b1.x), fmaxf(a1.y, b1.y), fmaxf(a1.z, b1.z), fmaxf(a1.w, b1.w)};
+}
 
 // input segment capacity in pixels for a BPX-pixel tile (host: tile_pixels)
 constexpr int x3_segmax(int bpx) { return bpx + 64; }
@@ -119,6 +145,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr bool RANGED = (VAR & 1024) != 0;
   constexpr bool SPLIT = (VAR & 2048) != 0;
   constexpr bool STAMP = (VAR & 16384) != 0;
+  constexpr bool VIN = (VAR & 32768) != 0;      // ConvLaunch::vin (pooled-input staging)
   static_assert(!(UNION && (RANGED || SPLIT)), "K ranges run on the generic loop");
   static_assert(PPS == 1 || !(UNION || RANGED || SPLIT), "two pairs per step: plain generic loop only");
   __shared__ f16x8 smem[SMEM];
@@ -144,6 +171,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   const int m0 = pt * a.tpx;                    // tpx = BPX unless the image is very narrow
   const int mlast = min(m0 + a.tpx, HW) - 1;
   const int Wi = a.W + 2 * a.in_pad;
+  const float inv_wi = 1.f / (float)Wi;          // VIN: x3_div
   const int ya = m0 / a.W, xa = m0 - ya * a.W;
   const int yb = mlast / a.W, xb = mlast - yb * a.W;
   const int La = (ya + a.in_pad) * Wi + xa + a.in_pad;
@@ -228,9 +256,17 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     auto load_c = [&](int c2, int ky) __attribute__((always_inline)) {
       if (c_px[ky] >= 0) {
         const int c = min(2 * c2 + c_ih[ky], a.cin_chunks - 1);
-        const float* src = in_f + (size_t)c * a.in_chs + (size_t)(ubase + c_px[ky]) * 8;
-        ru[0] = *(const f32x4*)src;
-        ru[1] = *(const f32x4*)(src + 4);
+        if constexpr (VIN) {   // padded (row, column) of the item, recomputed (no registers held across the loop)
+          const int u = (int)ubase + c_px[ky], yy = x3_div(u, inv_wi);
+          float4 l4, h4;
+          x3_vin_load(in_f + (size_t)c * a.in_chs, yy, u - yy * Wi, a, l4, h4);
+          ru[0] = f32x4{l4.x, l4.y, l4.z, l4.w};
+          ru[1] = f32x4{h4.x, h4.y, h4.z, h4.w};
+        } else {
+          const float* src = in_f + (size_t)c * a.in_chs + (size_t)(ubase + c_px[ky]) * 8;
+          ru[0] = *(const f32x4*)src;
+          ru[1] = *(const f32x4*)(src + 4);
+        }
       }
     };
     auto store_c = [&](int c2, int ky, int bx) __attribute__((always_inline)) {
@@ -323,9 +359,17 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       for (int i = 0; i < IT; ++i) {
         const int c = 2 * PPS * c2 + ih[i];
         if (ipx[i] >= 0 && c < a.cin_chunks) {
-          const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + ipx[i]) * 8;
-          raw[i][0] = *(const f32x4*)src;
-          raw[i][1] = *(const f32x4*)(src + 4);
+          if constexpr (VIN) {   // padded (row, column) of the item, recomputed per step
+            const int u = (int)row + ipx[i], yy = x3_div(u, inv_wi);
+            float4 l4, h4;
+            x3_vin_load(in_f + (size_t)c * a.in_chs, yy, u - yy * Wi, a, l4, h4);
+            raw[i][0] = f32x4{l4.x, l4.y, l4.z, l4.w};
+            raw[i][1] = f32x4{h4.x, h4.y, h4.z, h4.w};
+          } else {
+            const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + ipx[i]) * 8;
+            raw[i][0] = *(const f32x4*)src;
+            raw[i][1] = *(const f32x4*)(src + 4);
+          }
         } else {
           raw[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
           raw[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -506,14 +550,17 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
 // conv1_1 of every net: 3 input channels, 3x3, 64 outputs.  Through the generic
 // kernel a pixel costs 9 pair-taps of K = 16 for 27 real products (5.3x the work);
 // here K is the 27 real (ky, kx, c) values padded to 32 -- two MFMA K-steps --
-// from an im2col tile of 512 pixels x 32 k in LDS (fp16 hi | lo, 64 KiB), built
+// from an im2col tile of 256 pixels x 32 k in LDS (fp16 hi | lo, 32 KiB), built
 // straight from the padded input.  Weights [kk][hi|lo][h][64][8], k = 16 kk + 8 h
 // + j = 9 ky + 3 kx + c (host: pack_x3_rgb), scaled by 2^s as pack_x3.  The layer
-// is then bound by its 64-channel fp32 output write.  8 waves, 64co x 64px each.
+// is then bound by its 64-channel fp32 output write (~4.1 TB/s of HBM traffic).  4 waves,
+// 64co x 64px each.
 // ---------------------------------------------------------------------------
-constexpr int RGB_BPX = 512, RGB_BCO = 64, RGB_NT = 512;
+constexpr int RGB_BCO = 64, RGB_TILE = 256;
 
-__global__ void __launch_bounds__(RGB_NT, 1) conv_x3_rgb(X3Args a) {
+template <int RGB_BPX>
+__global__ void __launch_bounds__(RGB_BPX, 1) conv_x3_rgb(X3Args a) {
+  constexpr int RGB_NT = RGB_BPX;
   __shared__ f16x8 s_x[2][4][RGB_BPX];          // [hi|lo][k chunk q][px]
   __shared__ f16x8 s_w[2][2][2][RGB_BCO];        // [kk][hi|lo][h][co]
   __shared__ float s_b[2 * RGB_BCO];             // bias, PReLU slope
@@ -648,20 +695,23 @@ hipError_t launch_conv_x3_rgb(const ConvLaunch& c, hipStream_t s) {
   a.in_pad = c.in_pad; a.out_pad = c.out_pad;
   a.H = c.H; a.W = c.W; a.cin_chunks = 1; a.pairs = 1; a.cout = c.cout;
   a.co_tiles = 1;
-  a.px_tiles = (c.H * c.W + RGB_BPX - 1) / RGB_BPX;
-  a.tpx = RGB_BPX;
+  // 256-pixel blocks: 3 % faster than 512 (more blocks resident per CU), 128 lost 16 %
+  // (tools/gpu_rgb_bpx.sh)
+  constexpr int bpx = RGB_TILE;
+  a.px_tiles = (c.H * c.W + bpx - 1) / bpx;
+  a.tpx = bpx;
   a.act = c.act;
   a.ksplit = 1;
   a.nfr = c.n;
   const long long nb = (long long)c.n * a.px_tiles;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3_rgb: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
-  hipLaunchKernelGGL(conv_x3_rgb, dim3(a.nblocks), dim3(RGB_NT), 0, s, a);
+  hipLaunchKernelGGL(conv_x3_rgb<bpx>, dim3(a.nblocks), dim3(bpx), 0, s, a);
   return hipGetLastError();
 }
 
 double conv_x3_rgb_mfma_flops(const ConvLaunch& c) {
-  return 3.0 * 2.0 * RGB_BCO * 32.0 * (double)((c.H * c.W + RGB_BPX - 1) / RGB_BPX) * RGB_BPX * c.n;
+  return 3.0 * 2.0 * RGB_BCO * 32.0 * (double)((c.H * c.W + RGB_TILE - 1) / RGB_TILE) * RGB_TILE * c.n;
 }
 
 // Split-K reduction: the ranges' sums added in range order (the order of the in-block
@@ -726,6 +776,16 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   if ((VAR & 4096) && ((c.cin_chunks + 1) / 2) % 2) { set_error("conv_x3: two pairs per step needs an even pair count"); return hipErrorInvalidValue; }
   X3Args a;
   a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
+  if (c.vin) {   // the pool's pair-max buffer: [n][chunk][2H][W][8], unpadded
+    if (c.in_coff) { set_error("conv_x3: pooled-input staging reads whole buffers"); return hipErrorInvalidValue; }
+    if ((long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) >= (1 << 20)) {
+      set_error("conv_x3: pooled-input plane too large for the staging index math");
+      return hipErrorInvalidValue;
+    }
+    a.in_chs = (long long)2 * c.H * c.W * 8;
+  }
+  a.vin = c.vin;
+  if (c.vin != ((VAR & 32768) != 0)) { set_error("conv_x3: pooled-input variant mismatch"); return hipErrorInvalidValue; }
   a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
   a.in_fs = a.in_chs * (c.in_cs / 8);
   a.out_fs = a.out_chs * (c.out_cs / 8);
@@ -933,6 +993,11 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
         }
       }
 #endif
+      if (c.vin) {
+        if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 32768, 4>(c, s);
+        set_error("conv_x3: pooled-input staging without a variant (x3_vin_ok)");
+        return hipErrorInvalidValue;
+      }
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 512, 4>(c, s);
         case 96: return launch_t<KS, 1, 16, 3, 1, 512, 4>(c, s);
@@ -946,6 +1011,16 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   }
   if constexpr (KS <= 3) {
     if (x3_big_tiles(c)) {
+      if constexpr (KS == 3) {
+        if (c.vin) {
+          if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 32768, 4>(c, s);
+          if (x3_half64(c)) return launch_t<KS, 1, 8, 2, 1, 32768, 2>(c, s);
+        }
+      }
+      if (c.vin) {
+        set_error("conv_x3: pooled-input staging without a variant (x3_vin_ok)");
+        return hipErrorInvalidValue;
+      }
       if (x3_half64(c)) return launch_t<KS, 1, 8, 2, 1, 0, 2>(c, s);   // 8 waves of 64co x 32px, 256 px
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 0, 4>(c, s);   // 16 waves, 64co x 64px each
@@ -1004,6 +1079,15 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
 }
 
 bool x3_fits(const ConvLaunch& c) { return c.in_pad >= c.ks / 2; }
+
+// Launches with a pooled-input variant (VAR 32768): 3x3 layers on the 512-pixel family
+// with 128-channel tiles (row union or generic) or the 256-pixel 64-channel blocks -- the
+// layers after the body's and hand's pools at batch sizes that fill the chip.  Others
+// take vpool2_kernel + the plain variant.
+bool x3_vin_ok(const ConvLaunch& c) {
+  return x3_fits(c) && c.ks == 3 && c.in_coff == 0 && x3_ranges(c).S == 1 && x3_big_tiles(c) &&
+         (c.bco == 128 || x3_half64(c)) && (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) < (1 << 20);
+}
 
 bool x3_hpool_ok(const ConvLaunch& c) {
   return x3_fits(c) && !(c.W & 1) && !(x3_ranges(c).S > 1 && x3_ranges(c).across_blocks);

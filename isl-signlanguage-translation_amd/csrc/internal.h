@@ -51,6 +51,11 @@ struct ConvLaunch {
   // max of each horizontal pixel pair into `out` as an unpadded [n][chunk][H][W/2][8]
   // buffer (out_pad 0); launch_vpool2 then takes the max of row pairs.
   int hpool = 0;
+  // The other half (conv_x3 only): `in` is such a pair-max buffer [n][chunk][2H][W][8] of
+  // the pool whose H x W output this conv reads; its staging takes the max of each row
+  // pair on the fly (the ring, in_pad wide, reads as zeros), so the pool kernel and its
+  // output buffer are skipped.  in_pad / in_cs / in_coff describe the pooled buffer.
+  int vin = 0;
 };
 
 // Pixels per tile of the flattened-raster conv kernels: BPX, or fewer when the
@@ -78,6 +83,8 @@ hipError_t launch_wino(const ConvLaunch& c, hipStream_t s);
 // used for a launch when x3_wide1(c with bco 256) says its grid is big enough.
 bool x3_wide1_layer(int ks, int cout, int cin_phys);
 bool x3_wide1(const ConvLaunch& c);
+// whether launch_conv_x3 has a pooled-input (ConvLaunch::vin) variant for this launch
+bool x3_vin_ok(const ConvLaunch& c);
 // conv1_1 (3 input channels in one chunk, 3x3, <= 64 outputs): K packed as the 27
 // real (ky, kx, c) values; c.wx3 then holds the pack_x3_rgb filters [kk][hi|lo][h][64][8].
 bool x3_rgb_fits(const ConvLaunch& c);

@@ -741,6 +741,30 @@ static bool fused_pool_enabled() {
   return !(e && e[0] == '0');
 }
 
+// ISLPOSE_POOL_INPUT=0: a fused pool's row-pair max runs as vpool2_kernel into the pooled
+// buffer instead of inside the next conv's staging (ConvLaunch::vin; A/B, read per run)
+static bool pool_input_enabled() {
+  const char* e = getenv("ISLPOSE_POOL_INPUT");
+  return !(e && e[0] == '0');
+}
+
+// Pool op k may leave its output unwritten and hand its pair-max buffer to op k+1 (vin):
+// op k+1 is an x3 conv (not the 3-channel rgb kernel) reading the whole pooled buffer,
+// which nothing else reads and which is no net output.
+static bool pool_into_next_conv(const isl_net* net, size_t k) {
+  const Op& op = net->ops[k];
+  if (k + 1 >= net->ops.size() || net->algo != ISL_ALGO_X3) return false;
+  const Op& nx = net->ops[k + 1];
+  if (nx.type != 0 || nx.in != op.out || nx.in_coff != 0) return false;
+  const ConvLayer& c = net->layers[nx.layer];
+  if (c.cin_phys / 8 == 1 || net->act[op.out].pad < c.k / 2 || net->act[op.out].cs != (op.C + 7) / 8 * 8)
+    return false;
+  if (net->out0.buf == op.out || (net->n_out > 1 && net->out1.buf == op.out)) return false;
+  for (size_t j = 0; j < net->ops.size(); ++j)
+    if (j != k + 1 && (net->ops[j].in == op.out || (j != k && net->ops[j].out == op.out))) return false;
+  return true;
+}
+
 static int run_ops(isl_net* net, hipStream_t s) {
   isl_net::TimedRun* tr = nullptr;
   if (net->timing) {
@@ -751,13 +775,16 @@ static int run_ops(isl_net* net, hipStream_t s) {
     HIP_OK(hipEventRecord(tr->ev[0], s));
   }
   bool fused = false;   // the previous conv wrote the pair-max buffer of this pool
-  const bool fuse_pools = fused_pool_enabled();
+  int vin_buf = -1;     // this conv stages from that buffer (the pool op was skipped)
+  const bool fuse_pools = fused_pool_enabled(), pool_input = fuse_pools && pool_input_enabled();
   for (size_t k = 0; k < net->ops.size(); ++k) {
     const Op& op = net->ops[k];
     const Act& in = net->act[op.in];
     const Act& out = net->act[op.out];
     if (op.type == 1) {
-      if (fused) HIP_OK(launch_vpool2(net->act[op.hbuf], out, op.C, s));
+      // deferred: the next conv either stages from the pair-max buffer or runs vpool2 first
+      if (fused && pool_input && pool_into_next_conv(net, k)) vin_buf = (int)k;
+      else if (fused) HIP_OK(launch_vpool2(net->act[op.hbuf], out, op.C, s));
       else HIP_OK(launch_maxpool2(in, out, op.C, s));
       fused = false;
       if (tr) {
@@ -781,13 +808,22 @@ static int run_ops(isl_net* net, hipStream_t s) {
       HIP_OK(launch_wino(L, s));
       kind = 2; mf = wino_mfma_flops(L);
 #ifdef ISLPOSE_DEV
-    } else if (net->algo == ISL_ALGO_X3 && c.d_wux3 && x3_wino_enabled()) {
+    } else if (net->algo == ISL_ALGO_X3 && c.d_wux3 && x3_wino_enabled() && vin_buf < 0) {
       L.wx3 = c.d_wux3; L.wscale_inv = c.wx3_inv;
       HIP_OK(launch_wino_x3(L, s));
       kind = 4; mf = wino_x3_mfma_flops(L);
 #endif
     } else if (net->algo == ISL_ALGO_X3 && x3_fits(L)) {
       L.allow_split = net->split_k;
+      if (vin_buf >= 0) {   // the preceding pool's row-pair max happens in this conv's staging
+        const Op& pool = net->ops[vin_buf];
+        const Act& hb = net->act[pool.hbuf];
+        ConvLaunch Lv = L;
+        Lv.in = hb.base; Lv.in_cs = hb.cs; Lv.in_coff = 0; Lv.vin = 1;
+        if (x3_vin_ok(Lv) && !(c.d_wrgb && x3_rgb_fits(L))) L = Lv;
+        else HIP_OK(launch_vpool2(hb, net->act[pool.out], pool.C, s));   // no variant: the pool after all
+        vin_buf = -1;
+      }
       if (c.x3_wide) {   // 256-channel tiles, two pairs per step, where the grid is big enough
         ConvLaunch Lw = L;
         Lw.bco = 256;
@@ -812,7 +848,7 @@ static int run_ops(isl_net* net, hipStream_t s) {
       }
       L.ws = net->d_ks;
       L.ws_floats = net->ks_floats;
-      if (c.d_wrgb && x3_rgb_fits(L) && rgb_kernel_enabled()) {
+      if (c.d_wrgb && x3_rgb_fits(L) && rgb_kernel_enabled() && !L.vin) {
         L.wx3 = c.d_wrgb;
         HIP_OK(launch_conv_x3_rgb(L, s));
         kind = 3; mf = conv_x3_rgb_mfma_flops(L);
@@ -824,6 +860,7 @@ static int run_ops(isl_net* net, hipStream_t s) {
       HIP_OK(launch_conv(L, s));
       mf = conv_mfma_flops(L);
     }
+    if (vin_buf >= 0) return fail(ISL_E_STATE, "pooled-input staging: the conv after a skipped pool did not take it");
     if (tr) {
       tr->kind.push_back(kind);
       tr->flops.push_back(2.0 * c.cout * c.cin * c.k * c.k * (double)in.H * in.W * in.n);

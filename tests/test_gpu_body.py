@@ -63,17 +63,24 @@ def test_body25_forward_algo_vs_oracle(net25, w25, algo):
     assert ep < TOL and eh < TOL, (ep, eh)
 
 
-@pytest.mark.parametrize("n,h,w", [(2, 184, 328), (1, 368, 656), (2, 50, 70), (3, 96, 136)])
+@pytest.mark.parametrize("n,h,w", [(2, 184, 328), (1, 368, 656), (2, 50, 70), (3, 96, 136), (8, 368, 656),
+                                   (16, 184, 328)])
 def test_fused_pool_bit_identical(net25, n, h, w, monkeypatch):
     """conv1_2 / conv2_2 / conv3_4 writing horizontal pair maxima (ConvLaunch::hpool) +
-    the row-pair pool == conv + maxpool2, bit for bit (max is exact); odd widths
-    (50x70's 25x35 level) take the plain path."""
+    the row-pair max inside the next conv's staging (ConvLaunch::vin, on chip-filling
+    grids: 8 x 368x656 takes it after all three pools, 16 x 184x328 after two and
+    vpool2_kernel for the third) or in vpool2_kernel (ISLPOSE_POOL_INPUT=0) == conv +
+    maxpool2, bit for bit (max is exact); odd widths (50x70's 25x35 level) take the plain
+    path."""
     x = torch.from_numpy(_inputs(n, h, w, seed=h + w)).cuda()
     paf0, heat0 = net25.forward(x)
+    monkeypatch.setenv("ISLPOSE_POOL_INPUT", "0")
+    paf2, heat2 = net25.forward(x)
     monkeypatch.setenv("ISLPOSE_FUSED_POOL", "0")
     paf1, heat1 = net25.forward(x)
     torch.cuda.synchronize()
     assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
+    assert torch.equal(paf2, paf1) and torch.equal(heat2, heat1)
 
 
 @pytest.mark.parametrize("n,h,w", [(2, 184, 328), (1, 50, 70)])

@@ -175,10 +175,13 @@ __global__ void __launch_bounds__(256) resize_sep_kernel(MapSrc m, int nch, int 
     if (mode == 1) {
       ((float*)out)[i] = v;
     } else {
+      // mode | 8: the first scale -- the accumulator is the reference's np.zeros, so it
+      // starts from +0.0 here instead of a memset pass (same bits, 0.0 + x included)
       double* o = (double*)out + i;
+      const double o0 = (mode & 8) ? 0.0 : *o;
       const float q = v / inv_div_f;   // heatmap / len(multiplier), float32
-      if (mode == 2) *o = *o + (*o + (double)q);   // body.py:80, the doubling quirk
-      else *o = *o + (double)q;                    // hand.py:56
+      if ((mode & 7) == 2) *o = o0 + (o0 + (double)q);   // body.py:80, the doubling quirk
+      else *o = o0 + (double)q;                          // hand.py:56
     }
   }
 }
@@ -1809,7 +1812,6 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
 
   hipLaunchKernelGGL(init_records_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (char*)d_result, lay, n, nlimbs);
   PHIP(hipGetLastError());
-  if (multi) PHIP(hipMemsetAsync(heat, 0, heat_bytes, s));
 
   GroupArgs ga;
   memset(&ga, 0, sizeof(ga));
@@ -1851,7 +1853,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       fp = lp;
     }
     if (fused) fused_src = fh;   // no full-resolution heat: blur_nms resizes on the fly
-    else if ((rc = launch_resize(fh, n, nparts, H, W, multi ? 2 : 1, div_f, heat, s))) return rc;
+    else if ((rc = launch_resize(fh, n, nparts, H, W, multi ? (si == 0 ? 2 | 8 : 2) : 1, div_f, heat, s))) return rc;
     ga.paf[si] = fp;
   }
   // blur + NMS (body.py:86-100)
@@ -1937,7 +1939,6 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
   double* vals = (double*)((char*)parent + up(par_bytes));
   CcStats* stats = (CcStats*)((char*)vals + up(val_bytes));
   CcChunk* cks = (CcChunk*)((char*)stats + up(st_bytes));
-  PHIP(hipMemsetAsync(avg, 0, avg_bytes, s));
   const float div_f = (float)nscales;
   for (int si = 0; si < nscales; ++si) {
     const isl_scale_geom& g = geom[si];
@@ -1956,7 +1957,7 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
       fh.scy = 1.0 / ((double)h / g.valid_h); fh.scx = 1.0 / ((double)w / g.valid_w);
       fh.cn = nch; fh.identity = 0;
     }
-    if ((rc = launch_resize(fh, n, nparts, h, w, 3, div_f, avg, s))) return rc;
+    if ((rc = launch_resize(fh, n, nparts, h, w, si == 0 ? 3 | 8 : 3, div_f, avg, s))) return rc;
   }
   dim3 gb((w + NMS_TX - 1) / NMS_TX, (h + NMS_TY - 1) / NMS_TY, n * nparts);
   hipLaunchKernelGGL((blur_nms_kernel<double, false>), gb, dim3(256), 0, s, (const double*)avg, h, w, words, mask, 0.05,

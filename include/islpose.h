@@ -211,6 +211,21 @@ int isl_body_post(isl_net* net, int n, int H, int W, int nscales, const isl_scal
 int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, const isl_scale_geom* geom,
                   const float* const* d_heat, int64_t* d_peaks, void* stream);
 
+/* Hand post-processing of n square crops of different sizes in one call
+ * (HandEstimator.post_crops; hand.py:51-74 per crop): crop i is crop_w[i] px (host
+ * array), geom[i*nscales + si] its geometry at scale si (host), its low-res maps crop
+ * i of d_heat[si] (NCHW [n,22,net_h/8,net_w/8]; every crop has the same net size per
+ * scale) -> int64 peaks [n][21][2].  Stream-ordered on `stream`: the crops run side by
+ * side on the net's internal post streams, forked from and joined back into it. */
+int isl_hand_post_crops(isl_net* net, int n, const int32_t* crop_w, int nscales,
+                        const isl_scale_geom* geom, const float* const* d_heat, int64_t* d_peaks,
+                        void* stream);
+
+/* Diagnostic: numpy's np.sum of a float64 array (pairwise 8192-element buffers added
+ * left to right, hand.py:68's association) as the hand post computes it for component
+ * sums (the block-cooperative device routine): d_out[0] = sum(d_a[0..n)). */
+int isl_debug_np_sum(const double* d_a, int64_t n, double* d_out, void* stream);
+
 /* Sign classifier of ISLSignPosTranslator (reference demo_isl_translate.py:72-100,
  * applied in src/ISL_Model_parameter.py:337 to a [1,20,156] window of
  * populate_features rows, :376-443): Masking(0) -> BatchNorm -> BiLSTM(32, seq)

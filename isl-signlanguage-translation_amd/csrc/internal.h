@@ -145,4 +145,15 @@ int net_device(const isl_net* net);
 int net_low_res(isl_net* net, int which, MapSrc* m);
 // grow-only device scratch owned by the net (nullptr + error on failure)
 void* net_scratch(isl_net* net, size_t bytes);
+// streams on which isl_hand_post_crops runs its crops side by side, forked from and
+// joined back into the caller's stream; a grow-only scratch per lane
+constexpr int ISL_POST_LANES = 4;
+struct PostLanes {
+  hipStream_t stream[ISL_POST_LANES];
+  hipEvent_t fork, join[ISL_POST_LANES];
+  void* scratch[ISL_POST_LANES];
+  size_t bytes[ISL_POST_LANES];
+};
+// created on first use (nullptr + error on failure), destroyed with the net
+PostLanes* net_post_lanes(isl_net* net);
 }  // namespace isl

@@ -999,7 +999,24 @@ __device__ double np_sum_block(const double* a, int n) {
   for (int g = 0; g < nfull; g += nw) {
     const int b = g + wave;
     if (b < nfull) {
-      double v = np_leaf(a + (size_t)b * 8192 + lane * 128, 128);
+      // the 64 leaves of 128, eight at a time: lane j of a group of 8 keeps np_leaf's
+      // accumulator r[j] (coalesced 64-byte rows instead of a 1 KiB-strided leaf per
+      // lane), then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) as xor butterflies (a + b ==
+      // b + a exactly); leaf 8k+g ends in lane 8k+g
+      const double* buf = a + (size_t)b * 8192;
+      const int g8 = lane >> 3, j8 = lane & 7;
+      double v = 0.0;
+      for (int k = 0; k < 8; ++k) {
+        const double* leaf = buf + (k * 8 + g8) * 128 + j8;
+        double r = leaf[0];
+#pragma unroll
+        for (int i = 8; i < 128; i += 8) r += leaf[i];
+        r += __shfl_xor(r, 1, 64);
+        r += __shfl_xor(r, 2, 64);
+        r += __shfl_xor(r, 4, 64);
+        const double t = __shfl(r, (lane & 7) * 8, 64);   // group (lane & 7) holds leaf 8k + (lane & 7)
+        if (g8 == k) v = t;
+      }
 #pragma unroll
       for (int half = 32; half >= 1; half >>= 1) {
         const double x0 = __shfl(v, 2 * lane, 64), x1 = __shfl(v, 2 * lane + 1, 64);
@@ -1053,6 +1070,11 @@ __device__ double np_sum_block(const double* a, int n) {
   const double r = s_tot;
   __syncthreads();
   return r;
+}
+
+__global__ void __launch_bounds__(1024) np_sum_debug_kernel(const double* a, int n, double* out) {
+  const double s = np_sum_block(a, n);
+  if (threadIdx.x == 0) out[0] = s;
 }
 
 // np.sum of a contiguous float64 array: pairwise sums of 8192-element buffers, added left to right
@@ -1199,16 +1221,16 @@ __global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ 
   const int* parent = parent_all + (size_t)plane * P;
   const double* map = planes + (size_t)plane * P;
   double* vals = vals_all + (size_t)plane * P;
-  const int per = (p1 - p0 + 255) / 256;                    // a contiguous run per thread
-  const int a = min(p1, p0 + threadIdx.x * per), b = min(p1, a + per);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
   // runs of equal roots in registers (flushed on a root change); the last run of every
-  // thread is combined across the wave, then across the block, when the roots agree
+  // thread is combined across the wave, then across the block, when the roots agree.
+  // Block-strided pixels: every load is one coalesced row segment (a contiguous run per
+  // thread made each load touch 64 cache lines)
   int cnt = 0, cur = -1;
   double acc = 0.0;
-  for (int p = a; p < b; ++p) {
+  for (int p = p0 + threadIdx.x; p < p1; p += 256) {
     const int r = parent[p];
     if (r < 0) continue;
     ++cnt;
@@ -1351,8 +1373,6 @@ __global__ void __launch_bounds__(256) cc_scatter_kernel(const double* __restric
   double* vals = vals_all + (size_t)plane * P;
   const CcChunk* pc = ck + (size_t)plane * chunks;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int per = (p1 - p0 + 255) / 256;
-  const int a = min(p1, p0 + threadIdx.x * per), b = min(p1, a + per);
   for (int k = 0; k < nk; ++k) {
     const int root = stats[plane].cand[k];
     if (threadIdx.x == 0) {   // region of candidate k, then this chunk's place in it
@@ -1362,21 +1382,23 @@ __global__ void __launch_bounds__(256) cc_scatter_kernel(const double* __restric
       for (int cc = 0; cc < c; ++cc) base += pc[cc].count[k];
       s_base = base;
     }
-    int cnt = 0;
-    for (int p = a; p < b; ++p) cnt += parent[p] == root;
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += y;
+    __syncthreads();
+    int o = s_base;
+    // raster order, 256-pixel segments: each thread one pixel per segment (coalesced),
+    // its slot = the segment's base + the members before it (ballot prefix per wave,
+    // wave totals through LDS)
+    for (int s0 = p0; s0 < p1; s0 += 256) {
+      const int p = s0 + threadIdx.x;
+      const bool in = p < p1 && parent[p] == root;
+      const unsigned long long bal = __ballot(in);
+      if (lane == 0) s_w[wave] = __popcll(bal);
+      __syncthreads();
+      int before = o;
+      for (int q = 0; q < wave; ++q) before += s_w[q];
+      if (in) vals[before + __popcll(bal & ((1ull << lane) - 1ull))] = map[p];
+      o += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+      __syncthreads();
     }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    int o = s_base + incl - cnt;
-    for (int q = 0; q < wave; ++q) o += s_w[q];
-    for (int p = a; p < b; ++p)
-      if (parent[p] == root) vals[o++] = map[p];
-    __syncthreads();
   }
 }
 
@@ -1908,15 +1930,9 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   return ISL_OK;
 }
 
-extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, const isl_scale_geom* geom,
-                             const float* const* d_heat, int64_t* d_peaks, void* stream) {
-  if (!net || n <= 0 || h <= 0 || w <= 0 || nscales <= 0 || nscales > MAX_SCALES || !geom || !d_peaks)
-    return post_fail(ISL_E_ARG, "isl_hand_post: bad argument");
-  if (net_kind(net) != ISL_HAND) return post_fail(ISL_E_ARG, "isl_hand_post needs the hand net");
-  if (nscales > 1 && !d_heat) return post_fail(ISL_E_ARG, "isl_hand_post: maps required for several scales");
-  PHIP(hipSetDevice(net_device(net)));
-  hipStream_t s = (hipStream_t)stream;
-  const int nparts = 21, nch = 22;
+// scratch bytes of one hand post of n crops of h x w (layout: hand_post_launch)
+static size_t hand_post_bytes(int n, int h, int w, int nscales, const isl_scale_geom* geom) {
+  const int nparts = 21;
   const size_t P = (size_t)h * w;
   const int words = (w + 63) / 64;
   size_t mid_bytes = 0;
@@ -1929,9 +1945,25 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
   const size_t st_bytes = (size_t)n * nparts * sizeof(CcStats);
   const int cc_rows = std::max(1, CC_CHUNK / w), cc_chunks = (h + cc_rows - 1) / cc_rows;
   const size_t ck_bytes = (size_t)n * nparts * cc_chunks * sizeof(CcChunk);
-  char* base = (char*)net_scratch(net, up(avg_bytes) + up(mid_bytes) + up(mask_bytes) + up(par_bytes) + up(val_bytes) +
-                                           up(st_bytes) + up(ck_bytes));
-  if (!base) return ISL_E_HIP;
+  return up(avg_bytes) + up(mid_bytes) + up(mask_bytes) + up(par_bytes) + up(val_bytes) + up(st_bytes) + up(ck_bytes);
+}
+
+// the kernels of one hand post (hand.py:51-74) on stream s, scratch at base
+// (hand_post_bytes); heat planes of scale si at d_heat[si] (NULL: the arena output)
+static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, const isl_scale_geom* geom,
+                            const float* const* d_heat, int64_t* d_peaks, hipStream_t s, char* base) {
+  const int nparts = 21, nch = 22;
+  const size_t P = (size_t)h * w;
+  const int words = (w + 63) / 64;
+  size_t mid_bytes = 0;
+  for (int si = 0; si < nscales; ++si)
+    if (!(geom[si].valid_h == h && geom[si].valid_w == w))
+      mid_bytes = std::max(mid_bytes, (size_t)n * geom[si].valid_h * geom[si].valid_w * nparts * 4);
+  auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t avg_bytes = (size_t)n * nparts * P * 8, mask_bytes = (size_t)n * nparts * h * words * 8;
+  const size_t par_bytes = (size_t)n * nparts * P * 4, val_bytes = (size_t)n * nparts * P * 8;
+  const size_t st_bytes = (size_t)n * nparts * sizeof(CcStats);
+  const int cc_rows = std::max(1, CC_CHUNK / w), cc_chunks = (h + cc_rows - 1) / cc_rows;
   double* avg = (double*)base;
   float* mid = (float*)(base + up(avg_bytes));
   unsigned long long* mask = (unsigned long long*)((char*)mid + up(mid_bytes));
@@ -1988,6 +2020,81 @@ extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, con
     hipLaunchKernelGGL((hand_cc_kernel<false, true>), dim3(n * nparts), dim3(CC_NT), 0, s, (const double*)avg, mask,
                        h, w, words, parent, vals, stats, cks, chunks, (long long*)d_peaks);
   }
+  PHIP(hipGetLastError());
+  return ISL_OK;
+}
+
+extern "C" int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, const isl_scale_geom* geom,
+                             const float* const* d_heat, int64_t* d_peaks, void* stream) {
+  if (!net || n <= 0 || h <= 0 || w <= 0 || nscales <= 0 || nscales > MAX_SCALES || !geom || !d_peaks)
+    return post_fail(ISL_E_ARG, "isl_hand_post: bad argument");
+  if (net_kind(net) != ISL_HAND) return post_fail(ISL_E_ARG, "isl_hand_post needs the hand net");
+  if (nscales > 1 && !d_heat) return post_fail(ISL_E_ARG, "isl_hand_post: maps required for several scales");
+  PHIP(hipSetDevice(net_device(net)));
+  char* base = (char*)net_scratch(net, hand_post_bytes(n, h, w, nscales, geom));
+  if (!base) return ISL_E_HIP;
+  return hand_post_launch(net, n, h, w, nscales, geom, d_heat, d_peaks, (hipStream_t)stream, base);
+}
+
+// Crops of different sizes in one call (HandEstimator.post_crops): crop i is a square of
+// crop_w[i] px, geom[i * nscales + si] its scale geometries, its low-res maps crop i of
+// d_heat[si] ([n,22,net_h/8,net_w/8]: every crop has the same net size per scale).  Each
+// crop's kernel chain is small (21 planes), so the crops run on ISL_POST_LANES streams
+// forked from `stream` and joined back into it, each lane with its own grow-only scratch.
+extern "C" int isl_hand_post_crops(isl_net* net, int n, const int32_t* crop_w, int nscales,
+                                   const isl_scale_geom* geom, const float* const* d_heat, int64_t* d_peaks,
+                                   void* stream) {
+  if (!net || n <= 0 || !crop_w || nscales <= 0 || nscales > MAX_SCALES || !geom || !d_heat || !d_peaks)
+    return post_fail(ISL_E_ARG, "isl_hand_post_crops: bad argument");
+  if (net_kind(net) != ISL_HAND) return post_fail(ISL_E_ARG, "isl_hand_post_crops needs the hand net");
+  for (int i = 0; i < n; ++i) {
+    if (crop_w[i] <= 0) return post_fail(ISL_E_ARG, "isl_hand_post_crops: bad crop size");
+    for (int si = 0; si < nscales; ++si)
+      if (geom[i * nscales + si].net_h != geom[si].net_h || geom[i * nscales + si].net_w != geom[si].net_w)
+        return post_fail(ISL_E_ARG, "isl_hand_post_crops: crops differ in net size");
+  }
+  PHIP(hipSetDevice(net_device(net)));
+  hipStream_t s = (hipStream_t)stream;
+  PostLanes* L = net_post_lanes(net);
+  if (!L) return ISL_E_HIP;
+  const int nl = std::min(n, ISL_POST_LANES);
+  // lane k takes crops k, k + nl, ...; size its scratch for the largest first, before any
+  // launch of this call (a grown buffer is reallocated only once its lane has drained)
+  for (int k = 0; k < nl; ++k) {
+    size_t need = 0;
+    for (int i = k; i < n; i += nl) need = std::max(need, hand_post_bytes(1, crop_w[i], crop_w[i], nscales, geom + (size_t)i * nscales));
+    if (need > L->bytes[k]) {
+      PHIP(hipStreamSynchronize(L->stream[k]));
+      if (L->scratch[k]) PHIP(hipFree(L->scratch[k]));
+      L->scratch[k] = nullptr;
+      L->bytes[k] = 0;
+      PHIP(hipMalloc(&L->scratch[k], need));
+      L->bytes[k] = need;
+    }
+  }
+  PHIP(hipEventRecord(L->fork, s));
+  for (int k = 0; k < nl; ++k) PHIP(hipStreamWaitEvent(L->stream[k], L->fork, 0));
+  for (int i = 0; i < n; ++i) {
+    const int k = i % nl;
+    const float* hp[MAX_SCALES];
+    for (int si = 0; si < nscales; ++si) {
+      const isl_scale_geom& g = geom[si];
+      hp[si] = d_heat[si] + (size_t)i * 22 * (g.net_h / 8) * (g.net_w / 8);
+    }
+    const int rc = hand_post_launch(net, 1, crop_w[i], crop_w[i], nscales, geom + (size_t)i * nscales, hp,
+                                    d_peaks + (size_t)i * 42, L->stream[k], (char*)L->scratch[k]);
+    if (rc) return rc;
+  }
+  for (int k = 0; k < nl; ++k) {
+    PHIP(hipEventRecord(L->join[k], L->stream[k]));
+    PHIP(hipStreamWaitEvent(s, L->join[k], 0));
+  }
+  return ISL_OK;
+}
+
+extern "C" int isl_debug_np_sum(const double* d_a, int64_t n, double* d_out, void* stream) {
+  if (!d_a || !d_out || n <= 0 || n > (1ll << 30)) return post_fail(ISL_E_ARG, "isl_debug_np_sum: bad argument");
+  hipLaunchKernelGGL(np_sum_debug_kernel, dim3(1), dim3(CC_NT), 0, (hipStream_t)stream, d_a, (int)n, d_out);
   PHIP(hipGetLastError());
   return ISL_OK;
 }

@@ -217,6 +217,7 @@ struct isl_net {
   // post scratch
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  PostLanes* lanes = nullptr;   // isl_hand_post_crops (net_post_lanes)
   // split-K partial sums of the x3 convs on small grids (grow-only)
   float* d_ks = nullptr;
   size_t ks_floats = 0;
@@ -903,6 +904,25 @@ void* net_scratch(isl_net* net, size_t bytes) {
   return net->scratch;
 }
 
+PostLanes* net_post_lanes(isl_net* net) {
+  if (net->lanes) return net->lanes;
+  PostLanes* L = new PostLanes();
+  hipError_t e = hipEventCreateWithFlags(&L->fork, hipEventDisableTiming);
+  for (int k = 0; k < ISL_POST_LANES && e == hipSuccess; ++k) {
+    L->scratch[k] = nullptr;
+    L->bytes[k] = 0;
+    e = hipStreamCreateWithFlags(&L->stream[k], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&L->join[k], hipEventDisableTiming);
+  }
+  if (e != hipSuccess) {
+    set_error(std::string("post lanes: ") + hipGetErrorString(e));
+    delete L;   // (a partial set of streams/events is leaked on this failure path only)
+    return nullptr;
+  }
+  net->lanes = L;
+  return L;
+}
+
 }  // namespace isl
 
 // ---------------------------------------------------------------------------
@@ -959,6 +979,16 @@ int isl_net_destroy(isl_net* net) {
   if (net->d_tab) (void)hipFree(net->d_tab);
   for (auto& kv : net->plans) (void)hipFree(kv.second.base);
   if (net->scratch) (void)hipFree(net->scratch);
+  if (net->lanes) {
+    for (int k = 0; k < ISL_POST_LANES; ++k) {
+      (void)hipStreamSynchronize(net->lanes->stream[k]);
+      if (net->lanes->scratch[k]) (void)hipFree(net->lanes->scratch[k]);
+      (void)hipStreamDestroy(net->lanes->stream[k]);
+      (void)hipEventDestroy(net->lanes->join[k]);
+    }
+    (void)hipEventDestroy(net->lanes->fork);
+    delete net->lanes;
+  }
   if (net->d_ks) (void)hipFree(net->d_ks);
   for (auto& r : net->timed)
     for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);

@@ -96,15 +96,20 @@ class HandEstimator:
     def post_crops(self, boxes, heats):
         """isl_hand_post per crop (its resize-back target is the crop size) -> int64 [n,21,2]."""
         import torch
-        n = len(boxes)
+        n, ns = len(boxes), len(heats)
         out = torch.empty((n, 21, 2), dtype=torch.int64, device=heats[0].device)
-        # largest crop first: its post sizes the net's grow-only scratch once, so no
-        # later (queued) post reallocates it under an earlier one
-        for i in sorted(range(n), key=lambda k: -boxes[k][3]):
-            w = boxes[i][3]
-            geoms = [g[1:] for g in scale_geometry(w, w, self.scale_search)]
-            assert all((g[0], g[1]) == (hh.shape[2] * 8, hh.shape[3] * 8) for g, hh in zip(geoms, heats))
-            self.post_maps(w, w, geoms, [hh[i:i + 1] for hh in heats], out=out[i:i + 1])
+        # one call: the crops' kernel chains run side by side on the net's post streams
+        ws = (ctypes.c_int32 * n)(*[b[3] for b in boxes])
+        g = (rt.IslScaleGeom * (n * ns))()
+        for i, b in enumerate(boxes):
+            geoms = [gg[1:] for gg in scale_geometry(b[3], b[3], self.scale_search)]
+            assert all((gg[0], gg[1]) == (hh.shape[2] * 8, hh.shape[3] * 8) for gg, hh in zip(geoms, heats))
+            for si, gg in enumerate(geoms):
+                g[i * ns + si] = rt.IslScaleGeom(*gg)
+        assert all(hh.is_contiguous() for hh in heats)
+        hp = (ctypes.c_void_p * ns)(*[rt.ptr(hh).value for hh in heats])
+        rt.check(rt.lib().isl_hand_post_crops(self.net.h, n, ws, ns, g, hp, rt.ptr(out), rt.stream_handle()),
+                 "isl_hand_post_crops")
         return out.cpu().numpy()
 
     def estimate(self, crops):

@@ -24,7 +24,8 @@ EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destr
            "isl_net_param_info", "isl_net_set_param", "isl_net_forward", "isl_net_preprocess", "isl_net_run", "isl_net_debug_input",
            "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post",
            "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops",
-           "isl_sign_param_count", "isl_sign_classify", "isl_net_set_split_k", "isl_net_arena_info"]
+           "isl_sign_param_count", "isl_sign_classify", "isl_net_set_split_k", "isl_net_arena_info",
+           "isl_debug_np_sum", "isl_hand_post_crops"]
 
 
 class IslCaps(ctypes.Structure):
@@ -90,6 +91,9 @@ def lib():
     L.isl_net_set_split_k.argtypes = [vp, i32]
     L.isl_net_arena_info.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i32)]
     L.isl_sign_classify.argtypes = [vp, i32, i32, i32, vp, i32, vp, vp]
+    L.isl_debug_np_sum.argtypes = [vp, i64, vp, vp]
+    L.isl_hand_post_crops.argtypes = [vp, i32, ctypes.POINTER(i32), i32, ctypes.POINTER(IslScaleGeom),
+                                      ctypes.POINTER(vp), vp, vp]
     for name in EXPORTS[2:]:
         getattr(L, name).restype = i32
     if L.isl_abi_version() != 1:

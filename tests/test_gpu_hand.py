@@ -69,6 +69,23 @@ def test_hand_post_large_and_dense(hest, h, w, dense):
         assert np.array_equal(got[i], ref), i
 
 
+@pytest.mark.parametrize("n", [1, 7, 8, 100, 128, 129, 1000, 8192, 8193, 16384 + 77, 50000, 360000])
+def test_np_sum_association_bit_exact(n):
+    """The device np.sum that ranks tied hand components (hand.py:68) against numpy's
+    own np.sum, bit for bit, on values spread over 16 decades (where the association
+    of the additions shows in the result): partial trees, full 8192-element buffers
+    summed eight lanes per leaf, several buffers added left to right."""
+    import ctypes
+    from islpose import runtime as rt
+    rng = np.random.RandomState(n)
+    a = rng.standard_normal(n) * 10.0 ** rng.uniform(-8, 8, n)
+    d = torch.from_numpy(a).cuda()
+    out = torch.zeros(1, dtype=torch.float64, device="cuda")
+    rt.check(rt.lib().isl_debug_np_sum(rt.ptr(d), n, rt.ptr(out), rt.stream_handle()), "isl_debug_np_sum")
+    got = out.cpu().numpy()[0]
+    assert got.tobytes() == np.sum(a).tobytes(), (n, got, np.sum(a), float(np.sum(a.astype(np.longdouble))))
+
+
 def test_hand_estimate_end_to_end(hest):
     crops = synth.synth_frames(2, 96, 96, seed=11)
     t = torch.from_numpy(crops).cuda()

@@ -1,0 +1,14 @@
+# Hand post (CC path) check: hand GPU tests, C5 (overlapped) and a hand-post timing on dense maps.
+# usage: bash tools/gpu_hcc.sh <tag>
+export TMPDIR=/tmp
+T=${1:-hcc}; O=gpurun_out/$T; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_hand.py -v --timeout 120 --timeout-method thread > $O/hand_tests.log 2>&1
+rc=$?
+tail -3 $O/hand_tests.log
+if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $O/hand_tests.log | head -20; exit $rc; fi
+timeout -k 10 300 python3 -u tools/hand_post_timing.py > $O/hand_post_timing.txt 2>&1 &&
+timeout -k 10 600 python3 -u tools/bench_configs.py --config c5 > $O/c5.json 2> $O/c5.err &&
+timeout -k 10 600 python3 -u tools/bench_configs.py --config c3 > $O/c3.json 2>> $O/c5.err
+rc=$?
+cat $O/hand_post_timing.txt $O/c5.json $O/c3.json
+exit $rc

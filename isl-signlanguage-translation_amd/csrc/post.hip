@@ -186,6 +186,84 @@ __global__ void __launch_bounds__(256) resize_sep_kernel(MapSrc m, int nch, int 
   }
 }
 
+// The hand average over the scales in one pass (hand.py:51-56): for every output pixel
+// the final resize of each scale (resize_sep_kernel's arithmetic: horizontal pass into
+// LDS, vertical combine) and heatmap_avg += heatmap / len(multiplier) in scale order in
+// fp64 registers, one store.  The same bits as a mode-(3|8) pass then ns-1 mode-3 passes,
+// without their ns read-modify-write sweeps of the fp64 average.
+constexpr int RA_TY = 16;   // output rows per block (fp64 accumulators in registers)
+struct MapSrcN {   // up to MAX_SCALES (8) scales
+  MapSrc m[8];
+};
+__global__ void __launch_bounds__(256) resize_acc_kernel(MapSrcN ms, int ns, int nch, int oh, int ow, int ty_rows,
+                                                         float div_f, double* out) {
+  __shared__ float s_h[RS_MAXR][RS_TX];
+  const int plane = blockIdx.x, f = plane / nch, c = plane - f * nch;
+  const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * RS_TX + threadIdx.x;
+  const int ny = min(ty_rows, oh - y0);
+  double acc[RA_TY];
+#pragma unroll
+  for (int t = 0; t < RA_TY; ++t) acc[t] = 0.0;
+  for (int si = 0; si < ns; ++si) {
+    const MapSrc& m = ms.m[si];
+    const float* b = m.base + (size_t)f * m.fs + chan_off(m, c);
+    int r_lo = y0, nr = ny;
+    if (!m.identity) {
+      int lo[4], hi[4];
+      float dummy[4];
+      taps(y0, m.scy, m.sh, lo, dummy);
+      taps(y0 + ny - 1, m.scy, m.sh, hi, dummy);
+      r_lo = lo[0];
+      nr = hi[3] - r_lo + 1;
+    }
+    if (nr > RS_MAXR) __builtin_trap();   // the host sizes ty_rows so that this cannot happen
+    __syncthreads();                      // the previous scale's vertical pass is done with s_h
+    if (x < ow) {
+      if (m.identity) {
+        for (int r = 0; r < nr; ++r) s_h[r][threadIdx.x] = b[(size_t)(r_lo + r) * m.ys + (size_t)x * m.xs];
+      } else {
+        int xi[4];
+        float a[4];
+        taps(x, m.scx, m.sw, xi, a);
+        const long long o0 = xi[0] * m.xs, o1 = xi[1] * m.xs, o2 = xi[2] * m.xs, o3 = xi[3] * m.xs;
+        for (int r = 0; r < nr; ++r) {
+          const float* row = b + (size_t)(r_lo + r) * m.ys;
+          s_h[r][threadIdx.x] = ((row[o0] * a[0] + row[o1] * a[1]) + row[o2] * a[2]) + row[o3] * a[3];
+        }
+      }
+    }
+    __syncthreads();
+    if (x < ow) {
+      const int rowlen = m.dw * m.cn, body = rowlen - rowlen % 4;
+      const bool simd = x * m.cn + c < body;
+#pragma unroll
+      for (int t = 0; t < RA_TY; ++t) {
+        if (t >= ny) break;
+        float v;
+        if (m.identity) {
+          v = s_h[t][threadIdx.x];
+        } else {
+          int yi[4];
+          float be[4];
+          taps(y0 + t, m.scy, m.sh, yi, be);
+          const float h0 = s_h[yi[0] - r_lo][threadIdx.x], h1 = s_h[yi[1] - r_lo][threadIdx.x];
+          const float h2 = s_h[yi[2] - r_lo][threadIdx.x], h3 = s_h[yi[3] - r_lo][threadIdx.x];
+          v = simd ? h0 * be[0] + (h1 * be[1] + (h2 * be[2] + h3 * be[3]))
+                   : ((h0 * be[0] + h1 * be[1]) + h2 * be[2]) + h3 * be[3];
+        }
+        const float q = v / div_f;      // heatmap / len(multiplier), float32
+        acc[t] = acc[t] + (double)q;    // hand.py:56, from np.zeros (0.0 + x included)
+      }
+    }
+  }
+  if (x >= ow) return;
+#pragma unroll
+  for (int t = 0; t < RA_TY; ++t) {
+    if (t >= ny) break;
+    out[((size_t)plane * oh + y0 + t) * ow + x] = acc[t];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // fp64 blur + NMS
 // ---------------------------------------------------------------------------
@@ -573,6 +651,7 @@ __global__ void __launch_bounds__(256) compact_kernel(const unsigned long long* 
 // ---------------------------------------------------------------------------
 
 constexpr int MAX_SCALES = 8;
+static_assert(sizeof(MapSrcN::m) / sizeof(MapSrc) == MAX_SCALES, "resize_acc_kernel takes every scale");
 
 struct GroupArgs {
   MapSrc paf[MAX_SCALES];   // final-resolution PAF of each scale (sampled on demand)
@@ -1118,10 +1197,12 @@ __device__ __forceinline__ void cc_root_sums(PT parent, const double* map, doubl
     }
     acc += map[p];
   }
-  if (__all(cur == __shfl(cur, 0, 64)) && cur >= 0) {
+  const unsigned long long act = __ballot(cur >= 0);      // lanes without foreground: no vote
+  const int r0 = act ? __shfl(cur, __builtin_ctzll(act), 64) : -1;
+  if (act && __all(cur < 0 || cur == r0)) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&vals[cur], acc);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&vals[r0], acc);
   } else if (cur >= 0) {
     atomicAdd(&vals[cur], acc);
   }
@@ -1241,11 +1322,16 @@ __global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ 
     }
     acc += map[p];
   }
-  const bool wave_same = __all(cur == __shfl(cur, 0, 64));
+  // lanes that met no foreground pixel (cur < 0, acc 0) do not break the agreement:
+  // otherwise a plane that is one giant component with background lanes would flush
+  // every lane's sum into the same root with its own fp64 atomic
+  const unsigned long long act = __ballot(cur >= 0);
+  const int r0 = act ? __shfl(cur, __builtin_ctzll(act), 64) : -1;
+  const bool wave_same = __all(cur < 0 || cur == r0);
   if (wave_same) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (lane == 0) { s_root[wave] = cur; s_sum[wave] = acc; }
+    if (lane == 0) { s_root[wave] = r0; s_sum[wave] = acc; }   // r0 = -1: nothing to add
   } else {
     if (cur >= 0) atomicAdd(&vals[cur], acc);
     if (lane == 0) s_root[wave] = -2;                       // flushed already
@@ -1935,10 +2021,10 @@ static size_t hand_post_bytes(int n, int h, int w, int nscales, const isl_scale_
   const int nparts = 21;
   const size_t P = (size_t)h * w;
   const int words = (w + 63) / 64;
-  size_t mid_bytes = 0;
+  size_t mid_bytes = 0;   // every scale's intermediate stays until the fused average
   for (int si = 0; si < nscales; ++si)
     if (!(geom[si].valid_h == h && geom[si].valid_w == w))
-      mid_bytes = std::max(mid_bytes, (size_t)n * geom[si].valid_h * geom[si].valid_w * nparts * 4);
+      mid_bytes += (size_t)n * geom[si].valid_h * geom[si].valid_w * nparts * 4;
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t avg_bytes = (size_t)n * nparts * P * 8, mask_bytes = (size_t)n * nparts * h * words * 8;
   const size_t par_bytes = (size_t)n * nparts * P * 4, val_bytes = (size_t)n * nparts * P * 8;
@@ -1955,10 +2041,10 @@ static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, cons
   const int nparts = 21, nch = 22;
   const size_t P = (size_t)h * w;
   const int words = (w + 63) / 64;
-  size_t mid_bytes = 0;
+  size_t mid_bytes = 0;   // every scale's intermediate stays until the fused average
   for (int si = 0; si < nscales; ++si)
     if (!(geom[si].valid_h == h && geom[si].valid_w == w))
-      mid_bytes = std::max(mid_bytes, (size_t)n * geom[si].valid_h * geom[si].valid_w * nparts * 4);
+      mid_bytes += (size_t)n * geom[si].valid_h * geom[si].valid_w * nparts * 4;
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t avg_bytes = (size_t)n * nparts * P * 8, mask_bytes = (size_t)n * nparts * h * words * 8;
   const size_t par_bytes = (size_t)n * nparts * P * 4, val_bytes = (size_t)n * nparts * P * 8;
@@ -1972,6 +2058,9 @@ static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, cons
   CcStats* stats = (CcStats*)((char*)vals + up(val_bytes));
   CcChunk* cks = (CcChunk*)((char*)stats + up(st_bytes));
   const float div_f = (float)nscales;
+  MapSrcN fin;                        // per scale: the resize that lands on the crop
+  float* midp = mid;
+  int ty = RA_TY;
   for (int si = 0; si < nscales; ++si) {
     const isl_scale_geom& g = geom[si];
     const int h8 = g.net_h / 8, w8 = g.net_w / 8;
@@ -1981,15 +2070,25 @@ static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, cons
     lh.dh = h8 * 8; lh.dw = w8 * 8; lh.scy = lh.scx = 1.0 / 8.0; lh.cn = nch; lh.identity = 0;
     MapSrc fh = lh;
     if (!(g.valid_h == h && g.valid_w == w)) {
-      if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, mid, s))) return rc;
-      fh.base = mid; fh.xs = 1; fh.ys = g.valid_w; fh.cstr = (long long)g.valid_h * g.valid_w;
+      if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, midp, s))) return rc;
+      fh.base = midp; fh.xs = 1; fh.ys = g.valid_w; fh.cstr = (long long)g.valid_h * g.valid_w;
       fh.fs = (long long)nparts * g.valid_h * g.valid_w;
       fh.cshift = 30; fh.cbig = 0;
       fh.sh = g.valid_h; fh.sw = g.valid_w; fh.dh = h; fh.dw = w;
       fh.scy = 1.0 / ((double)h / g.valid_h); fh.scx = 1.0 / ((double)w / g.valid_w);
       fh.cn = nch; fh.identity = 0;
+      midp += (size_t)n * g.valid_h * g.valid_w * nparts;
     }
-    if ((rc = launch_resize(fh, n, nparts, h, w, si == 0 ? 3 | 8 : 3, div_f, avg, s))) return rc;
+    fin.m[si] = fh;
+    if (!fh.identity)   // rows per tile: every scale's source window fits the LDS rows
+      while (ty > 1 && (ty - 1) * fh.scy + 5.0 > (double)RS_MAXR) --ty;
+  }
+  {
+    const long long ty_tiles = (h + ty - 1) / ty;
+    if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "hand post: crop too tall");
+    hipLaunchKernelGGL(resize_acc_kernel, dim3(n * nparts, (unsigned)ty_tiles, (w + RS_TX - 1) / RS_TX), dim3(RS_TX),
+                       0, s, fin, nscales, nparts, h, w, ty, div_f, avg);
+    PHIP(hipGetLastError());
   }
   dim3 gb((w + NMS_TX - 1) / NMS_TX, (h + NMS_TY - 1) / NMS_TY, n * nparts);
   hipLaunchKernelGGL((blur_nms_kernel<double, false>), gb, dim3(256), 0, s, (const double*)avg, h, w, words, mask, 0.05,

@@ -1067,22 +1067,13 @@ __device__ __forceinline__ double np_leaf(const double* x, int len) {
 // leaves of its split tree, the block sums them, thread 0 combines them in tree
 // order.  Buffers are added left to right.  Every thread of the block must call it;
 // the result is returned to all of them.
-__device__ double np_sum_block(const double* a, int n) {
-  constexpr int MAXL = 128;   // leaves of a < 8192-element tree have 65..128 elements
-  __shared__ int s_loff[MAXL], s_llen[MAXL], s_nl;
-  __shared__ double s_lsum[MAXL];
-  __shared__ double s_part[32];
-  __shared__ double s_tot;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  const int nfull = n / 8192;
-  for (int g = 0; g < nfull; g += nw) {
-    const int b = g + wave;
-    if (b < nfull) {
+// numpy's pairwise sum of one full 8192-element buffer by one wave (the sum in lane 0)
+__device__ __forceinline__ double np_buf8192_wave(const double* buf) {
+  const int lane = threadIdx.x & 63;
       // the 64 leaves of 128, eight at a time: lane j of a group of 8 keeps np_leaf's
       // accumulator r[j] (coalesced 64-byte rows instead of a 1 KiB-strided leaf per
       // lane), then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) as xor butterflies (a + b ==
       // b + a exactly); leaf 8k+g ends in lane 8k+g
-      const double* buf = a + (size_t)b * 8192;
       const int g8 = lane >> 3, j8 = lane & 7;
       double v = 0.0;
       for (int k = 0; k < 8; ++k) {
@@ -1101,6 +1092,28 @@ __device__ double np_sum_block(const double* a, int n) {
         const double x0 = __shfl(v, 2 * lane, 64), x1 = __shfl(v, 2 * lane + 1, 64);
         if (lane < half) v = x0 + x1;
       }
+  return v;
+}
+
+// np_sum_block with the full buffers' sums already computed (pre[b], cc_bufsum_kernel)
+// when pre != nullptr
+__device__ double np_sum_block(const double* a, int n, const double* pre = nullptr) {
+  constexpr int MAXL = 128;   // leaves of a < 8192-element tree have 65..128 elements
+  __shared__ int s_loff[MAXL], s_llen[MAXL], s_nl;
+  __shared__ double s_lsum[MAXL];
+  __shared__ double s_part[32];
+  __shared__ double s_tot;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int nfull = n / 8192;
+  if (pre) {
+    if (tid == 0)
+      for (int b = 0; b < nfull; ++b) s_tot = b == 0 ? pre[0] : s_tot + pre[b];
+    __syncthreads();
+  }
+  for (int g = 0; !pre && g < nfull; g += nw) {
+    const int b = g + wave;
+    if (b < nfull) {
+      const double v = np_buf8192_wave(a + (size_t)b * 8192);
       if (lane == 0) s_part[wave] = v;
     }
     __syncthreads();
@@ -1223,28 +1236,52 @@ __global__ void __launch_bounds__(256) cc_local_kernel(const unsigned long long*
                                                        int words, int rows, int chunks, int* __restrict__ parent_all,
                                                        double* __restrict__ vals_all, CcStats* __restrict__ stats) {
   __shared__ int s_lp[CC_WMAX > CC_CHUNK ? CC_WMAX : CC_CHUNK];
+  // the chunk's mask rows in LDS (unions stay inside the chunk); chunks of very narrow
+  // planes (many rows of one word) read the global mask instead
+  constexpr int MW = 256;
+  __shared__ unsigned long long s_mk[MW];
   lds_int* lp = (lds_int*)s_lp;
   const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
-  const int P = h * w, y0 = c * rows, y1 = min(h, y0 + rows), base = y0 * w, n = (y1 - y0) * w;
-  const unsigned long long* mk = mask + (size_t)plane * h * words;
-  int* parent = parent_all + (size_t)plane * P;
-  double* vals = vals_all + (size_t)plane * P;
-  auto bit = [&](int y, int x) -> bool { return (mk[(size_t)y * words + (x >> 6)] >> (x & 63)) & 1ull; };
+  const int y0 = c * rows, y1 = min(h, y0 + rows), base = y0 * w, n = (y1 - y0) * w;
+  const unsigned long long* mk = mask + (size_t)plane * h * words + (size_t)y0 * words;
+  int* parent = parent_all + (size_t)plane * h * w;
   if (c == 0 && threadIdx.x == 0) { stats[plane].count = 0; stats[plane].ncand = 0; stats[plane].maxbits = 0; }
+  const int nw = (y1 - y0) * words;
+  const bool in_lds = nw <= MW;
+  if (in_lds)
+    for (int i = threadIdx.x; i < nw; i += 256) s_mk[i] = mk[i];
+  __syncthreads();
+  auto bit = [&](int yl, int x) -> bool {
+    const int q = yl * words + (x >> 6);
+    return ((in_lds ? s_mk[q] : mk[q]) >> (x & 63)) & 1ull;
+  };
+  auto word = [&](int yl, int k) -> unsigned long long {
+    const int q = yl * words + k;
+    return in_lds ? s_mk[q] : mk[q];
+  };
+  // horizontal runs without atomics: every foreground pixel's parent is the first pixel
+  // of its run (the highest clear mask bit below it, across words)
   for (int i = threadIdx.x; i < n; i += 256) {
-    const int y = y0 + i / w, x = i % w;
-    lp[i] = bit(y, x) ? i : -1;
-    vals[base + i] = 0.0;
+    const int yl = i / w, x = i - yl * w;
+    if (!bit(yl, x)) { lp[i] = -1; continue; }
+    int k = x >> 6;
+    unsigned long long z = ~word(yl, k) & ((1ull << (x & 63)) - 1ull);   // clear bits below x
+    while (!z && k > 0) z = ~word(yl, --k);
+    const int xs = z ? (k << 6) + 64 - __clzll((long long)z) : 0;
+    lp[i] = yl * w + xs;
   }
   __syncthreads();
+  // vertical: one union per 8-adjacent (run, run above) pair, as cc_merge_kernel (a pixel
+  // unions with an upper neighbour when either starts its run)
   for (int i = threadIdx.x; i < n; i += 256) {
-    if (lp[i] < 0) continue;
-    const int yl = i / w, x = i - yl * w, y = y0 + yl;
-    if (x > 0 && bit(y, x - 1)) uf_union(lp, i, i - 1);
-    if (yl > 0) {
-      if (x > 0 && bit(y - 1, x - 1)) uf_union(lp, i, i - w - 1);
-      if (bit(y - 1, x)) uf_union(lp, i, i - w);
-      if (x + 1 < w && bit(y - 1, x + 1)) uf_union(lp, i, i - w + 1);
+    const int yl = i / w, x = i - yl * w;
+    if (yl == 0 || lp[i] < 0) continue;
+    const bool start = lp[i] == i;
+#pragma unroll
+    for (int d = -1; d <= 1; ++d) {
+      const int xu = x + d;
+      if (xu < 0 || xu >= w || !bit(yl - 1, xu)) continue;
+      if (start || xu == 0 || !bit(yl - 1, xu - 1)) uf_union(lp, i, i - w + d);
     }
   }
   __syncthreads();
@@ -1252,6 +1289,7 @@ __global__ void __launch_bounds__(256) cc_local_kernel(const unsigned long long*
     if (ld_parent(lp, i) >= 0) __hip_atomic_store(lp + i, uf_root(lp, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += 256) parent[base + i] = lp[i] >= 0 ? base + lp[i] : -1;
+  (void)vals_all;   // the root accumulators are zeroed by cc_find_kernel (roots only)
 }
 
 __global__ void __launch_bounds__(256) cc_merge_kernel(const unsigned long long* __restrict__ mask, int h, int w,
@@ -1283,13 +1321,18 @@ __global__ void __launch_bounds__(256) cc_merge_kernel(const unsigned long long*
 
 // labelling: every pixel's parent becomes its root (roots are final once every union
 // is done; uf_root)
-__global__ void __launch_bounds__(256) cc_find_kernel(int h, int w, int rows, int chunks, int* __restrict__ parent_all) {
+__global__ void __launch_bounds__(256) cc_find_kernel(int h, int w, int rows, int chunks, int* __restrict__ parent_all,
+                                                      double* __restrict__ vals_all) {
   const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
   const int P = h * w, p0 = c * rows * w, p1 = min(P, p0 + rows * w);
   int* parent = parent_all + (size_t)plane * P;
+  double* vals = vals_all + (size_t)plane * P;
   for (int p = p0 + threadIdx.x; p < p1; p += 256)
-    if (ld_parent(parent, p) >= 0)
-      __hip_atomic_store(parent + p, uf_root(parent, p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ld_parent(parent, p) >= 0) {
+      const int r = uf_root(parent, p);
+      __hip_atomic_store(parent + p, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (r == p) vals[p] = 0.0;   // a root: its cc_sum accumulator (only roots are ever read)
+    }
 }
 
 __global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ planes, int h, int w, int rows,
@@ -1309,18 +1352,33 @@ __global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ 
   // thread is combined across the wave, then across the block, when the roots agree.
   // Block-strided pixels: every load is one coalesced row segment (a contiguous run per
   // thread made each load touch 64 cache lines)
+  // a chunk is <= CC_CHUNK = 16 x 256 pixels: every parent load of the thread, then every
+  // value load, in flight together (one exposed latency each, not two per pixel)
+  // (one row of a plane wider than CC_CHUNK takes several rounds)
+  constexpr int PER = CC_CHUNK / 256;
   int cnt = 0, cur = -1;
   double acc = 0.0;
-  for (int p = p0 + threadIdx.x; p < p1; p += 256) {
-    const int r = parent[p];
-    if (r < 0) continue;
-    ++cnt;
-    if (r != cur) {
-      if (cur >= 0) atomicAdd(&vals[cur], acc);
-      cur = r;
-      acc = 0.0;
+  for (int q0 = p0; q0 < p1; q0 += CC_CHUNK) {
+    int r[PER];
+    double v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int p = q0 + threadIdx.x + 256 * k;
+      r[k] = p < p1 ? parent[p] : -1;
     }
-    acc += map[p];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) v[k] = r[k] >= 0 ? map[q0 + threadIdx.x + 256 * k] : 0.0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (r[k] < 0) continue;
+      ++cnt;
+      if (r[k] != cur) {
+        if (cur >= 0) atomicAdd(&vals[cur], acc);
+        cur = r[k];
+        acc = 0.0;
+      }
+      acc += v[k];
+    }
   }
   // lanes that met no foreground pixel (cur < 0, acc 0) do not break the agreement:
   // otherwise a plane that is one giant component with background lanes would flush
@@ -1573,13 +1631,46 @@ __device__ __forceinline__ int cc_block_scan(int v, int* s_i, int& total) {
 // walk CC_RUN consecutive pixels per thread and round with 1024 threads: a plane of a
 // 600 px crop is ~44 rounds per pass, not the ~1400 dependent rounds of a
 // 256-thread, one-pixel-per-round loop.
+// The full 8192-element buffers of every candidate's compacted values (cc_scatter) summed
+// across many blocks, one wave per buffer (numpy's exact tree); hand_cc_kernel<false, true>
+// adds them left to right.  bsum[(plane * CC_KFAST + k) * maxb + b].
+__global__ void __launch_bounds__(256) cc_bufsum_kernel(const CcStats* __restrict__ stats,
+                                                        const CcChunk* __restrict__ ck, int chunks, int P,
+                                                        const double* __restrict__ vals_all, double* __restrict__ bsum,
+                                                        int maxb) {
+  __shared__ int s_tot[CC_KFAST];
+  const int plane = blockIdx.x, nk = stats[plane].ncand;
+  if (stats[plane].count == 0 || nk < 1 || nk > CC_KFAST) return;
+  const CcChunk* pc = ck + (size_t)plane * chunks;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x < CC_KFAST) s_tot[threadIdx.x] = 0;
+  __syncthreads();
+  for (int k = 0; k < nk; ++k) {
+    int t = 0;
+    for (int c = threadIdx.x; c < chunks; c += 256) t += pc[c].count[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) atomicAdd(&s_tot[k], t);
+  }
+  __syncthreads();
+  const double* vals = vals_all + (size_t)plane * P;
+  for (int k = 0, base = 0; k < nk; base += s_tot[k], ++k) {
+    const int nb = s_tot[k] / 8192;
+    for (int b = blockIdx.y * 4 + wave; b < nb; b += gridDim.y * 4) {
+      const double v = np_buf8192_wave(vals + base + (size_t)b * 8192);
+      if (lane == 0) bsum[((size_t)plane * CC_KFAST + k) * maxb + b] = v;
+    }
+  }
+}
+
 template <bool LDSP, bool PRE>
 __global__ void __launch_bounds__(CC_NT) hand_cc_kernel(const double* __restrict__ planes,
                                                         const unsigned long long* __restrict__ mask, int h, int w,
                                                         int words, int* __restrict__ parent_all,
                                                         double* __restrict__ vals_all, const CcStats* __restrict__ stats,
                                                         const CcChunk* __restrict__ ck, int chunks,
-                                                        long long* __restrict__ out) {
+                                                        long long* __restrict__ out,
+                                                        const double* __restrict__ bsum_all, int maxb) {
   extern __shared__ int s_dyn[];
   const int plane = blockIdx.x;   // crop * 21 + part
   const int P = h * w, tid = threadIdx.x;
@@ -1641,7 +1732,8 @@ __global__ void __launch_bounds__(CC_NT) hand_cc_kernel(const double* __restrict
       double bestsum = 0.0;
       for (int q = 0; q < nk; ++q) {
         const int k = order[q];
-        const double sum = np_sum_block(vals + base[k], tot[k]);
+        const double sum = np_sum_block(vals + base[k], tot[k],
+                                        bsum_all ? bsum_all + ((size_t)plane * CC_KFAST + k) * maxb : nullptr);
         if (bestk < 0 || sum > bestsum) { bestsum = sum; bestk = k; }   // first max
       }
       double bv = -INFINITY;
@@ -2031,7 +2123,9 @@ static size_t hand_post_bytes(int n, int h, int w, int nscales, const isl_scale_
   const size_t st_bytes = (size_t)n * nparts * sizeof(CcStats);
   const int cc_rows = std::max(1, CC_CHUNK / w), cc_chunks = (h + cc_rows - 1) / cc_rows;
   const size_t ck_bytes = (size_t)n * nparts * cc_chunks * sizeof(CcChunk);
-  return up(avg_bytes) + up(mid_bytes) + up(mask_bytes) + up(par_bytes) + up(val_bytes) + up(st_bytes) + up(ck_bytes);
+  const size_t bs_bytes = (size_t)n * nparts * CC_KFAST * (P / 8192 + 1) * 8;
+  return up(avg_bytes) + up(mid_bytes) + up(mask_bytes) + up(par_bytes) + up(val_bytes) + up(st_bytes) + up(ck_bytes) +
+         up(bs_bytes);
 }
 
 // the kernels of one hand post (hand.py:51-74) on stream s, scratch at base
@@ -2057,6 +2151,7 @@ static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, cons
   double* vals = (double*)((char*)parent + up(par_bytes));
   CcStats* stats = (CcStats*)((char*)vals + up(val_bytes));
   CcChunk* cks = (CcChunk*)((char*)stats + up(st_bytes));
+  double* bsum = (double*)((char*)cks + up((size_t)n * nparts * cc_chunks * sizeof(CcChunk)));
   const float div_f = (float)nscales;
   MapSrcN fin;                        // per scale: the resize that lands on the crop
   float* midp = mid;
@@ -2102,22 +2197,26 @@ static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, cons
       attr = true;
     }
     hipLaunchKernelGGL((hand_cc_kernel<true, false>), dim3(n * nparts), dim3(CC_NT), (size_t)h * w * 4, s,
-                       (const double*)avg, mask, h, w, words, parent, vals, nullptr, nullptr, 0, (long long*)d_peaks);
+                       (const double*)avg, mask, h, w, words, parent, vals, nullptr, nullptr, 0, (long long*)d_peaks,
+                       nullptr, 0);
   } else {
     if (w > CC_WMAX) return post_fail(ISL_E_ARG, "isl_hand_post: crop wider than 8192 px");
     const int rows = cc_rows, chunks = cc_chunks;
     const dim3 g(n * nparts * chunks);
     hipLaunchKernelGGL(cc_local_kernel, g, dim3(256), 0, s, mask, h, w, words, rows, chunks, parent, vals, stats);
     hipLaunchKernelGGL(cc_merge_kernel, g, dim3(256), 0, s, mask, h, w, words, rows, chunks, parent);
-    hipLaunchKernelGGL(cc_find_kernel, g, dim3(256), 0, s, h, w, rows, chunks, parent);
+    hipLaunchKernelGGL(cc_find_kernel, g, dim3(256), 0, s, h, w, rows, chunks, parent, vals);
     hipLaunchKernelGGL(cc_sum_kernel, g, dim3(256), 0, s, (const double*)avg, h, w, rows, chunks, parent, vals, stats);
     hipLaunchKernelGGL(cc_stats_kernel, g, dim3(256), 0, s, h, w, rows, chunks, parent, vals, stats);
     hipLaunchKernelGGL(cc_cand_kernel, g, dim3(256), 0, s, h, w, rows, chunks, parent, vals, stats);
     hipLaunchKernelGGL(cc_count_kernel, g, dim3(256), 0, s, (const double*)avg, h, w, rows, chunks, parent, stats, cks);
     hipLaunchKernelGGL(cc_scatter_kernel, g, dim3(256), 0, s, (const double*)avg, h, w, rows, chunks, parent, stats, cks,
                        vals);
+    const int maxb = (int)(P / 8192) + 1;
+    hipLaunchKernelGGL(cc_bufsum_kernel, dim3(n * nparts, std::max(1, std::min(32, (maxb + 3) / 4))), dim3(256), 0, s,
+                       stats, cks, chunks, (int)P, vals, bsum, maxb);
     hipLaunchKernelGGL((hand_cc_kernel<false, true>), dim3(n * nparts), dim3(CC_NT), 0, s, (const double*)avg, mask,
-                       h, w, words, parent, vals, stats, cks, chunks, (long long*)d_peaks);
+                       h, w, words, parent, vals, stats, cks, chunks, (long long*)d_peaks, bsum, maxb);
   }
   PHIP(hipGetLastError());
   return ISL_OK;

@@ -148,6 +148,10 @@ int isl_net_set_split_k(isl_net* net, int mode);
  * ISL_ALGO_DIRECT), else ISL_OK; clear != 0 resets the flag.  The post records
  * of isl_body_post carry the same flag in their status word without a sync. */
 int isl_net_check(isl_net* net, int clear);
+/* The same check stream-ordered, for pipelined callers: enqueues on `stream` a copy of
+ * the flag into *h_flag (pinned host memory; valid once the stream has reached it) and
+ * its reset.  *h_flag != 0 then means ISL_E_RANGE for the work enqueued before. */
+int isl_net_check_async(isl_net* net, int32_t* h_flag, void* stream);
 
 /* Per-op device timing (measurement; not in the reference).  After
  * isl_net_set_timing(net, 1) every isl_net_run records a HIP event on its stream

@@ -1191,6 +1191,16 @@ int isl_net_check(isl_net* net, int clear) {
   return ISL_OK;
 }
 
+int isl_net_check_async(isl_net* net, int32_t* h_flag, void* stream) {
+  if (!net || !h_flag) return fail(ISL_E_ARG, "NULL argument");
+  if (!net->d_flag) { *h_flag = 0; return ISL_OK; }
+  HIP_OK(hipSetDevice(net->device));
+  hipStream_t s = (hipStream_t)stream;
+  HIP_OK(hipMemcpyAsync(h_flag, net->d_flag, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemsetAsync(net->d_flag, 0, sizeof(int), s));
+  return ISL_OK;
+}
+
 const int* isl_net_range_flag(const isl_net* net) { return net ? net->d_flag : nullptr; }
 
 int isl_net_arena_info(const isl_net* net, int64_t* bytes, int* n_arenas) {

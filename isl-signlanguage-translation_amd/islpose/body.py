@@ -192,6 +192,52 @@ class BodyEstimator:
         out = [(r.candidate, r.subset) for r in res]
         return out[0] if single else out
 
+    # -- pipelined (stream-ordered) form of estimate --------------------------------
+    def launch(self, frames_t):
+        """Enqueue estimate() on the current stream without waiting: nets, post, the
+        records' copy to pinned host memory and a stream-ordered range check.  frames_t:
+        cuda uint8 [n,H,W,3].  finish(job) completes it; the net must not run again
+        before that (its arena holds the maps a capacity re-run reads)."""
+        import torch
+        n, H, W, _ = frames_t.shape
+        geoms, pafs, heats = self.run_scales(frames_t)
+        caps = dict(self.caps)
+        c = rt.IslCaps(**caps)
+        lay = rt.body_layout(self.kind, c)
+        res = torch.empty(n * lay.record_bytes, dtype=torch.uint8, device=frames_t.device)
+        ns = len(geoms)
+        g = (rt.IslScaleGeom * ns)(*[rt.IslScaleGeom(*gg) for gg in geoms])
+        pp = (ctypes.c_void_p * ns)(*[rt.ptr(p).value for p in pafs])
+        hp = (ctypes.c_void_p * ns)(*[rt.ptr(h).value for h in heats])
+        rt.check(rt.lib().isl_body_post(self.net.h, n, H, W, ns, g, pp, hp, ctypes.byref(c), rt.ptr(res),
+                                       rt.stream_handle()), "isl_body_post")
+        host = torch.empty(res.shape, dtype=torch.uint8, pin_memory=True)
+        host.copy_(res, non_blocking=True)
+        flag = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.net.check_async(flag)
+        ev = torch.cuda.Event()
+        ev.record()
+        return dict(t=frames_t, n=n, H=H, W=W, geoms=geoms, pafs=pafs, heats=heats, caps=caps, lay=lay, res=res,
+                    host=host, flag=flag, ev=ev)
+
+    def finish(self, job, details=False):
+        """Wait for a launch() and decode it: the same results as estimate(), including
+        the fp32 re-run of a batch that left the split-fp16 range and the post re-run
+        with larger buffers on a capacity overflow."""
+        job["ev"].synchronize()
+        n, H, W = job["n"], job["H"], job["W"]
+        if int(job["flag"][0]) != 0:
+            with self.net.algo_scope("direct"):
+                geoms, pafs, heats = self.run_scales(job["t"])
+                host, lay, caps = self.post(n, H, W, geoms, pafs, heats)
+        else:
+            host, lay, caps = job["host"].numpy(), job["lay"], job["caps"]
+            grow = self._grow(host, lay, n, caps)
+            if grow is not None:
+                host, lay, caps = self.post(n, H, W, job["geoms"], job["pafs"], job["heats"], caps=grow)
+        res = self.decode(host, lay, caps, n, details)
+        return res if details else [(r.candidate, r.subset) for r in res]
+
     def post_maps(self, H, W, geoms, pafs, heats, details=True):
         """Post-processing only, on caller low-res maps (NCHW cuda tensors per scale)."""
         n = pafs[0].shape[0]

@@ -93,8 +93,40 @@ class HandEstimator:
             heats.append(heat)
         return heats
 
+    def launch_crops(self, frames_t, boxes):
+        """Enqueue estimate_crops() on the current stream without waiting (nets, posts,
+        peaks to pinned host memory, stream-ordered range check); finish_crops(job)
+        completes it."""
+        import torch
+        parts = []
+        for c in range(0, len(boxes), CROP_CHUNK):
+            part = boxes[c:c + CROP_CHUNK]
+            heats = self.run_crops(frames_t, part)
+            out = self._post_crops_dev(part, heats)
+            host = torch.empty(out.shape, dtype=torch.int64, pin_memory=True)
+            host.copy_(out, non_blocking=True)
+            parts.append((part, heats, out, host))
+        flag = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.net.check_async(flag)
+        ev = torch.cuda.Event()
+        ev.record()
+        return dict(t=frames_t, boxes=boxes, parts=parts, flag=flag, ev=ev)
+
+    def finish_crops(self, job):
+        if not job["boxes"]:
+            return np.zeros((0, 21, 2), np.int64)
+        job["ev"].synchronize()
+        if int(job["flag"][0]) != 0:     # split-fp16 range left: the whole call again on fp32
+            with self.net.algo_scope("direct"):
+                return np.concatenate([self.post_crops(part, self.run_crops(job["t"], part))
+                                       for part, _, _, _ in job["parts"]])
+        return np.concatenate([host.numpy() for _, _, _, host in job["parts"]])
+
     def post_crops(self, boxes, heats):
         """isl_hand_post per crop (its resize-back target is the crop size) -> int64 [n,21,2]."""
+        return self._post_crops_dev(boxes, heats).cpu().numpy()
+
+    def _post_crops_dev(self, boxes, heats):
         import torch
         n, ns = len(boxes), len(heats)
         out = torch.empty((n, 21, 2), dtype=torch.int64, device=heats[0].device)
@@ -110,7 +142,7 @@ class HandEstimator:
         hp = (ctypes.c_void_p * ns)(*[rt.ptr(hh).value for hh in heats])
         rt.check(rt.lib().isl_hand_post_crops(self.net.h, n, ws, ns, g, hp, rt.ptr(out), rt.stream_handle()),
                  "isl_hand_post_crops")
-        return out.cpu().numpy()
+        return out
 
     def estimate(self, crops):
         """crops: uint8 [n,h,w,3] or one [h,w,3] (numpy or torch) -> int64 [n,21,2] / [21,2]."""

@@ -263,10 +263,18 @@ class KeypointExtractor:
         dev = getattr(self.model, "_device", None)
         dev = torch.cuda.current_device() if dev is None else dev
         writer = _Writer(self._write)
+
+        def bgr_batches():
+            for meta, rgb in _Prefetch(self._batches(vids), dev):
+                yield meta, rgb.flip(-1)                      # extract_features_mp.py:124, on the GPU
+
+        # models with the pipelined form (ISLSignPos.call_batches) overlap the body of
+        # batch k with the hands of batch k-1 on the GPU
+        batches = getattr(self.model, "call_batches", None)
+        if batches is None:
+            batches = lambda it: ((meta, self.model.call_batch(bgr)) for meta, bgr in it)  # noqa: E731
         try:
-            for (rows, filename, lt, ex, ids), rgb in _Prefetch(self._batches(vids), dev):
-                bgr = rgb.flip(-1)                            # extract_features_mp.py:124, on the GPU
-                feats = self.model.call_batch(bgr)
+            for (rows, filename, lt, ex, ids), feats in batches(bgr_batches()):
                 writer.put(rows, filename, lt, ex, ids, feats)
                 self.frames_done += len(ids)
         finally:

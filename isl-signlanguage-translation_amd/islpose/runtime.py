@@ -25,7 +25,7 @@ EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destr
            "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post",
            "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops",
            "isl_sign_param_count", "isl_sign_classify", "isl_net_set_split_k", "isl_net_arena_info",
-           "isl_debug_np_sum", "isl_hand_post_crops"]
+           "isl_debug_np_sum", "isl_hand_post_crops", "isl_net_check_async"]
 
 
 class IslCaps(ctypes.Structure):
@@ -81,6 +81,7 @@ def lib():
     L.isl_net_set_algo.argtypes = [vp, i32]
     L.isl_net_get_algo.argtypes = [vp]
     L.isl_net_check.argtypes = [vp, i32]
+    L.isl_net_check_async.argtypes = [vp, vp, vp]
     pi, pd = ctypes.POINTER(i32), ctypes.POINTER(dbl)
     L.isl_net_timing.argtypes = [vp, i32, pi, pi, pd, pi, pd, pd]
     L.isl_body_layout.argtypes = [i32, ctypes.POINTER(IslCaps), ctypes.POINTER(IslLayout)]
@@ -235,6 +236,13 @@ class Net:
             return False
         check(rc, "isl_net_check")
         return True
+
+    def check_async(self, flag_host, stream=None):
+        """Stream-ordered range check (isl_net_check_async): flag_host, a pinned int32
+        tensor of one element, holds the flag (then cleared on the device) once `stream`
+        has reached this point."""
+        assert flag_host.is_pinned() and flag_host.dtype.itemsize == 4
+        check(lib().isl_net_check_async(self.h, ptr(flag_host), stream_handle(stream)), "isl_net_check_async")
 
     def preprocess(self, frames_u8, scale: float, stream=None):
         """frames uint8 [n,H,W,3] cuda -> fills the net input; returns (net_h, net_w)."""

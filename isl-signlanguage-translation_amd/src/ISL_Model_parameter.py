@@ -120,6 +120,10 @@ class ISLSignPos(object):
             for x, y, w, _is_left in util.handDetect(c, s, t[i]):
                 boxes.append((i, x, y, w))
         peaks = hand.estimate_crops(t, boxes)
+        return self._assemble(res, boxes, peaks)
+
+    @staticmethod
+    def _assemble(res, boxes, peaks):
         out = [(c, s, []) for (c, s) in res]
         for (i, x, y, _w), pk in zip(boxes, peaks):
             pk = pk.copy()
@@ -127,6 +131,36 @@ class ISLSignPos(object):
             pk[:, 1] = np.where(pk[:, 1] == 0, pk[:, 1], pk[:, 1] + y)
             out[i][2].append(pk)
         return out
+
+    def call_batches(self, batches):
+        """call_batch over an iterable of (key, frames) -- frames cuda uint8 [n, H, W, 3]
+        BGR, ready on the current stream -- yielding (key, results) in order, the same
+        results as call_batch.  Software-pipelined across batches on two streams: the
+        body net and post of batch k run while the hand nets and posts of batch k-1 do,
+        so one phase's small grids fill the CUs the other leaves idle."""
+        body, hand = self._estimators()
+        dev = torch.device("cuda:%d" % body.device)
+        cur = torch.cuda.current_stream(dev)
+        if getattr(self, "_pipe_streams", None) is None:
+            self._pipe_streams = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+        sb, sh = self._pipe_streams
+        prev = None                                  # (key, body results, boxes, hand job)
+        for key, t in batches:
+            sb.wait_stream(cur)
+            with torch.cuda.stream(sb):
+                bjob = body.launch(t)
+            t.record_stream(sb)
+            if prev is not None:                     # its hands ran beside this body
+                yield prev[0], self._assemble(prev[1], prev[2], hand.finish_crops(prev[3]))
+            res = body.finish(bjob)
+            boxes = [(i, x, y, w) for i, (c, s) in enumerate(res) for x, y, w, _l in util.handDetect(c, s, t[i])]
+            sh.wait_stream(cur)
+            with torch.cuda.stream(sh):
+                hjob = hand.launch_crops(t, boxes)
+            t.record_stream(sh)
+            prev = (key, res, boxes, hjob)
+        if prev is not None:
+            yield prev[0], self._assemble(prev[1], prev[2], hand.finish_crops(prev[3]))
 
 
 class ISLSignPosTranslator(ISLSignPos):

@@ -95,3 +95,29 @@ def test_isl_sign_pos_matches_composition(body, hand):
         assert np.array_equal(pk, ref)
     out = isl.call_batch(np.stack([frame, frame]))
     assert np.array_equal(out[1][0], cand) and len(out[1][2]) == len(hands)
+
+
+def test_call_batches_pipelined_equals_call_batch(body, hand):
+    """ISLSignPos.call_batches (the body of batch k on one stream beside the hands of
+    batch k-1 on another) yields, in order, exactly what call_batch gives per batch:
+    ragged batches, frames with and without hand crops."""
+    from src.ISL_Model_parameter import ISLSignPos
+    isl = ISLSignPos(body.model, hand.model)
+    frames = synth.synth_frames(7, 240, 368, seed=21)
+    sizes = [3, 1, 3]
+    ref, batches, o = [], [], 0
+    for k, n in enumerate(sizes):
+        ref.append(isl.call_batch(frames[o:o + n]))
+        batches.append((k, torch.from_numpy(frames[o:o + n]).cuda()))
+        o += n
+    got = list(isl.call_batches(iter(batches)))
+    assert [k for k, _ in got] == list(range(len(sizes)))
+    n_hands = 0
+    for (_, res), exp in zip(got, ref):
+        assert len(res) == len(exp)
+        for (c, s, hs), (c2, s2, hs2) in zip(res, exp):
+            assert np.array_equal(c, c2) and np.array_equal(s, s2) and len(hs) == len(hs2)
+            n_hands += len(hs)
+            for a, b in zip(hs, hs2):
+                assert np.array_equal(a, b)
+    assert n_hands > 0

@@ -136,6 +136,7 @@ def c5(args):
     from src.hand import Hand
     from src.ISL_Model_parameter import ISLSignPos
     T, H, W = args.c5_frames, 1080, 1920
+    B = args.c5_batch
     rgb = synth.synth_frames(T, H, W, seed=57)
     # heat layer tamed on the GPU net's own output for frame 0 (a few persons per frame)
     wb = synth.synth_weights(0)
@@ -148,18 +149,18 @@ def c5(args):
     clips = {"v%d.mp4" % k: rgb for k in range(args.c5_videos)}
     rows = [{"Filepath": f, "type": "Greetings", "expression": "hello"} for f in clips]
     res = {"config": "C5 video -> per-frame JSON, 1080x1920 RGB frames", "frames": T * len(rows),
-           "videos": len(rows), "batch": args.batch, "export": False,
+           "videos": len(rows), "batch": B, "export": False,
            "decode": "frames already decoded in host memory (pims/ffmpeg absent); the pipeline reads them as "
                      "slices of the [T,H,W,3] array"}
     for ov in ((True,) if args.c5_overlap_only else (False, True)):
         out = tempfile.mkdtemp(prefix="c5_")
         try:
             # warm-up (arenas, hand scales) on the first video, then the timed pass over all
-            pipeline.extract_dataset(rows[:1], clips.__getitem__, isl, out, batch=args.batch, export=False, overlap=ov)
+            pipeline.extract_dataset(rows[:1], clips.__getitem__, isl, out, batch=B, export=False, overlap=ov)
             shutil.rmtree(out)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            feats, ex = pipeline.extract_dataset(rows, clips.__getitem__, isl, out, batch=args.batch,
+            feats, ex = pipeline.extract_dataset(rows, clips.__getitem__, isl, out, batch=B,
                                                  export=False, overlap=ov)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
@@ -213,7 +214,8 @@ def c6(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", choices=["c3", "c4", "c5", "c6", "all"], default="all")
-    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=16, help="C3 / C4 frames per step")
+    ap.add_argument("--c5-batch", type=int, default=32, help="C5 frames per pipeline batch")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--c5-frames", type=int, default=96, help="C5: frames per (synthetic 1080p) video")

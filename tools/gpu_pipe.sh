@@ -6,8 +6,8 @@ rc=$?
 tail -3 $O/tests.log
 if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $O/tests.log | head -30; exit $rc; fi
 timeout -k 10 300 python3 -u tools/c5_timeline.py 96 2 32 > $O/c5tl.txt 2>&1 &&
-timeout -k 10 600 python3 -u tools/bench_configs.py --config c5 --c5-overlap-only > $O/c5_b16.json 2> $O/c5.err &&
-timeout -k 10 600 python3 -u tools/bench_configs.py --config c5 --c5-overlap-only --batch 32 > $O/c5_b32.json 2>> $O/c5.err
+timeout -k 10 600 python3 -u tools/bench_configs.py --config c5 --c5-overlap-only --c5-batch 16 > $O/c5_b16.json 2> $O/c5.err &&
+timeout -k 10 600 python3 -u tools/bench_configs.py --config c5 --c5-overlap-only --c5-batch 32 > $O/c5_b32.json 2>> $O/c5.err
 rc=$?
 cat $O/c5tl.txt $O/c5_b16.json $O/c5_b32.json
 exit $rc

@@ -209,8 +209,15 @@ struct isl_net {
     std::vector<size_t> offs;   // buffer offsets for n_cap frames
     size_t bytes = 0;
     unsigned long long last_use = 0;
+    // per-arena (per net size) pre-processing table and split-K workspace, so runs of
+    // different sizes may be in flight on different streams at once (the hand scales)
+    void* tab = nullptr;
+    size_t tab_bytes = 0;
+    float* ks = nullptr;
+    size_t ks_floats = 0;
   };
   std::map<long long, Arena> plans;
+  Arena* cur = nullptr;        // the arena of the current plan
   unsigned long long plan_clock = 0;
   size_t plans_bytes = 0;
   void* arena = nullptr;
@@ -218,9 +225,6 @@ struct isl_net {
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   PostLanes* lanes = nullptr;   // isl_hand_post_crops (net_post_lanes)
-  // split-K partial sums of the x3 convs on small grids (grow-only)
-  float* d_ks = nullptr;
-  size_t ks_floats = 0;
   // per-op event timing (isl_net_set_timing / isl_net_timing)
   struct TimedRun {
     std::vector<hipEvent_t> ev;          // ops + 1 events: before op 0, after every op
@@ -233,9 +237,8 @@ struct isl_net {
   int algo = ISL_ALGO_X3;
   int split_k = 1;             // isl_net_set_split_k: K-range mode (env ISLPOSE_X3_SPLITK=0|1|2)
   int* d_flag = nullptr;
-  // pre-processing image table (device, grow-only; refilled stream-ordered per call)
-  void* d_tab = nullptr;
-  size_t tab_bytes = 0;
+  // pre-processing image table (host staging; the device copy is per arena)
+  void* d_tab = nullptr;       // the current arena's table (Arena::tab)
   std::vector<char> h_tab;
 };
 
@@ -652,9 +655,12 @@ static size_t arena_budget() {
 static void drop_arena(isl_net* net, std::map<long long, isl_net::Arena>::iterator it) {
   // hipFree waits for queued work that may still use the arena
   (void)hipFree(it->second.base);
+  if (it->second.tab) (void)hipFree(it->second.tab);
+  if (it->second.ks) (void)hipFree(it->second.ks);
   net->plans_bytes -= it->second.bytes;
   if (net->arena == it->second.base) {
     net->arena = nullptr;
+    net->cur = nullptr;
     net->pn = net->ph = net->pw = 0;
   }
   net->plans.erase(it);
@@ -692,6 +698,7 @@ static int plan(isl_net* net, int n, int h, int w) {
   }
   isl_net::Arena& ar = it->second;
   ar.last_use = ++net->plan_clock;
+  net->cur = &ar;
   if (net->arena == ar.base && net->pn == n && net->ph == h && net->pw == w) return ISL_OK;
   const int lh[4] = {h, h / 2, h / 4, h / 8}, lw[4] = {w, w / 2, w / 4, w / 8};
   net->act.assign(net->bufs.size(), Act{});
@@ -839,16 +846,17 @@ static int run_ops(isl_net* net, hipStream_t s) {
         fused = true;
       }
       const size_t need = x3_splitk_ws_floats(L);
-      if (need > net->ks_floats) {
+      isl_net::Arena& ar = *net->cur;
+      if (need > ar.ks_floats) {
         // grow-only; hipFree waits for the queued work that may still read the old one
-        if (net->d_ks) HIP_OK(hipFree(net->d_ks));
-        net->d_ks = nullptr;
-        net->ks_floats = 0;
-        HIP_OK(hipMalloc(&net->d_ks, need * sizeof(float)));
-        net->ks_floats = need;
+        if (ar.ks) HIP_OK(hipFree(ar.ks));
+        ar.ks = nullptr;
+        ar.ks_floats = 0;
+        HIP_OK(hipMalloc(&ar.ks, need * sizeof(float)));
+        ar.ks_floats = need;
       }
-      L.ws = net->d_ks;
-      L.ws_floats = net->ks_floats;
+      L.ws = ar.ks;
+      L.ws_floats = ar.ks_floats;
       if (c.d_wrgb && x3_rgb_fits(L) && rgb_kernel_enabled() && !L.vin) {
         L.wx3 = c.d_wrgb;
         HIP_OK(launch_conv_x3_rgb(L, s));
@@ -976,7 +984,10 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_wux3) (void)hipFree(c.d_wux3);
   }
   if (net->d_flag) (void)hipFree(net->d_flag);
-  if (net->d_tab) (void)hipFree(net->d_tab);
+  for (auto& kv : net->plans) {
+    if (kv.second.tab) (void)hipFree(kv.second.tab);
+    if (kv.second.ks) (void)hipFree(kv.second.ks);
+  }
   for (auto& kv : net->plans) (void)hipFree(kv.second.base);
   if (net->scratch) (void)hipFree(net->scratch);
   if (net->lanes) {
@@ -989,7 +1000,7 @@ int isl_net_destroy(isl_net* net) {
     (void)hipEventDestroy(net->lanes->fork);
     delete net->lanes;
   }
-  if (net->d_ks) (void)hipFree(net->d_ks);
+
   for (auto& r : net->timed)
     for (hipEvent_t e : r.ev) (void)hipEventDestroy(e);
   delete net;
@@ -1050,16 +1061,19 @@ int isl_net_forward(isl_net* net, const float* d_x, int n, int h, int w, float* 
 }
 
 // Upload the image table built in net->h_tab (stream-ordered; pageable source is staged by HIP).
+// The table lives with the current plan's arena (one per net size).
 static int upload_tab(isl_net* net, hipStream_t s) {
   const size_t bytes = net->h_tab.size();
-  if (bytes > net->tab_bytes) {
-    if (net->d_tab) HIP_OK(hipFree(net->d_tab));
-    net->d_tab = nullptr;
-    net->tab_bytes = 0;
-    HIP_OK(hipMalloc(&net->d_tab, bytes));
-    net->tab_bytes = bytes;
+  isl_net::Arena& ar = *net->cur;
+  if (bytes > ar.tab_bytes) {
+    if (ar.tab) HIP_OK(hipFree(ar.tab));
+    ar.tab = nullptr;
+    ar.tab_bytes = 0;
+    HIP_OK(hipMalloc(&ar.tab, bytes));
+    ar.tab_bytes = bytes;
   }
-  HIP_OK(hipMemcpyAsync(net->d_tab, net->h_tab.data(), bytes, hipMemcpyHostToDevice, s));
+  HIP_OK(hipMemcpyAsync(ar.tab, net->h_tab.data(), bytes, hipMemcpyHostToDevice, s));
+  net->d_tab = ar.tab;
   return ISL_OK;
 }
 

@@ -69,6 +69,27 @@ class BodyEstimator:
         n, H, W, _ = frames.shape
         geoms, pafs, heats = [], [], []
         multi = len(self.scale_search) > 1 or keep_maps
+        if len(self.scale_search) > 1:
+            # pyramid: the scales side by side on their own streams (per-size arenas), as
+            # HandEstimator.run_crops
+            cur = torch.cuda.current_stream(frames.device)
+            for st, (m, nh, nw, vh, vw) in zip(rt.scale_streams(self, frames.device, len(self.scale_search)),
+                                               scale_geometry(H, W, self.scale_search)):
+                st.wait_stream(cur)
+                with torch.cuda.stream(st):
+                    gh, gw = self.net.preprocess(frames, m)
+                    assert (gh, gw) == (nh, nw)
+                    paf = torch.empty((n, self.npaf, nh // 8, nw // 8), device=frames.device)
+                    heat = torch.empty((n, self.njoint, nh // 8, nw // 8), device=frames.device)
+                    self.net.run(paf, heat)
+                frames.record_stream(st)
+                paf.record_stream(cur)
+                heat.record_stream(cur)
+                cur.wait_stream(st)
+                geoms.append((nh, nw, vh, vw))
+                pafs.append(paf)
+                heats.append(heat)
+            return geoms, pafs, heats
         for (m, nh, nw, vh, vw) in scale_geometry(H, W, self.scale_search):
             gh, gw = self.net.preprocess(frames, m)
             assert (gh, gw) == (nh, nw)

@@ -82,14 +82,23 @@ class HandEstimator:
         return np.concatenate(out)
 
     def run_crops(self, frames_t, boxes):
-        """The hand net over all crops, one batch per scale -> low-res heat [n,22,h8,w8] per scale."""
+        """The hand net over all crops, one batch per scale -> low-res heat [n,22,h8,w8] per
+        scale.  The scales run side by side, each on its own stream forked from the current
+        one and joined back (every scale has its own arena, table and split-K workspace in
+        the net): the small scales' grids fill the CUs the large ones leave idle."""
         import torch
         crops = [(f, x, y, w, w) for (f, x, y, w) in boxes]
+        cur = torch.cuda.current_stream(frames_t.device)
         heats = []
-        for s in self.scale_search:
-            gh, gw = self.net.preprocess_crops(frames_t, crops, s * BOXSIZE)
-            heat = torch.empty((len(crops), 22, gh // 8, gw // 8), device=frames_t.device)
-            self.net.run(heat)
+        for st, s in zip(rt.scale_streams(self, frames_t.device, len(self.scale_search)), self.scale_search):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                gh, gw = self.net.preprocess_crops(frames_t, crops, s * BOXSIZE)
+                heat = torch.empty((len(crops), 22, gh // 8, gw // 8), device=frames_t.device)
+                self.net.run(heat)
+            frames_t.record_stream(st)
+            heat.record_stream(cur)
+            cur.wait_stream(st)
             heats.append(heat)
         return heats
 

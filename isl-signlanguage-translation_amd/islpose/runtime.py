@@ -126,6 +126,15 @@ def stream_handle(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+def scale_streams(owner, device, k):
+    """k HIP streams kept on `owner` (an estimator) for its pyramid scales."""
+    import torch
+    ss = getattr(owner, "_scale_streams", None)
+    if ss is None or len(ss) < k:
+        ss = owner._scale_streams = [torch.cuda.Stream(device) for _ in range(k)]
+    return ss[:k]
+
+
 def ptr(t) -> ctypes.c_void_p:
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 

@@ -138,9 +138,14 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   static_assert(WSLAB % 64 == 0, "weight slab is whole 1 KiB DMA pieces");
   static_assert(BPX <= SEGMAX, "segment must hold a tile");
   constexpr bool UNION = (VAR & 512) != 0;
+  // VAR 65536: one input buffer (two barriers per step) so that a wider pixel tile fits
+  // beside the double-buffered weight slabs (7x7 on 384 pixels: the 56 KiB slab per step
+  // is amortised over 1.5x the pixels)
+  constexpr bool SIB = (VAR & 65536) != 0;
   constexpr int SEGUP = x3_segu_max() + 1;       // + dummy slot
   constexpr int XSLABU = 2 * 2 * SEGUP;          // [hi|lo][h][px]
-  constexpr int SMEM = UNION ? 2 * WSLAB + 2 * XSLABU : 2 * BUF;
+  constexpr int SMEM = UNION ? 2 * WSLAB + 2 * XSLABU : SIB ? 2 * WSLAB + XSLAB : 2 * BUF;
+  static_assert(!(SIB && UNION), "one input buffer: generic loop only");
   static_assert(SMEM * 16 <= 160 * 1024, "LDS");
   constexpr bool RANGED = (VAR & 1024) != 0;
   constexpr bool SPLIT = (VAR & 2048) != 0;
@@ -376,8 +381,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
         }
       }
     };
+    auto wbuf = [&](int buf) __attribute__((always_inline)) { return smem + buf * (SIB ? WSLAB : BUF); };
+    auto xbuf = [&](int buf) __attribute__((always_inline)) { return SIB ? smem + 2 * WSLAB : smem + buf * BUF + WSLAB; };
     auto store_x = [&](int buf) __attribute__((always_inline)) {
-      f16x8* s = smem + buf * BUF + WSLAB;
+      f16x8* s = xbuf(buf);
 #pragma unroll
       for (int i = 0; i < IT; ++i) {
         if (ipx[i] < 0) continue;
@@ -394,7 +401,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     };
     auto issue_w = [&](int t, int buf) __attribute__((always_inline)) {
       const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
-      f16x8* dst = smem + buf * BUF;
+      f16x8* dst = wbuf(buf);
 #pragma unroll
       for (int q0 = 0; q0 < WSLAB / 64; q0 += NWAVES) {
         const int q = q0 + wave_u;
@@ -406,8 +413,8 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     auto compute = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
       for (int pp = 0; pp < PPS; ++pp) {
-        const f16x8* sw = smem + buf * BUF + pp * WSLAB1 + h * BCO + wave_m * WM * 32 + l32;
-        const f16x8* sx = smem + buf * BUF + WSLAB + (2 * pp + h) * SEGP;
+        const f16x8* sw = wbuf(buf) + pp * WSLAB1 + h * BCO + wave_m * WM * 32 + l32;
+        const f16x8* sx = xbuf(buf) + (2 * pp + h) * SEGP;
 #pragma unroll
         for (int kx = 0; kx < KS; ++kx) tap(sw, sx, PPS * SEGP, kx);
       }
@@ -448,6 +455,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
             }
         }
       }
+      if constexpr (SIB) __syncthreads();         // every wave is done with the one input buffer
       if (t + 1 < t1) store_x(buf ^ 1);
       __syncthreads();
     }
@@ -915,21 +923,39 @@ bool x3_wide1(const ConvLaunch& c) {
 // X3_WIDE7_COST 128-pixel blocks (measured over 92^2 / 69^2 / 46x82 grids at batch
 // 13-64, tools/gpu_wide7.sh).  Both pack the weights for 128-channel tiles.
 constexpr double X3_WIDE7_COST = 1.74;
+// a round of 384-pixel blocks (12 waves, one input buffer): 2.58 rounds of 128 pixels,
+// from the hand's 92^2 layers (tools/gpu_w384.sh, profiles/r02/w384/)
+constexpr double X3_W384_COST = 2.58;
 
 static int x3_wide7_mode() {   // ISLPOSE_X3_WIDE7: 0 never, 1 always (A/B), default by the estimate
   static const int m = getenv("ISLPOSE_X3_WIDE7") ? atoi(getenv("ISLPOSE_X3_WIDE7")) : 2;
   return m;
 }
 
-static bool x3_wide7(const ConvLaunch& c) {
-  if (c.ks != 7 || c.bco != 128 || x3_small_tiles() || x3_canonical_ranges(c) > 1) return false;
+// pixels per 7x7 tile (128, 256 or 384), chosen per launch by grid quantisation: rounds
+// of one block per CU, a round of 256- / 384-pixel blocks costing X3_WIDE7_COST /
+// X3_W384_COST of a 128-pixel round.  ISLPOSE_X3_WIDE7=0|1|3 forces 128 / 256 / 384 (A/B).
+static int x3_7x7_bpx(const ConvLaunch& c) {
+  if (c.ks != 7 || c.bco != 128 || x3_small_tiles() || x3_canonical_ranges(c) > 1) return 128;
   const int mode = x3_wide7_mode();
-  if (mode != 2) return mode == 1;
+  if (mode != 2) return mode == 1 ? 256 : mode == 3 ? 384 : 128;
   const long long HW = (long long)c.H * c.W, co = (c.cout + 127) / 128, cus = device_cus();
-  const int t1 = tile_pixels(c, 128, x3_segmax(128)), t2 = tile_pixels(c, 256, x3_segmax(256));
-  const long long b1 = c.n * ((HW + t1 - 1) / t1) * co, b2 = c.n * ((HW + t2 - 1) / t2) * co;
-  return (double)((b2 + cus - 1) / cus) * X3_WIDE7_COST < (double)((b1 + cus - 1) / cus);
+  int best = 128;
+  double best_t = 0.0;
+  for (int bpx : {128, 256, 384}) {
+    const int t = tile_pixels(c, bpx, x3_segmax(bpx));
+    const long long b = c.n * ((HW + t - 1) / t) * co;
+    const double cost = bpx == 128 ? 1.0 : bpx == 256 ? X3_WIDE7_COST : X3_W384_COST;
+    const double tt = (double)((b + cus - 1) / cus) * cost;
+    if (bpx == 128 || tt < best_t) { best = bpx; best_t = tt; }
+  }
+  return best;
 }
+
+static bool x3_wide7(const ConvLaunch& c) { return x3_7x7_bpx(c) == 256; }
+
+// 7x7 on 384-pixel tiles (VAR 65536, one input buffer)
+static bool x3_wide7_384(const ConvLaunch& c) { return x3_7x7_bpx(c) == 384; }
 
 // Row-union staging (VAR 512) when the longest union run of any 512-pixel tile fits.
 // longest row-union run (pixels) over the 512-pixel tiles of a layer
@@ -962,7 +988,7 @@ struct X3Ranges {
 
 static X3Ranges x3_ranges(const ConvLaunch& c) {
   X3Ranges r;
-  if (x3_big_tiles(c) || x3_wide7(c)) return r;
+  if (x3_big_tiles(c) || x3_7x7_bpx(c) != 128) return r;
   const int tpx = tile_pixels(c, 128, x3_segmax(128));
   const long long blocks = (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * ((c.cout + c.bco - 1) / c.bco);
   const int cus = device_cus(), pairs = (c.cin_chunks + 1) / 2;
@@ -1035,6 +1061,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
     // of 64co x 32px on 128 pixels (one block per CU either way: the 56 KiB weight
     // slabs; 8 waves measured 2-6 % over 4 waves of 64co x 64px / x 128px)
     if (c.ksplit <= 1 && c.bco == 128) {
+      if (x3_wide7_384(c)) return launch_t<KS, 2, 6, 2, 2, 65536, 1>(c, s);   // 12 waves, 384 px
       if (x3_wide7(c)) return launch_t<KS, 2, 4, 2, 2, 0, 1>(c, s);
       return launch_t<KS, 2, 4, 2, 1, 0, 1>(c, s);
     }
@@ -1094,7 +1121,7 @@ bool x3_hpool_ok(const ConvLaunch& c) {
 }
 
 double conv_x3_mfma_flops(const ConvLaunch& c) {
-  const int BPX = x3_big_tiles(c) ? x3_big_bpx(c) : x3_wide7(c) ? 256 : 128;
+  const int BPX = x3_big_tiles(c) ? x3_big_bpx(c) : x3_wide7_384(c) ? 384 : x3_wide7(c) ? 256 : 128;
   const double co = (double)((c.cout + c.bco - 1) / c.bco) * c.bco;
   const double px = std::ceil((double)c.H * c.W / tile_pixels(c, BPX, x3_segmax(BPX))) * BPX;
   return 3.0 * 2.0 * co * (((c.cin_chunks + 1) / 2) * 16.0) * c.ks * c.ks * px * c.n;

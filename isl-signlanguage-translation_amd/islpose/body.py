@@ -234,7 +234,7 @@ class BodyEstimator:
                                        rt.stream_handle()), "isl_body_post")
         host = torch.empty(res.shape, dtype=torch.uint8, pin_memory=True)
         host.copy_(res, non_blocking=True)
-        flag = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        flag = rt.flag_slot(self)
         self.net.check_async(flag)
         ev = torch.cuda.Event()
         ev.record()

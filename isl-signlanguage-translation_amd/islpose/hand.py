@@ -36,11 +36,19 @@ class HandEstimator:
         import torch
         n, h, w, _ = crops.shape
         geoms, heats = [], []
-        for (m, nh, nw, vh, vw) in scale_geometry(h, w, self.scale_search):
-            gh, gw = self.net.preprocess(crops, m)
-            assert (gh, gw) == (nh, nw)
-            heat = torch.empty((n, 22, nh // 8, nw // 8), device=crops.device)
-            self.net.run(heat)
+        cur = torch.cuda.current_stream(crops.device)
+        # the scales side by side on their own streams, as run_crops
+        for st, (m, nh, nw, vh, vw) in zip(rt.scale_streams(self, crops.device, len(self.scale_search)),
+                                           scale_geometry(h, w, self.scale_search)):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                gh, gw = self.net.preprocess(crops, m)
+                assert (gh, gw) == (nh, nw)
+                heat = torch.empty((n, 22, nh // 8, nw // 8), device=crops.device)
+                self.net.run(heat)
+            crops.record_stream(st)
+            heat.record_stream(cur)
+            cur.wait_stream(st)
             geoms.append((nh, nw, vh, vw))
             heats.append(heat)
         return geoms, heats
@@ -107,6 +115,8 @@ class HandEstimator:
         peaks to pinned host memory, stream-ordered range check); finish_crops(job)
         completes it."""
         import torch
+        if not boxes:      # nothing to enqueue (and no flag copy left in flight into a freed buffer)
+            return dict(t=frames_t, boxes=boxes, parts=[], flag=None, ev=None)
         parts = []
         for c in range(0, len(boxes), CROP_CHUNK):
             part = boxes[c:c + CROP_CHUNK]
@@ -115,7 +125,7 @@ class HandEstimator:
             host = torch.empty(out.shape, dtype=torch.int64, pin_memory=True)
             host.copy_(out, non_blocking=True)
             parts.append((part, heats, out, host))
-        flag = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        flag = rt.flag_slot(self)
         self.net.check_async(flag)
         ev = torch.cuda.Event()
         ev.record()

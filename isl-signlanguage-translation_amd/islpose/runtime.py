@@ -126,6 +126,21 @@ def stream_handle(stream=None):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+def flag_slot(owner, ring: int = 4):
+    """A pinned int32 slot for Net.check_async, from a ring kept on `owner` for its life
+    (the copy into it is issued outside torch, so the buffer must never go back to torch's
+    pinned cache while a copy may be in flight); at most `ring` launches in flight."""
+    import torch
+    slots = getattr(owner, "_flag_slots", None)
+    if slots is None:
+        slots = owner._flag_slots = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(ring)]
+        owner._flag_next = 0
+    f = slots[owner._flag_next % len(slots)]
+    owner._flag_next += 1
+    f.zero_()
+    return f
+
+
 def scale_streams(owner, device, k):
     """k HIP streams kept on `owner` (an estimator) for its pyramid scales."""
     import torch

@@ -295,7 +295,7 @@ constexpr int NMS_SEG = 14;                        // g outputs per thread in th
 // (stage-1 cv2.resize x8, cropped: body.py:68-73 when the net input is the frame),
 // with resize_sep_kernel's exact operation order.  Only scale 1/8 is fused.
 constexpr int NMS_SRC_ROWS = 16;
-constexpr int NMS_SRC_COLS = 40;                   // low-res columns (218 / 8 + 5 = 33 at scale 1/8)
+constexpr int NMS_SRC_COLS = 48;                   // source columns (218 / 8 + 5 = 33 at scale 1/8; 42 at 1/5.9)
 
 // [min, max] of reflect_idx(i, n) over i in [lo, hi]
 __device__ __forceinline__ void reflect_range(int lo, int hi, int n, int* a, int* b) {
@@ -1984,7 +1984,14 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   const bool multi = nscales > 1;
   // single scale with the net input at frame size (one x8 resize): fuse resize + blur,
   // no full-resolution heat planes
-  const bool fused = !multi && geom[0].valid_h == H && geom[0].valid_w == W && fused_blur_enabled();
+  // single scale, two stages (Mode R on large frames: 184 x 327 -> 1080 x 1920): the
+  // second resize is a strong upsampling whose full-resolution planes cost more HBM
+  // traffic than the on-the-fly resize; fused too when a blur tile's source window fits
+  // the LDS window (~1/5.2 and below; at 368 x 656, scale 1/2, it does not)
+  const bool fuse2 = !multi && !(geom[0].valid_h == H && geom[0].valid_w == W) &&
+                     41.0 * geom[0].valid_h / H + 6.0 <= NMS_SRC_ROWS &&
+                     217.0 * geom[0].valid_w / W + 6.0 <= NMS_SRC_COLS;
+  const bool fused = !multi && ((geom[0].valid_h == H && geom[0].valid_w == W) || fuse2) && fused_blur_enabled();
   const size_t heat_bytes = fused ? 0 : (size_t)n * nparts * H * W * (multi ? 8 : 4);
   size_t mid_bytes = 0;
   for (int si = 0; si < nscales; ++si) {

@@ -253,6 +253,29 @@ def test_fused_resize_blur_matches_unfused(est25, monkeypatch, H, W):
         assert np.array_equal(fused[i].subset, subset), i
 
 
+@pytest.mark.parametrize("H,W", [(1000, 1000), (1080, 1920)])
+def test_fused_two_stage_post_matches_unfused(est25, monkeypatch, H, W):
+    """Mode R on large frames (scale 0.5: net 184 px tall, then a >5x second resize): the
+    second resize fused into blur_nms (no full-resolution planes) == the materialised
+    two-kernel path == the oracle, on noisy maps around the 0.1 threshold."""
+    geoms = [g[1:] for g in scale_geometry(H, W, (0.5,))]
+    nh, nw = geoms[0][0] // 8, geoms[0][1] // 8
+    rng = np.random.RandomState(H + W)
+    pl, hl = synth.designed_pose_maps(nh, nw, 2, 300)
+    hl = hl + (rng.uniform(0.0, 0.16, hl.shape) * (rng.rand(*hl.shape) < 0.15)).astype(np.float32)
+    paf, heat = torch.from_numpy(pl[None]).cuda(), torch.from_numpy(hl[None]).cuda()
+    monkeypatch.setenv("ISLPOSE_FUSED_BLUR", "1")
+    fused = est25.post_maps(H, W, geoms, [paf], [heat])[0]
+    monkeypatch.setenv("ISLPOSE_FUSED_BLUR", "0")
+    plain = est25.post_maps(H, W, geoms, [paf], [heat])[0]
+    assert np.array_equal(fused.candidate, plain.candidate) and np.array_equal(fused.subset, plain.subset)
+    heat_avg, paf_avg = cpu_ref.body_maps(np.zeros((H, W, 3), np.uint8), lambda im: (pl[None], hl[None]),
+                                          "body25", (0.5,))
+    cand, subset, _, _ = cpu_ref.body_post(heat_avg, paf_avg, "body25", H)
+    assert np.array_equal(fused.candidate, cand) and np.array_equal(fused.subset, subset)
+    assert len(cand) > 0
+
+
 def test_fused_post_reads_the_arena(est25, monkeypatch):
     """Mode N estimate (scale 1.0: the fused resize + blur) reading the net's own arena
     output == the same maps handed over as caller tensors == the unfused kernels."""

@@ -19,8 +19,10 @@ from islpose.body import BodyEstimator, scale_geometry  # noqa: E402
 
 
 def main():
-    B, H, W = 32, 368, 656
     scale = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
+    H = int(sys.argv[2]) if len(sys.argv) > 2 else 368          # frame size (e.g. 1080 1920)
+    W = int(sys.argv[3]) if len(sys.argv) > 3 else 656
+    B = 32
     est = BodyEstimator(synth.synth_weights(0), "body25")
     geoms = [g[1:] for g in scale_geometry(H, W, (scale,))]
     nh, nw = geoms[0][0] // 8, geoms[0][1] // 8

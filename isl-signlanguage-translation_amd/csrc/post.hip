@@ -196,7 +196,7 @@ struct MapSrcN {   // up to MAX_SCALES (8) scales
   MapSrc m[8];
 };
 __global__ void __launch_bounds__(256) resize_acc_kernel(MapSrcN ms, int ns, int nch, int oh, int ow, int ty_rows,
-                                                         float div_f, double* out) {
+                                                         float div_f, int quirk, double* out) {
   __shared__ float s_h[RS_MAXR][RS_TX];
   const int plane = blockIdx.x, f = plane / nch, c = plane - f * nch;
   const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * RS_TX + threadIdx.x;
@@ -252,7 +252,8 @@ __global__ void __launch_bounds__(256) resize_acc_kernel(MapSrcN ms, int ns, int
                    : ((h0 * be[0] + h1 * be[1]) + h2 * be[2]) + h3 * be[3];
         }
         const float q = v / div_f;      // heatmap / len(multiplier), float32
-        acc[t] = acc[t] + (double)q;    // hand.py:56, from np.zeros (0.0 + x included)
+        // from np.zeros (0.0 + x included): hand.py:56, or body.py:80's doubling quirk
+        acc[t] = quirk ? acc[t] + (acc[t] + (double)q) : acc[t] + (double)q;
       }
     }
   }
@@ -2022,6 +2023,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
 
   GroupArgs ga;
   memset(&ga, 0, sizeof(ga));
+  MapSrcN fin;                      // multi-scale: every scale's final-resolution heat source
   char* midp = mid;
   MapSrc fused_src{};
   const float div_f = (float)nscales;
@@ -2060,8 +2062,22 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       fp = lp;
     }
     if (fused) fused_src = fh;   // no full-resolution heat: blur_nms resizes on the fly
-    else if ((rc = launch_resize(fh, n, nparts, H, W, multi ? (si == 0 ? 2 | 8 : 2) : 1, div_f, heat, s))) return rc;
+    else if (multi) fin.m[si] = fh;   // every scale's final resize, one fp64 pass below
+    else if ((rc = launch_resize(fh, n, nparts, H, W, 1, div_f, heat, s))) return rc;
     ga.paf[si] = fp;
+  }
+  if (multi) {
+    // heatmap_avg += heatmap_avg + heatmap / len(m) over the scales (body.py:80, the
+    // doubling quirk) in fp64 registers, one store (resize_acc_kernel)
+    int ty = RA_TY;
+    for (int si = 0; si < nscales; ++si)
+      if (!fin.m[si].identity)
+        while (ty > 1 && (ty - 1) * fin.m[si].scy + 5.0 > (double)RS_MAXR) --ty;
+    const long long ty_tiles = (H + ty - 1) / ty;
+    if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "body post: frame too tall");
+    hipLaunchKernelGGL(resize_acc_kernel, dim3(n * nparts, (unsigned)ty_tiles, (W + RS_TX - 1) / RS_TX), dim3(RS_TX),
+                       0, s, fin, nscales, nparts, H, W, ty, div_f, 1, (double*)heat);
+    PHIP(hipGetLastError());
   }
   // blur + NMS (body.py:86-100)
   dim3 gb((W + NMS_TX - 1) / NMS_TX, (H + NMS_TY - 1) / NMS_TY, n * nparts);
@@ -2189,7 +2205,7 @@ static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, cons
     const long long ty_tiles = (h + ty - 1) / ty;
     if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "hand post: crop too tall");
     hipLaunchKernelGGL(resize_acc_kernel, dim3(n * nparts, (unsigned)ty_tiles, (w + RS_TX - 1) / RS_TX), dim3(RS_TX),
-                       0, s, fin, nscales, nparts, h, w, ty, div_f, avg);
+                       0, s, fin, nscales, nparts, h, w, ty, div_f, 0, avg);
     PHIP(hipGetLastError());
   }
   dim3 gb((w + NMS_TX - 1) / NMS_TX, (h + NMS_TY - 1) / NMS_TY, n * nparts);

@@ -2154,7 +2154,8 @@ static size_t hand_post_bytes(int n, int h, int w, int nscales, const isl_scale_
 // the kernels of one hand post (hand.py:51-74) on stream s, scratch at base
 // (hand_post_bytes); heat planes of scale si at d_heat[si] (NULL: the arena output)
 static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, const isl_scale_geom* geom,
-                            const float* const* d_heat, int64_t* d_peaks, hipStream_t s, char* base) {
+                            const float* const* d_heat, int64_t* d_peaks, hipStream_t s, char* base,
+                            const float* const* mid_pre = nullptr) {
   const int nparts = 21, nch = 22;
   const size_t P = (size_t)h * w;
   const int words = (w + 63) / 64;
@@ -2188,8 +2189,10 @@ static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, cons
     lh.dh = h8 * 8; lh.dw = w8 * 8; lh.scy = lh.scx = 1.0 / 8.0; lh.cn = nch; lh.identity = 0;
     MapSrc fh = lh;
     if (!(g.valid_h == h && g.valid_w == w)) {
-      if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, midp, s))) return rc;
-      fh.base = midp; fh.xs = 1; fh.ys = g.valid_w; fh.cstr = (long long)g.valid_h * g.valid_w;
+      const float* mid_s = midp;
+      if (mid_pre && mid_pre[si]) mid_s = mid_pre[si];   // stage 1 done for the whole crop batch
+      else if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, midp, s))) return rc;
+      fh.base = mid_s; fh.xs = 1; fh.ys = g.valid_w; fh.cstr = (long long)g.valid_h * g.valid_w;
       fh.fs = (long long)nparts * g.valid_h * g.valid_w;
       fh.cshift = 30; fh.cbig = 0;
       fh.sh = g.valid_h; fh.sw = g.valid_w; fh.dh = h; fh.dw = w;
@@ -2293,17 +2296,50 @@ extern "C" int isl_hand_post_crops(isl_net* net, int n, const int32_t* crop_w, i
       L->bytes[k] = need;
     }
   }
+  // Stage 1 of every scale (low-res x8 -> the net's valid size) for the whole crop batch, one
+  // launch per scale on the caller's stream: every crop has the same net and valid size per
+  // scale (round(s * 368) for square crops), so only the per-crop final resize onto the crop
+  // is left to the lanes.  Scales whose valid size differs between crops stay per crop.
+  float* mid_all[MAX_SCALES] = {};
+  {
+    size_t tot = 0, off[MAX_SCALES] = {};
+    for (int si = 0; si < nscales; ++si) {
+      bool same = true;
+      for (int i = 1; i < n; ++i)
+        same &= geom[i * nscales + si].valid_h == geom[si].valid_h && geom[i * nscales + si].valid_w == geom[si].valid_w;
+      if (!same) continue;
+      off[si] = tot + 1;   // + 1: "present"
+      tot += ((size_t)n * 21 * geom[si].valid_h * geom[si].valid_w * 4 + 255) / 256 * 256;
+    }
+    if (tot) {
+      char* base = (char*)net_scratch(net, tot);
+      if (!base) return ISL_E_HIP;
+      for (int si = 0; si < nscales; ++si) {
+        if (!off[si]) continue;
+        const isl_scale_geom& g = geom[si];
+        const int h8 = g.net_h / 8, w8 = g.net_w / 8;
+        MapSrc lh;
+        int rc = low_src(net, d_heat[si], 0, n, 22, h8, w8, &lh);
+        if (rc) return rc;
+        lh.dh = h8 * 8; lh.dw = w8 * 8; lh.scy = lh.scx = 1.0 / 8.0; lh.cn = 22; lh.identity = 0;
+        mid_all[si] = (float*)(base + off[si] - 1);
+        if ((rc = launch_resize(lh, n, 21, g.valid_h, g.valid_w, 1, 1.f, mid_all[si], s))) return rc;
+      }
+    }
+  }
   PHIP(hipEventRecord(L->fork, s));
   for (int k = 0; k < nl; ++k) PHIP(hipStreamWaitEvent(L->stream[k], L->fork, 0));
   for (int i = 0; i < n; ++i) {
     const int k = i % nl;
     const float* hp[MAX_SCALES];
+    const float* mp[MAX_SCALES];
     for (int si = 0; si < nscales; ++si) {
       const isl_scale_geom& g = geom[si];
       hp[si] = d_heat[si] + (size_t)i * 22 * (g.net_h / 8) * (g.net_w / 8);
+      mp[si] = mid_all[si] ? mid_all[si] + (size_t)i * 21 * g.valid_h * g.valid_w : nullptr;
     }
     const int rc = hand_post_launch(net, 1, crop_w[i], crop_w[i], nscales, geom + (size_t)i * nscales, hp,
-                                    d_peaks + (size_t)i * 42, L->stream[k], (char*)L->scratch[k]);
+                                    d_peaks + (size_t)i * 42, L->stream[k], (char*)L->scratch[k], mp);
     if (rc) return rc;
   }
   for (int k = 0; k < nl; ++k) {

@@ -57,3 +57,23 @@ def test_body_layout():
     assert lay.peaks % 8 == 0 and lay.record_bytes % 8 == 0
     assert lay.subset + 8 * 27 * 8 <= lay.record_bytes
     assert lay.conns - lay.peaks == 25 * 16 * 3 * 8
+
+
+def test_new_entry_points_reject_bad_arguments():
+    """The batched / pipelined entry points fail with ISL_E_ARG before any device work:
+    NULL net or buffers, an empty crop list, a crop of the wrong net (a body net)."""
+    if not os.path.exists(rt.LIB_PATH):
+        pytest.skip("libislpose.so not built")
+    L = rt.lib()
+    vp = ctypes.c_void_p
+    ws = (ctypes.c_int32 * 1)(100)
+    g = (rt.IslScaleGeom * 1)(rt.IslScaleGeom(184, 184, 184, 184))
+    hp = (vp * 1)(vp(16))
+    assert L.isl_hand_post_crops(None, 1, ws, 1, g, hp, vp(16), None) == rt.ISL_E_ARG
+    body = rt.Net(rt.ISL_BODY25)
+    assert L.isl_hand_post_crops(body.h, 0, ws, 1, g, hp, vp(16), None) == rt.ISL_E_ARG
+    assert L.isl_hand_post_crops(body.h, 1, ws, 1, g, hp, vp(16), None) == rt.ISL_E_ARG   # not a hand net
+    assert L.isl_net_check_async(None, vp(16), None) == rt.ISL_E_ARG
+    assert L.isl_net_check_async(body.h, None, None) == rt.ISL_E_ARG
+    assert L.isl_debug_np_sum(None, 8, vp(16), None) == rt.ISL_E_ARG
+    assert L.isl_debug_np_sum(vp(16), 0, vp(16), None) == rt.ISL_E_ARG

@@ -145,6 +145,7 @@ int net_device(const isl_net* net);
 int net_low_res(isl_net* net, int which, MapSrc* m);
 // grow-only device scratch owned by the net (nullptr + error on failure)
 void* net_scratch(isl_net* net, size_t bytes);
+size_t net_scratch_size(const isl_net* net);
 // streams on which isl_hand_post_crops runs its crops side by side, forked from and
 // joined back into the caller's stream; a grow-only scratch per lane
 constexpr int ISL_POST_LANES = 4;

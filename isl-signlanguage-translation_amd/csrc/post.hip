@@ -2312,6 +2312,8 @@ extern "C" int isl_hand_post_crops(isl_net* net, int n, const int32_t* crop_w, i
       tot += ((size_t)n * 21 * geom[si].valid_h * geom[si].valid_w * 4 + 255) / 256 * 256;
     }
     if (tot) {
+      if (tot > net_scratch_size(net))   // the buffer is reallocated: the lanes may still read it
+        for (int k = 0; k < ISL_POST_LANES; ++k) PHIP(hipStreamSynchronize(L->stream[k]));
       char* base = (char*)net_scratch(net, tot);
       if (!base) return ISL_E_HIP;
       for (int si = 0; si < nscales; ++si) {

@@ -912,6 +912,8 @@ void* net_scratch(isl_net* net, size_t bytes) {
   return net->scratch;
 }
 
+size_t net_scratch_size(const isl_net* net) { return net->scratch_bytes; }
+
 PostLanes* net_post_lanes(isl_net* net) {
   if (net->lanes) return net->lanes;
   PostLanes* L = new PostLanes();

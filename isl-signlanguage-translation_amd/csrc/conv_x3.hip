@@ -112,6 +112,27 @@ __device__ __forceinline__ void x3_vin_load(const float* src, int yy, int xx, co
   hi4 = float4{fmaxf(a1.x, b1.x), fmaxf(a1.y, b1.y), fmaxf(a1.z, b1.z), fmaxf(a1.w, b1.w)};
 }
 
+// x = hi + lo for 8 fp32 values: packed RNE conversions (v_cvt_pk_f16_f32), hi converted
+// back once for the residual -- the same bits as hi = (f16)x; lo = (f16)(x - (f32)hi)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void x3_split8(const f32x4& a, const f32x4& b, f16x8& hi, f16x8& lo) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x2 x = k < 2 ? f32x2{a[2 * k], a[2 * k + 1]} : f32x2{b[2 * k - 4], b[2 * k - 3]};
+    const f16x2 h = __builtin_convertvector(x, f16x2);
+    const f32x2 hf = __builtin_convertvector(h, f32x2);
+    // two scalar subtractions: hipcc would pack them into v_pk_add_f32, which beside the
+    // other waves' MFMAs measured 0.6 % slower (tools/gpu_split_ab.sh, profiles/r02/split_ab/)
+    f32x2 r;
+    asm volatile("v_sub_f32 %0, %1, %2" : "=v"(r.x) : "v"(x.x), "v"(hf.x));
+    asm volatile("v_sub_f32 %0, %1, %2" : "=v"(r.y) : "v"(x.y), "v"(hf.y));
+    const f16x2 l = __builtin_convertvector(r, f16x2);
+    hi[2 * k] = h.x; hi[2 * k + 1] = h.y;
+    lo[2 * k] = l.x; lo[2 * k + 1] = l.y;
+  }
+}
+
 // input segment capacity in pixels for a BPX-pixel tile (host: tile_pixels)
 constexpr int x3_segmax(int bpx) { return bpx + 64; }
 // capacity of the row-union run (VAR 512): 2 x (1536 + 4 x 857) x 16 B = 155 KiB of LDS
@@ -276,14 +297,11 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     };
     auto store_c = [&](int c2, int ky, int bx) __attribute__((always_inline)) {
       f16x8* sx = smem + 2 * WSLAB + bx * XSLABU;
-      const bool zero = 2 * c2 + c_ih[ky] >= a.cin_chunks;   // missing odd chunk: zeroed here, at the use
+      // a missing odd chunk stages the last real chunk again (load_c clamps): its packed
+      // weights are zero (pack_x3), and the staged values are finite (range-checked), so
+      // it adds exact zeros
       f16x8 hi, lo;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = zero ? 0.f : ru[j >> 2][j & 3];
-        hi[j] = (_Float16)x;
-        lo[j] = (_Float16)(x - (float)hi[j]);
-      }
+      x3_split8(ru[0], ru[1], hi, lo);
       const int px = c_px[ky] < 0 ? SEGUP - 1 : c_px[ky];   // idle items: the dummy slot
       sx[(0 * 2 + c_ih[ky]) * SEGUP + px] = hi;
       sx[(1 * 2 + c_ih[ky]) * SEGUP + px] = lo;
@@ -389,12 +407,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       for (int i = 0; i < IT; ++i) {
         if (ipx[i] < 0) continue;
         f16x8 hi, lo;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float x = raw[i][j >> 2][j & 3];
-          hi[j] = (_Float16)x;
-          lo[j] = (_Float16)(x - (float)hi[j]);
-        }
+        x3_split8(raw[i][0], raw[i][1], hi, lo);
         s[(0 * 2 * PPS + ih[i]) * SEGP + ipx[i]] = hi;
         s[(1 * 2 * PPS + ih[i]) * SEGP + ipx[i]] = lo;
       }

@@ -1328,12 +1328,24 @@ __global__ void __launch_bounds__(256) cc_find_kernel(int h, int w, int rows, in
   const int P = h * w, p0 = c * rows * w, p1 = min(P, p0 + rows * w);
   int* parent = parent_all + (size_t)plane * P;
   double* vals = vals_all + (size_t)plane * P;
-  for (int p = p0 + threadIdx.x; p < p1; p += 256)
-    if (ld_parent(parent, p) >= 0) {
-      const int r = uf_root(parent, p);
-      __hip_atomic_store(parent + p, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (r == p) vals[p] = 0.0;   // a root: its cc_sum accumulator (only roots are ever read)
+  // a thread's pixels (256 apart) mostly share their chunk-local root: its walk up the
+  // merged chunk roots is done once and reused while that local root repeats (roots are
+  // final here; p's own slot is written only by this thread)
+  int last_q = -1, last_r = -1;
+  for (int p = p0 + threadIdx.x; p < p1; p += 256) {
+    const int q = ld_parent(parent, p);
+    if (q < 0) continue;
+    int r;
+    if (q == last_q) {
+      r = last_r;
+    } else {
+      r = uf_root(parent, q);
+      last_q = q;
+      last_r = r;
     }
+    __hip_atomic_store(parent + p, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r == p) vals[p] = 0.0;   // a root: its cc_sum accumulator (only roots are ever read)
+  }
 }
 
 __global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ planes, int h, int w, int rows,

@@ -79,6 +79,11 @@ def parse(argv=None):
                         "batch-dependent split of small grids); the default is mode 1 (canonical ranges)")
     p.add_argument("--dry-run", action="store_true",
                    help="no GPU: run the rank launch, shard and max-over-ranks timing structure only")
+    p.add_argument("--fail-rank", type=int, default=-1,
+                   help="test only (with --dry-run): this rank exits 1 after the group is up, so the "
+                        "launcher's fail-fast path is exercised (tests/test_bench_launch.py)")
+    p.add_argument("--pg-timeout", type=float, default=120.0,
+                   help="seconds a gloo collective (init, barrier, gather) may block before the rank fails")
     return p.parse_args(argv)
 
 
@@ -87,17 +92,19 @@ def rank_env():
             int(os.environ.get("WORLD_SIZE", "1")))
 
 
-def init_group(world):
+def init_group(world, timeout_s=120.0):
     """Host-side (gloo) group for the barrier and the timing reductions only.  gloo
     prints its connection lines on the process's stdout: they go to stderr here, so
-    rank 0's stdout carries only the JSON line."""
+    rank 0's stdout carries only the JSON line.  An explicit timeout bounds every
+    collective: a rank whose peer died fails instead of blocking for torch's default."""
     if world > 1:
+        import datetime
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         sys.stdout.flush()
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
-            torch.distributed.init_process_group("gloo")
+            torch.distributed.init_process_group("gloo", timeout=datetime.timedelta(seconds=timeout_s))
             torch.distributed.barrier()
         finally:
             sys.stdout.flush()
@@ -128,11 +135,16 @@ def main():
         codes, out0 = parallel.spawn_ranks([os.path.abspath(__file__)] + sys.argv[1:], args.gpus)
         sys.stdout.write(out0 or "")
         sys.stdout.flush()
-        sys.exit(next((c for c in codes if c), 0))
+        # a rank's own failure (positive code) wins over the signal codes of the siblings
+        # the launcher terminated after it
+        bad = [c for c in codes if c > 0] or [1 for c in codes if c]
+        if bad:
+            print("bench.py: rank exit codes %s" % codes, file=sys.stderr)
+        sys.exit(bad[0] if bad else 0)
     rank, local, world = rank_env()
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
-    init_group(world)
+    init_group(world, args.pg_timeout)
     try:
         if args.dry_run:
             dry_run(args, rank, world)
@@ -148,6 +160,9 @@ def dry_run(args, rank, world):
     'processes' its own frame shard per step; rank 0 prints what the real run
     would report about ranks and shards."""
     lo, hi = frame_shard(rank, args.batch)
+    if rank == args.fail_rank:
+        print("bench.py: rank %d failing on request (--fail-rank)" % rank, file=sys.stderr, flush=True)
+        os._exit(1)
     for _ in range(args.warmup):
         pass
     if world > 1:
@@ -303,6 +318,10 @@ def gpu_main(args, rank, local, world):
     elapsed = time.perf_counter() - t0
     for ln in lanes:
         ln.net.set_timing(False)
+    # range guard over the timed steps (outside the timed region): a set flag would mean a
+    # batch needed the fp32 recompute the timed loop did not do
+    range_timed = sum(0 if ln.net.range_ok() else 1 for ln in lanes)
+    range_trips = sum(ln.net.range_trips() for ln in lanes)
     ops = [ln.net.timing() for ln in lanes]
     net_ms = float(np.mean([net_window_ms(r, m) for r, m in ev]))
     post_ms = float(np.mean([post_window_ms(r, m) for r, m in ev]))
@@ -411,6 +430,10 @@ def gpu_main(args, rank, local, world):
                      "mfma_loop_ceiling_tflops": MFMA_LOOP_CEILING_TF if key == "x3" else None,
                      "frac_of_mfma_loop_ceiling": round(achieved / MFMA_LOOP_CEILING_TF, 4) if key == "x3" else None,
                      "ceiling_source": "tools/mfma_shape_bench.hip step32, profiles/r02/mfma_shape/mfma_shape_bench.txt"},
+        "range_guard": {"trips_in_timed_steps": range_timed, "trips_total": range_trips,
+                        "basis": "split-fp16 range flag (|x| >= 65504 in any conv output) checked after the "
+                                 "timed steps; a trip means a batch must be recomputed on the fp32 kernels "
+                                 "(isl_net_range_info counts them per net)"},
         "post": post_fields(H, W, B, post_ms, pairs),
         "e2e": e2e,
         "cpu_baseline": None,

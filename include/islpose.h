@@ -152,6 +152,10 @@ int isl_net_check(isl_net* net, int clear);
  * the flag into *h_flag (pinned host memory; valid once the stream has reached it) and
  * its reset.  *h_flag != 0 then means ISL_E_RANGE for the work enqueued before. */
 int isl_net_check_async(isl_net* net, int32_t* h_flag, void* stream);
+/* Range-guard diagnostics: *trips = how many checks (isl_net_check with clear != 0, and
+ * isl_net_check_async once the stream has reached them) found the flag set, i.e. how
+ * many batches the caller had to recompute on the fp32 kernels.  Waits for the device. */
+int isl_net_range_info(isl_net* net, int64_t* trips);
 
 /* Per-op device timing (measurement; not in the reference).  After
  * isl_net_set_timing(net, 1) every isl_net_run records a HIP event on its stream
@@ -164,6 +168,16 @@ int isl_net_check_async(isl_net* net, int32_t* h_flag, void* stream);
 int isl_net_set_timing(isl_net* net, int on);
 int isl_net_timing(isl_net* net, int max_ops, int* n_ops, int* n_runs, double* op_ms, int* op_kind,
                    double* op_flops, double* op_mfma_flops);
+
+/* Diagnostic: the ops of the net's graph (convs by their caffe layer name, pools as
+ * "maxpool2") and, for the last isl_net_run / isl_net_forward, which conv kernel variant
+ * each ran: for ISL_ALGO_X3 convs the variant code of csrc/internal.h x3_variant_code
+ * (VAR bits: 512 row union, 1024 in-block K ranges, 2048 split-K, 4096 two pairs per
+ * step, 32768 pooled-input staging, 65536 one input buffer, 262144 conv1_1 kernel;
+ * tile pixels / 32 at bits 20-24, output channels / 32 at bits 25-28, ks / 2 at 29-30);
+ * -1 for a pool folded into the next conv's staging; 0 otherwise.  index < the op
+ * count (isl_net_timing's *n_ops). */
+int isl_net_op_info(const isl_net* net, int index, const char** name, int* variant);
 
 /* Diagnostic: copy the net input buffer (filled by isl_net_preprocess) out as
  * float32 NCHW [n,3,net_h,net_w]. */
@@ -220,7 +234,12 @@ int isl_hand_post(isl_net* net, int n, int h, int w, int nscales, const isl_scal
  * array), geom[i*nscales + si] its geometry at scale si (host), its low-res maps crop
  * i of d_heat[si] (NCHW [n,22,net_h/8,net_w/8]; every crop has the same net size per
  * scale) -> int64 peaks [n][21][2].  Stream-ordered on `stream`: the crops run side by
- * side on the net's internal post streams, forked from and joined back into it. */
+ * side on the net's internal post streams, forked from and joined back into it.  The
+ * batch's stage-1 maps live in a buffer of their own whose next writer waits (on the
+ * device) for the lanes of the previous call, whatever stream either runs on.
+ * Host synchronisation: only when a call needs more lane or stage-1 scratch than any
+ * call before it does it wait for that buffer's earlier readers before reallocating
+ * (once per new maximum size); otherwise it never blocks the host. */
 int isl_hand_post_crops(isl_net* net, int n, const int32_t* crop_w, int nscales,
                         const isl_scale_geom* geom, const float* const* d_heat, int64_t* d_peaks,
                         void* stream);

@@ -579,6 +579,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
 // ---------------------------------------------------------------------------
 constexpr int RGB_BCO = 64, RGB_TILE = 256;
 
+// the variant of the last conv_x3 / conv_x3_rgb launch of this thread (x3_last_variant)
+static thread_local int t_last_variant = 0;
+int x3_last_variant() { return t_last_variant; }
+
 template <int RGB_BPX>
 __global__ void __launch_bounds__(RGB_BPX, 1) conv_x3_rgb(X3Args a) {
   constexpr int RGB_NT = RGB_BPX;
@@ -727,6 +731,7 @@ hipError_t launch_conv_x3_rgb(const ConvLaunch& c, hipStream_t s) {
   const long long nb = (long long)c.n * a.px_tiles;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3_rgb: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
+  t_last_variant = x3_variant_code(X3V_RGB, 3, bpx, RGB_BCO);
   hipLaunchKernelGGL(conv_x3_rgb<bpx>, dim3(a.nblocks), dim3(bpx), 0, s, a);
   return hipGetLastError();
 }
@@ -784,6 +789,7 @@ template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, int VAR, int OCC>
 static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   constexpr int BCO = WAVES_M * WM * 32;
   constexpr int BPX = WAVES_N * WN * 32;
+  t_last_variant = x3_variant_code(VAR, KS, BPX, BCO);
   constexpr int P = KS / 2;
   constexpr int SEGCAP = x3_segmax(BPX);
   constexpr bool SPLIT = (VAR & 2048) != 0, RANGED = (VAR & 1024) != 0;
@@ -803,6 +809,8 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
       set_error("conv_x3: pooled-input plane too large for the staging index math");
       return hipErrorInvalidValue;
     }
+    // the pair-max buffer must be exactly 2H x W (even pre-pool height): the chunk stride
+    // below assumes it (runtime pool_into_next_conv checks the producer's height)
     a.in_chs = (long long)2 * c.H * c.W * 8;
   }
   a.vin = c.vin;

@@ -95,6 +95,16 @@ bool x3_fits(const ConvLaunch& c);
 // whether launch_conv_x3 can run c with hpool (even W, not split across blocks)
 bool x3_hpool_ok(const ConvLaunch& c);
 double conv_x3_mfma_flops(const ConvLaunch& c);
+// Which conv_x3 variant a launch ran (isl_net_op_info): the template's VAR bits (512 row
+// union, 1024 in-block K ranges, 2048 split-K across blocks, 4096 two pairs per step,
+// 32768 pooled-input staging, 65536 one input buffer), X3V_RGB for conv_x3_rgb, the tile
+// (pixels / 32 at bits 20-24, output channels / 32 at bits 25-28) and the kernel radius
+// (ks / 2) at bits 29-30.
+constexpr int X3V_RGB = 1 << 18;
+constexpr int x3_variant_code(int var, int ks, int bpx, int bco) {
+  return (var & 0xfffff) | ((bpx / 32) << 20) | ((bco / 32) << 25) | ((ks / 2) << 29);
+}
+int x3_last_variant();
 // floats of split-K workspace launch_conv_x3 would use for c (0 = no split)
 size_t x3_splitk_ws_floats(const ConvLaunch& c);
 // Split-fp16 Winograd F(2x2,3x3) (wino_x3.hip): 3x3 layers with cout % 4 == 0;
@@ -107,6 +117,8 @@ double conv_mfma_flops(const ConvLaunch& c);
 double wino_mfma_flops(const ConvLaunch& c);
 
 hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s);
+// adds 1 to *trips when *flag is set (stream-ordered range-guard count)
+hipError_t launch_range_count(const int* flag, unsigned long long* trips, hipStream_t s);
 // second half of a fused 2x2 max-pool: row pairs of a horizontally pooled buffer
 // (ConvLaunch::hpool, [n][chunk][H][W/2][8]) into the padded next buffer
 hipError_t launch_vpool2(const Act& half, const Act& out, int C, hipStream_t s);
@@ -154,6 +166,13 @@ struct PostLanes {
   hipEvent_t fork, join[ISL_POST_LANES];
   void* scratch[ISL_POST_LANES];
   size_t bytes[ISL_POST_LANES];
+  // the batch's stage-1 maps (written on the caller's stream, read by the lanes): a buffer
+  // of their own, released by `mid_free` (recorded on the caller's stream after the lanes
+  // joined); the next writer waits on it, whatever stream it runs on
+  void* mid;
+  size_t mid_bytes;
+  hipEvent_t mid_free;
+  bool mid_used;
 };
 // created on first use (nullptr + error on failure), destroyed with the net
 PostLanes* net_post_lanes(isl_net* net);

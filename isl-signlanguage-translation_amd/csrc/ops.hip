@@ -32,6 +32,17 @@ __global__ void maxpool2_kernel(const float* __restrict__ in, int ip, int iH, in
   *(f32x4*)(out + ((size_t)f * out_chunks + k) * och + (size_t)((y + op) * oWp + x + op) * 8 + 4 * half) = m;
 }
 
+// Range-guard bookkeeping of isl_net_check_async: a set flag adds one to the net's trip
+// counter (read by isl_net_range_info) before the flag is copied out and reset.
+__global__ void range_count_kernel(const int* __restrict__ flag, unsigned long long* __restrict__ trips) {
+  if (threadIdx.x == 0 && *flag) *trips += 1ull;
+}
+
+hipError_t launch_range_count(const int* flag, unsigned long long* trips, hipStream_t s) {
+  hipLaunchKernelGGL(range_count_kernel, dim3(1), dim3(64), 0, s, flag, trips);
+  return hipGetLastError();
+}
+
 hipError_t launch_maxpool2(const Act& in, const Act& out, int C, hipStream_t s) {
   const int chunks = (C + 7) / 8;
   const long long per_plane = (long long)out.H * out.W * 2;

@@ -2324,10 +2324,22 @@ extern "C" int isl_hand_post_crops(isl_net* net, int n, const int32_t* crop_w, i
       tot += ((size_t)n * 21 * geom[si].valid_h * geom[si].valid_w * 4 + 255) / 256 * 256;
     }
     if (tot) {
-      if (tot > net_scratch_size(net))   // the buffer is reallocated: the lanes may still read it
-        for (int k = 0; k < ISL_POST_LANES; ++k) PHIP(hipStreamSynchronize(L->stream[k]));
-      char* base = (char*)net_scratch(net, tot);
-      if (!base) return ISL_E_HIP;
+      // the maps' own buffer, not the net scratch (which isl_body_post / isl_hand_post on
+      // other streams reuse): a previous call's lanes may still read it, so the writer waits
+      // for their release event; growing it waits on the host, once per new maximum
+      if (tot > L->mid_bytes) {
+        if (L->mid) {
+          if (L->mid_used) PHIP(hipEventSynchronize(L->mid_free));
+          PHIP(hipFree(L->mid));
+        }
+        L->mid = nullptr;
+        L->mid_bytes = 0;
+        L->mid_used = false;
+        PHIP(hipMalloc(&L->mid, tot));
+        L->mid_bytes = tot;
+      }
+      if (L->mid_used) PHIP(hipStreamWaitEvent(s, L->mid_free, 0));
+      char* base = (char*)L->mid;
       for (int si = 0; si < nscales; ++si) {
         if (!off[si]) continue;
         const isl_scale_geom& g = geom[si];
@@ -2359,6 +2371,10 @@ extern "C" int isl_hand_post_crops(isl_net* net, int n, const int32_t* crop_w, i
   for (int k = 0; k < nl; ++k) {
     PHIP(hipEventRecord(L->join[k], L->stream[k]));
     PHIP(hipStreamWaitEvent(s, L->join[k], 0));
+  }
+  if (L->mid) {   // the lanes have joined: the stage-1 maps are free once s gets here
+    PHIP(hipEventRecord(L->mid_free, s));
+    L->mid_used = true;
   }
   return ISL_OK;
 }

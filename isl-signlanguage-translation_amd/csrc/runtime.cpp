@@ -233,10 +233,15 @@ struct isl_net {
   };
   bool timing = false;
   std::vector<TimedRun> timed;
+  std::vector<int> op_variant;   // per op of the last run: x3_variant_code, -1 pool skipped (vin), 0 other
   // conv algorithm (ISL_ALGO_*) and the split-fp16 range flag (isl_net_check)
   int algo = ISL_ALGO_X3;
   int split_k = 1;             // isl_net_set_split_k: K-range mode (env ISLPOSE_X3_SPLITK=0|1|2)
   int* d_flag = nullptr;
+  // range-guard trips: seen by the synchronous check (host count) and by the stream-ordered
+  // one (device count, range_count_kernel); isl_net_range_info sums them
+  long long range_trips_host = 0;
+  unsigned long long* d_trips = nullptr;
   // pre-processing image table (host staging; the device copy is per arena)
   void* d_tab = nullptr;       // the current arena's table (Arena::tab)
   std::vector<char> h_tab;
@@ -630,6 +635,10 @@ static int upload_params(isl_net* net) {
     HIP_OK(hipMalloc(&net->d_flag, sizeof(int)));
     HIP_OK(hipMemset(net->d_flag, 0, sizeof(int)));
   }
+  if (!net->d_trips) {
+    HIP_OK(hipMalloc(&net->d_trips, sizeof(unsigned long long)));
+    HIP_OK(hipMemset(net->d_trips, 0, sizeof(unsigned long long)));
+  }
   net->packed = true;
   return ISL_OK;
 }
@@ -768,6 +777,10 @@ static bool pool_into_next_conv(const isl_net* net, size_t k) {
   if (c.cin_phys / 8 == 1 || net->act[op.out].pad < c.k / 2 || net->act[op.out].cs != (op.C + 7) / 8 * 8)
     return false;
   if (net->out0.buf == op.out || (net->n_out > 1 && net->out1.buf == op.out)) return false;
+  // the staging addresses the pair-max buffer as [chunk][2H][W][8] of the pooled H x W: a
+  // pre-pool plane of odd height (floor-mode pool drops its last row) has another chunk
+  // stride, so it takes vpool2 (e.g. 8 x 372 x 656, level-2 height 93)
+  if (net->act[op.in].H != 2 * net->act[op.out].H || net->act[op.in].W != 2 * net->act[op.out].W) return false;
   for (size_t j = 0; j < net->ops.size(); ++j)
     if (j != k + 1 && (net->ops[j].in == op.out || (j != k && net->ops[j].out == op.out))) return false;
   return true;
@@ -782,6 +795,7 @@ static int run_ops(isl_net* net, hipStream_t s) {
     for (hipEvent_t& e : tr->ev) HIP_OK(hipEventCreate(&e));
     HIP_OK(hipEventRecord(tr->ev[0], s));
   }
+  net->op_variant.assign(net->ops.size(), 0);
   bool fused = false;   // the previous conv wrote the pair-max buffer of this pool
   int vin_buf = -1;     // this conv stages from that buffer (the pool op was skipped)
   const bool fuse_pools = fused_pool_enabled(), pool_input = fuse_pools && pool_input_enabled();
@@ -791,7 +805,7 @@ static int run_ops(isl_net* net, hipStream_t s) {
     const Act& out = net->act[op.out];
     if (op.type == 1) {
       // deferred: the next conv either stages from the pair-max buffer or runs vpool2 first
-      if (fused && pool_input && pool_into_next_conv(net, k)) vin_buf = (int)k;
+      if (fused && pool_input && pool_into_next_conv(net, k)) { vin_buf = (int)k; net->op_variant[k] = -1; }
       else if (fused) HIP_OK(launch_vpool2(net->act[op.hbuf], out, op.C, s));
       else HIP_OK(launch_maxpool2(in, out, op.C, s));
       fused = false;
@@ -829,7 +843,10 @@ static int run_ops(isl_net* net, hipStream_t s) {
         ConvLaunch Lv = L;
         Lv.in = hb.base; Lv.in_cs = hb.cs; Lv.in_coff = 0; Lv.vin = 1;
         if (x3_vin_ok(Lv) && !(c.d_wrgb && x3_rgb_fits(L))) L = Lv;
-        else HIP_OK(launch_vpool2(hb, net->act[pool.out], pool.C, s));   // no variant: the pool after all
+        else {   // no variant: the pool after all
+          HIP_OK(launch_vpool2(hb, net->act[pool.out], pool.C, s));
+          net->op_variant[vin_buf] = 0;
+        }
         vin_buf = -1;
       }
       if (c.x3_wide) {   // 256-channel tiles, two pairs per step, where the grid is big enough
@@ -865,6 +882,7 @@ static int run_ops(isl_net* net, hipStream_t s) {
         HIP_OK(launch_conv_x3(L, s));
         kind = 3; mf = conv_x3_mfma_flops(L);
       }
+      net->op_variant[k] = x3_last_variant();
     } else {
       HIP_OK(launch_conv(L, s));
       mf = conv_mfma_flops(L);
@@ -917,7 +935,11 @@ size_t net_scratch_size(const isl_net* net) { return net->scratch_bytes; }
 PostLanes* net_post_lanes(isl_net* net) {
   if (net->lanes) return net->lanes;
   PostLanes* L = new PostLanes();
+  L->mid = nullptr;
+  L->mid_bytes = 0;
+  L->mid_used = false;
   hipError_t e = hipEventCreateWithFlags(&L->fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&L->mid_free, hipEventDisableTiming);
   for (int k = 0; k < ISL_POST_LANES && e == hipSuccess; ++k) {
     L->scratch[k] = nullptr;
     L->bytes[k] = 0;
@@ -986,6 +1008,7 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_wux3) (void)hipFree(c.d_wux3);
   }
   if (net->d_flag) (void)hipFree(net->d_flag);
+  if (net->d_trips) (void)hipFree(net->d_trips);
   for (auto& kv : net->plans) {
     if (kv.second.tab) (void)hipFree(kv.second.tab);
     if (kv.second.ks) (void)hipFree(kv.second.ks);
@@ -1000,6 +1023,11 @@ int isl_net_destroy(isl_net* net) {
       (void)hipEventDestroy(net->lanes->join[k]);
     }
     (void)hipEventDestroy(net->lanes->fork);
+    if (net->lanes->mid) {
+      (void)hipEventSynchronize(net->lanes->mid_free);
+      (void)hipFree(net->lanes->mid);
+    }
+    (void)hipEventDestroy(net->lanes->mid_free);
     delete net->lanes;
   }
 
@@ -1180,6 +1208,14 @@ int isl_net_timing(isl_net* net, int max_ops, int* n_ops, int* n_runs, double* o
   return ISL_OK;
 }
 
+int isl_net_op_info(const isl_net* net, int index, const char** name, int* variant) {
+  if (!net || index < 0 || index >= (int)net->ops.size()) return fail(ISL_E_ARG, "bad op index");
+  const Op& op = net->ops[index];
+  if (name) *name = op.type == 1 ? "maxpool2" : net->layers[op.layer].name.c_str();
+  if (variant) *variant = index < (int)net->op_variant.size() ? net->op_variant[index] : 0;
+  return ISL_OK;
+}
+
 int isl_net_set_algo(isl_net* net, int algo) {
   if (!net) return fail(ISL_E_ARG, "net is NULL");
   if (algo < ISL_ALGO_X3 || algo > ISL_ALGO_DIRECT) return fail(ISL_E_ARG, "unknown conv algorithm");
@@ -1202,7 +1238,10 @@ int isl_net_check(isl_net* net, int clear) {
   HIP_OK(hipSetDevice(net->device));
   int f = 0;
   HIP_OK(hipMemcpy(&f, net->d_flag, sizeof(int), hipMemcpyDeviceToHost));   // device-synchronising
-  if (f && clear) HIP_OK(hipMemset(net->d_flag, 0, sizeof(int)));
+  if (f && clear) {
+    HIP_OK(hipMemset(net->d_flag, 0, sizeof(int)));
+    ++net->range_trips_host;   // one trip per cleared flag (a check without clear counts nothing)
+  }
   if (f) return fail(ISL_E_RANGE, "an activation left the split-fp16 range (|x| >= 65504); re-run with ISL_ALGO_DIRECT");
   return ISL_OK;
 }
@@ -1212,8 +1251,20 @@ int isl_net_check_async(isl_net* net, int32_t* h_flag, void* stream) {
   if (!net->d_flag) { *h_flag = 0; return ISL_OK; }
   HIP_OK(hipSetDevice(net->device));
   hipStream_t s = (hipStream_t)stream;
+  if (net->d_trips) HIP_OK(launch_range_count(net->d_flag, net->d_trips, s));
   HIP_OK(hipMemcpyAsync(h_flag, net->d_flag, sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_OK(hipMemsetAsync(net->d_flag, 0, sizeof(int), s));
+  return ISL_OK;
+}
+
+int isl_net_range_info(isl_net* net, int64_t* trips) {
+  if (!net || !trips) return fail(ISL_E_ARG, "NULL argument");
+  unsigned long long d = 0;
+  if (net->d_trips) {
+    HIP_OK(hipSetDevice(net->device));
+    HIP_OK(hipMemcpy(&d, net->d_trips, sizeof(d), hipMemcpyDeviceToHost));   // device-synchronising
+  }
+  *trips = (int64_t)(net->range_trips_host + (long long)d);
   return ISL_OK;
 }
 

@@ -73,8 +73,11 @@ class BodyEstimator:
             # pyramid: the scales side by side on their own streams (per-size arenas), as
             # HandEstimator.run_crops
             cur = torch.cuda.current_stream(frames.device)
-            for st, (m, nh, nw, vh, vw) in zip(rt.scale_streams(self, frames.device, len(self.scale_search)),
-                                               scale_geometry(H, W, self.scale_search)):
+            sg = scale_geometry(H, W, self.scale_search)
+            # one stream per net size: two scales that pad to the same size share one arena,
+            # preprocess table and split-K workspace, so they run in order on one stream
+            streams = rt.size_streams(self, frames.device, [(g[1], g[2]) for g in sg])
+            for st, (m, nh, nw, vh, vw) in zip(streams, sg):
                 st.wait_stream(cur)
                 with torch.cuda.stream(st):
                     gh, gw = self.net.preprocess(frames, m)

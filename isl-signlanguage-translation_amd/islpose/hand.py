@@ -37,9 +37,9 @@ class HandEstimator:
         n, h, w, _ = crops.shape
         geoms, heats = [], []
         cur = torch.cuda.current_stream(crops.device)
-        # the scales side by side on their own streams, as run_crops
-        for st, (m, nh, nw, vh, vw) in zip(rt.scale_streams(self, crops.device, len(self.scale_search)),
-                                           scale_geometry(h, w, self.scale_search)):
+        # the scales side by side on their own streams, as run_crops (one per net size)
+        sg = scale_geometry(h, w, self.scale_search)
+        for st, (m, nh, nw, vh, vw) in zip(rt.size_streams(self, crops.device, [(g[1], g[2]) for g in sg]), sg):
             st.wait_stream(cur)
             with torch.cuda.stream(st):
                 gh, gw = self.net.preprocess(crops, m)
@@ -98,7 +98,9 @@ class HandEstimator:
         crops = [(f, x, y, w, w) for (f, x, y, w) in boxes]
         cur = torch.cuda.current_stream(frames_t.device)
         heats = []
-        for st, s in zip(rt.scale_streams(self, frames_t.device, len(self.scale_search)), self.scale_search):
+        # one stream per net size (scales that pad to one size share its arena)
+        keys = [rt.crop_net_size(crops[0][4], crops[0][3], s * BOXSIZE) for s in self.scale_search]
+        for st, s in zip(rt.size_streams(self, frames_t.device, keys), self.scale_search):
             st.wait_stream(cur)
             with torch.cuda.stream(st):
                 gh, gw = self.net.preprocess_crops(frames_t, crops, s * BOXSIZE)

@@ -35,15 +35,22 @@ def free_port() -> int:
     return port
 
 
-def spawn_ranks(argv, world: int, env=None):
+def spawn_ranks(argv, world: int, env=None, poll_s: float = 0.2):
     """Start `world` child processes running `argv` (one per GPU: RANK = LOCAL_RANK =
     r, WORLD_SIZE = world, rendezvous on 127.0.0.1) -- the launcher the reference
     builds from mp.Process (extract_features_mp.py:205-220), with every child on its
     own device instead of cuda:0.  The caller must not have touched the GPU (children
     are separate processes, never an exec of this one).  Returns (exit codes, rank-0
-    stdout); the other ranks' stdout and every stderr pass through."""
+    stdout); the other ranks' stdout and every stderr pass through.
+
+    Fail-fast: every child is polled; the first one to exit non-zero gets its siblings
+    terminated (SIGTERM, then SIGKILL after a grace period), so one rank dying during
+    init or the timed loop never leaves the others blocked at a gloo barrier until
+    torch's default timeout.  Terminated siblings report their signal exit codes."""
     import subprocess
     import sys
+    import threading
+    import time
     port = free_port()
     procs = []
     for r in range(world):
@@ -52,9 +59,33 @@ def spawn_ranks(argv, world: int, env=None):
                  MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable] + list(argv), env=e,
                                       stdout=subprocess.PIPE if r == 0 else None, text=True))
-    out0 = procs[0].communicate()[0]
+    # rank 0's stdout is drained by a thread so polling never blocks on a full pipe
+    chunks = []
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    failed = False
+    while True:
+        codes = [p.poll() for p in procs]
+        if any(c not in (None, 0) for c in codes):
+            failed = True
+            break
+        if all(c is not None for c in codes):
+            break
+        time.sleep(poll_s)
+    if failed:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 10.0
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    reader.join(timeout=10.0)
     codes = [p.wait() for p in procs]
-    return codes, out0
+    return codes, "".join(c for c in chunks if c)
 
 
 def run_sharded(n_frames, get_frames, estimate, batch: int, rank: int, world: int):

@@ -192,7 +192,8 @@ class KeypointExtractor:
     """Runs `model.call_batch(bgr_frames) -> [(candidate, subset, all_hand_peaks)]` over
     videos in batches and writes the reference's per-frame outputs.
 
-    overlap=True (the default when a GPU is visible) pipelines the host work around
+    overlap=True (the default when a GPU is visible and the model takes device frames:
+    it has call_batches or accepts_device_frames) pipelines the host work around
     the GPU: frames are read and uploaded one batch ahead (_Prefetch, pinned buffers +
     a copy stream), the RGB -> BGR flip of extract_features_mp.py:124 runs on the GPU,
     and the JSON / feature-row writing runs on a writer thread.  The outputs are the
@@ -239,7 +240,7 @@ class KeypointExtractor:
             todo = self._todo(filename, frames, label_type, expression)
             for s in range(0, len(todo), self.batch):
                 ids = todo[s:s + self.batch]
-                if ids == list(range(ids[0], ids[-1] + 1)):
+                if ids == list(range(ids[0], ids[-1] + 1)) and hasattr(frames, "shape"):
                     sel = frames[ids[0]:ids[-1] + 1]          # contiguous: a view (mmap / array slice)
                 else:
                     sel = np.stack([np.asarray(frames[i]) for i in ids])
@@ -252,7 +253,11 @@ class KeypointExtractor:
         import torch
         out = [[] for _ in videos]
         vids = [(f, fr, lt, ex, out[k]) for k, (f, fr, lt, ex) in enumerate(videos)]
-        overlap = torch.cuda.is_available() if self.overlap is None else self.overlap
+        # the overlapped path hands the model GPU tensors: by default only models that
+        # declare it (ISLSignPos: call_batches / accepts_device_frames) get it; any other
+        # model keeps numpy BGR batches
+        device_ok = hasattr(self.model, "call_batches") or getattr(self.model, "accepts_device_frames", False)
+        overlap = (torch.cuda.is_available() and device_ok) if self.overlap is None else self.overlap
         if not overlap:
             for (rows, filename, lt, ex, ids), sel in self._batches(vids):
                 # model(frame[:, :, ::-1]): the reference feeds BGR (extract_features_mp.py:124)

@@ -25,7 +25,8 @@ EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destr
            "isl_net_set_timing", "isl_net_timing", "isl_body_layout", "isl_body_post", "isl_hand_post",
            "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops",
            "isl_sign_param_count", "isl_sign_classify", "isl_net_set_split_k", "isl_net_arena_info",
-           "isl_debug_np_sum", "isl_hand_post_crops", "isl_net_check_async"]
+           "isl_debug_np_sum", "isl_hand_post_crops", "isl_net_check_async", "isl_net_range_info",
+           "isl_net_op_info"]
 
 
 class IslCaps(ctypes.Structure):
@@ -82,6 +83,8 @@ def lib():
     L.isl_net_get_algo.argtypes = [vp]
     L.isl_net_check.argtypes = [vp, i32]
     L.isl_net_check_async.argtypes = [vp, vp, vp]
+    L.isl_net_range_info.argtypes = [vp, ctypes.POINTER(i64)]
+    L.isl_net_op_info.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(i32)]
     pi, pd = ctypes.POINTER(i32), ctypes.POINTER(dbl)
     L.isl_net_timing.argtypes = [vp, i32, pi, pi, pd, pi, pd, pd]
     L.isl_body_layout.argtypes = [i32, ctypes.POINTER(IslCaps), ctypes.POINTER(IslLayout)]
@@ -150,8 +153,40 @@ def scale_streams(owner, device, k):
     return ss[:k]
 
 
+def size_streams(owner, device, keys):
+    """One stream per distinct key (a net input size) from owner's scale streams, in the
+    order of `keys`: runs that pad to the same net size share the net's arena, preprocess
+    table and split-K workspace for that size, so they must run in order on one stream;
+    runs of different sizes may overlap."""
+    lane = {}
+    for k in keys:
+        lane.setdefault(k, len(lane))
+    ss = scale_streams(owner, device, len(lane))
+    return [ss[lane[k]] for k in keys]
+
+
+def crop_net_size(crop_h: int, crop_w: int, scale_times_box: float):
+    """Padded net size isl_net_preprocess_crops gives a crop (runtime.cpp: fx = fy =
+    scale_times_box / h, cvRound, then padRightDownCorner to a multiple of 8)."""
+    m = scale_times_box / crop_h
+    rh, rw = int(np.rint(crop_h * m)), int(np.rint(crop_w * m))
+    return (rh + 7) // 8 * 8, (rw + 7) // 8 * 8
+
+
 def ptr(t) -> ctypes.c_void_p:
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def decode_variant(code: int) -> dict:
+    """isl_net_op_info's variant code -> dict(var=VAR bits, bpx, bco, ks, rgb, pool_fused)."""
+    if code == -1:
+        return {"pool_fused": True}
+    if code <= 0:
+        return {}
+    return {"var": code & 0xfffff, "bpx": ((code >> 20) & 31) * 32, "bco": ((code >> 25) & 15) * 32,
+            "ks": 2 * ((code >> 29) & 3) + 1, "rgb": bool(code & (1 << 18)),
+            "union": bool(code & 512), "ranged": bool(code & 1024), "split": bool(code & 2048),
+            "pairs2": bool(code & 4096), "vin": bool(code & 32768), "sib": bool(code & 65536)}
 
 
 class Net:
@@ -268,6 +303,13 @@ class Net:
         assert flag_host.is_pinned() and flag_host.dtype.itemsize == 4
         check(lib().isl_net_check_async(self.h, ptr(flag_host), stream_handle(stream)), "isl_net_check_async")
 
+    def range_trips(self) -> int:
+        """Range-guard trips so far (isl_net_range_info): batches whose split-fp16 range
+        check failed and that the caller recomputed on the fp32 kernels.  Synchronising."""
+        t = ctypes.c_int64()
+        check(lib().isl_net_range_info(self.h, ctypes.byref(t)), "isl_net_range_info")
+        return t.value
+
     def preprocess(self, frames_u8, scale: float, stream=None):
         """frames uint8 [n,H,W,3] cuda -> fills the net input; returns (net_h, net_w)."""
         n, H, W, _ = frames_u8.shape
@@ -301,6 +343,20 @@ class Net:
         b, k = ctypes.c_int64(), ctypes.c_int32()
         check(lib().isl_net_arena_info(self.h, ctypes.byref(b), ctypes.byref(k)), "isl_net_arena_info")
         return b.value, k.value
+
+    def op_variants(self):
+        """[(op name, variant code)] of the last run (isl_net_op_info): the conv kernel
+        variant of every op; decode with decode_variant."""
+        L = lib()
+        n_ops, n_runs = ctypes.c_int32(), ctypes.c_int32()
+        check(L.isl_net_timing(self.h, 0, ctypes.byref(n_ops), ctypes.byref(n_runs), None, None, None, None),
+              "isl_net_timing")
+        out = []
+        for k in range(n_ops.value):
+            name, var = ctypes.c_char_p(), ctypes.c_int32()
+            check(L.isl_net_op_info(self.h, k, ctypes.byref(name), ctypes.byref(var)), "isl_net_op_info")
+            out.append((name.value.decode(), var.value))
+        return out
 
     def set_timing(self, on: bool):
         """Record HIP events around every op of the following runs (isl_net_set_timing)."""

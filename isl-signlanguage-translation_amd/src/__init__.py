@@ -25,18 +25,30 @@ if _pkg_root not in _sys.path:
     _sys.path.insert(0, _pkg_root)
 
 
+# files the reference's src package holds (pytorch-openpose core + the ISL wrapper): a
+# candidate found by search must have all of them, so an unrelated project's ``src``
+# (the cwd, site-packages) never becomes the fall-through
+_MARKERS = ("model.py", "body.py", "hand.py", "util.py", "ISL_Model_parameter.py")
+
+
+def _is_reference_src(c):
+    return all(_os.path.isfile(_os.path.join(c, m)) for m in _MARKERS)
+
+
 def reference_src():
-    """The reference's original ``src`` directory, or None when it cannot be found."""
+    """The reference's original ``src`` directory, or None when it cannot be found.
+    ``$ISLPOSE_REFERENCE_SRC`` is taken as given; ``src.orig`` next to this package and
+    ``src`` directories on sys.path must carry the reference's marker files."""
     real = _os.path.realpath(_here)
     cands = []
     if _os.environ.get("ISLPOSE_REFERENCE_SRC"):
-        cands.append(_os.environ["ISLPOSE_REFERENCE_SRC"])
-    cands.append(_os.path.join(_os.path.dirname(_here), "src.orig"))
+        cands.append((_os.environ["ISLPOSE_REFERENCE_SRC"], False))
+    cands.append((_os.path.join(_os.path.dirname(_here), "src.orig"), True))
     for p in _sys.path:
-        cands.append(_os.path.join(p or _os.getcwd(), "src"))
-    for c in cands:
+        cands.append((_os.path.join(p or _os.getcwd(), "src"), True))
+    for c, need_markers in cands:
         if c and _os.path.isdir(c) and _os.path.realpath(c) != real and \
-                _os.path.isfile(_os.path.join(c, "__init__.py")):
+                _os.path.isfile(_os.path.join(c, "__init__.py")) and (not need_markers or _is_reference_src(c)):
             return c
     return None
 

@@ -46,3 +46,32 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run"], env=e,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_bench_launch_fails_fast_when_a_rank_dies():
+    """One rank exits 1 right after the group is up; its sibling would block at the next
+    gloo barrier.  The launcher must notice the failure, terminate the sibling and exit
+    non-zero long before the collective timeout (--pg-timeout 120 s here)."""
+    import time
+    t0 = time.time()
+    r = _run("--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1", "--batch", "4", "--fail-rank", "1")
+    dt = time.time() - t0
+    assert r.returncode == 1, (r.returncode, r.stderr[-2000:])
+    assert "failing on request" in r.stderr
+    assert dt < 60, dt
+
+
+def test_spawn_ranks_kills_siblings_on_first_failure():
+    """parallel.spawn_ranks: child 0 sleeps far longer than the test, child 1 exits 3;
+    the launcher returns promptly with child 1's code and child 0 terminated."""
+    import time
+    from islpose import parallel
+    prog = ("import os, sys, time\n"
+            "r = int(os.environ['RANK'])\n"
+            "print('rank', r, flush=True)\n"
+            "time.sleep(300) if r == 0 else sys.exit(3)\n")
+    t0 = time.time()
+    codes, out0 = parallel.spawn_ranks(["-c", prog], 2, env=_env())
+    assert time.time() - t0 < 30
+    assert codes[1] == 3 and codes[0] != 0
+    assert "rank 0" in out0

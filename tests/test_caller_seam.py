@@ -81,6 +81,9 @@ def test_other_modules_fall_through_to_reference_src(tmp_path):
         path.write_text("".join("%s = %r\n" % (n, n) for n in sorted(names)) or "ORIGINAL = True\n")
     # the reference's util.py carries the drawing helpers the drop-in delegates to
     (orig / "util.py").write_text("def drawStickmodel(img, *a):\n    return ('drawn', img)\n")
+    for m in ("model.py", "body.py", "hand.py", "ISL_Model_parameter.py"):   # the reference's marker files
+        if not (orig / m).exists():
+            (orig / m).write_text("ORIGINAL = True\n")
     os.symlink(os.path.join(PKG, "src"), ref / "src")
     lines = ["import sys", "sys.path.insert(0, %r)" % str(ref)]
     for script, e in _imports():
@@ -145,3 +148,20 @@ def test_translator_cache_dropped_when_weights_change():
         body.weight.copy_(body.weight + 1)
     t.call(frames[1:21])
     assert counted == [20, 1, 20]
+
+
+def test_fall_through_ignores_unrelated_src(tmp_path, monkeypatch):
+    """A ``src`` package on sys.path without the reference's files (model.py, body.py,
+    hand.py, util.py, ISL_Model_parameter.py) never becomes the fall-through."""
+    import sys
+    import src
+    other = tmp_path / "src"
+    other.mkdir()
+    (other / "__init__.py").write_text("")
+    (other / "util.py").write_text("raise SystemExit('must not be imported')\n")
+    monkeypatch.delenv("ISLPOSE_REFERENCE_SRC", raising=False)
+    monkeypatch.setattr(sys, "path", [str(tmp_path)] + list(sys.path))
+    assert src.reference_src() != str(other)
+    for m in src._MARKERS:
+        (other / m).write_text("")
+    assert src.reference_src() == str(other)

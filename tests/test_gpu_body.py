@@ -64,14 +64,16 @@ def test_body25_forward_algo_vs_oracle(net25, w25, algo):
 
 
 @pytest.mark.parametrize("n,h,w", [(2, 184, 328), (1, 368, 656), (2, 50, 70), (3, 96, 136), (8, 368, 656),
-                                   (16, 184, 328)])
+                                   (16, 184, 328), (8, 372, 656), (4, 100, 104)])
 def test_fused_pool_bit_identical(net25, n, h, w, monkeypatch):
     """conv1_2 / conv2_2 / conv3_4 writing horizontal pair maxima (ConvLaunch::hpool) +
     the row-pair max inside the next conv's staging (ConvLaunch::vin, on chip-filling
     grids: 8 x 368x656 takes it after all three pools, 16 x 184x328 after two and
     vpool2_kernel for the third) or in vpool2_kernel (ISLPOSE_POOL_INPUT=0) == conv +
     maxpool2, bit for bit (max is exact); odd widths (50x70's 25x35 level) take the plain
-    path."""
+    path.  8 x 372x656 and 4 x 100x104 have an odd pre-pool height (93 / 25 rows before
+    pool3) with an even width: that pool must not hand its pair-max buffer to the next
+    conv's staging, whose chunk stride assumes 2H rows."""
     x = torch.from_numpy(_inputs(n, h, w, seed=h + w)).cuda()
     paf0, heat0 = net25.forward(x)
     monkeypatch.setenv("ISLPOSE_POOL_INPUT", "0")
@@ -362,3 +364,50 @@ def test_x3_matches_direct_small_shapes(net25):
         p1, h1 = net25.forward(x)
         assert _rel(p1.cpu().numpy(), p0.cpu().numpy()) < TOL
         assert _rel(h1.cpu().numpy(), h0.cpu().numpy()) < TOL
+
+
+def test_timed_config_forward_vs_oracle(net25, w25):
+    """The bench's own configuration (configs[1]: body_25, 32 frames of 368x656, net input
+    368x656; reference src/model.py:171-207) checked against the oracle on frames 0, 17 and
+    31, with the kernel variants the bench times asserted through isl_net_op_info: the
+    46x82 stage 3x3 layers on the 512-pixel row union, conv2_1 / conv3_1 / conv4_1 staging
+    their pooled input (the pools folded away), Mconv6 on 256-channel tiles with two chunk
+    pairs per step, conv1_1 on its 27-term kernel."""
+    n, h, w = 32, 368, 656
+    x = _inputs(n, h, w, seed=2024)
+    paf, heat = net25.forward(torch.from_numpy(x).cuda())
+    torch.cuda.synchronize()
+    var = {name: rt.decode_variant(v) for name, v in net25.op_variants()}
+    stage3 = [k for k in var if k.startswith("Mconv") and k[5] in "12345"]
+    assert len(stage3) == 90
+    for k in stage3:
+        assert var[k].get("union") and var[k]["bpx"] == 512, (k, var[k])
+    for k in ("conv2_1", "conv3_1", "conv4_1"):
+        assert var[k].get("vin"), (k, var[k])
+    assert var["conv4_1"].get("union"), var["conv4_1"]
+    m6 = [k for k in var if k.startswith("Mconv6")]
+    assert len(m6) == 6 and all(var[k].get("pairs2") and var[k]["bco"] == 256 for k in m6), m6
+    assert var["conv1_1"].get("rgb")
+    assert sum(1 for _, v in net25.op_variants() if v == -1) == 3      # all three pools folded
+    fn = cpu_ref.make_net_fn("body25", w25)
+    for f in (0, 17, 31):
+        rp, rh = fn(x[f:f + 1])
+        ep = _rel(paf[f:f + 1].cpu().numpy(), rp)
+        eh = _rel(heat[f:f + 1].cpu().numpy(), rh)
+        assert ep < TOL and eh < TOL, (f, ep, eh)
+
+
+def test_colliding_pyramid_scales_serialised(w25):
+    """Two pyramid scales that pad to the same net size (0.505 and 0.51 -> 192 x 336) share
+    the net's arena for that size; run_scales must run them in order on one stream (ADVICE
+    r02).  Each scale's maps must equal the same scale run alone."""
+    frames = torch.from_numpy(synth.synth_frames(2, 368, 656, seed=77)).cuda()
+    est = BodyEstimator(w25, "body25", scale_search=(0.505, 0.51, 1.0))
+    geoms, pafs, heats = est.run_scales(frames)
+    torch.cuda.synchronize()
+    assert geoms[0][:2] == geoms[1][:2]
+    for i, s in enumerate((0.505, 0.51, 1.0)):
+        one = BodyEstimator(w25, "body25", scale_search=(s,))
+        _, p1, h1 = one.run_scales(frames, keep_maps=True)
+        torch.cuda.synchronize()
+        assert torch.equal(pafs[i], p1[0]) and torch.equal(heats[i], h1[0]), s

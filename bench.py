@@ -82,6 +82,8 @@ def parse(argv=None):
     p.add_argument("--fail-rank", type=int, default=-1,
                    help="test only (with --dry-run): this rank exits 1 after the group is up, so the "
                         "launcher's fail-fast path is exercised (tests/test_bench_launch.py)")
+    p.add_argument("--no-mode-r", dest="mode_r", action="store_false",
+                   help="skip the Mode R sub-measurement (net 184x328 at batch 32 and batch 1)")
     p.add_argument("--pg-timeout", type=float, default=120.0,
                    help="seconds a gloo collective (init, barrier, gather) may block before the rank fails")
     return p.parse_args(argv)
@@ -195,178 +197,182 @@ def gpu_main(args, rank, local, world):
     local = local % ndev if ndev > 0 else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    B, H, W = args.batch, args.height, args.width
-    S = args.streams
-    assert B % S == 0, "batch must split evenly over the streams"
+    H, W = args.height, args.width
     weights = synth.synth_weights(0)
-    lo, hi = frame_shard(rank, B)
-    # frames of this rank: indices [lo, hi), disjoint shards
-    frames_h = synth.synth_frames(B, H, W, seed=1000 + rank)
-    frames = torch.from_numpy(frames_h).to(dev)
-    (mult, nh, nw, vh, vw), = scale_geometry(H, W, (args.scale,))
-    geoms = [(nh, nw, vh, vw)]
-    maps = [synth.designed_pose_maps(nh // 8, nw // 8, args.persons, seed=i) for i in range(lo, hi)]
-    d_paf = torch.from_numpy(np.stack([m[0] for m in maps])).to(dev)
-    d_heat = torch.from_numpy(np.stack([m[1] for m in maps])).to(dev)
     L = rt.lib()
     main_stream = torch.cuda.current_stream(dev)
 
-    class Lane:
-        """One sub-batch on its own stream with its own net arena; lanes overlap on the GPU."""
+    def measure(scale, B, steps, warmup, S, op_timing):
+        """One configuration: B frames per rank per step at `scale`, S lanes (streams); warmup
+        steps, then `steps` timed steps between barriers; per-op HIP events on the last."""
+        assert B % S == 0, "batch must split evenly over the streams"
+        lo, hi = frame_shard(rank, B)
+        # frames of this rank: indices [lo, hi), disjoint shards
+        frames_h = synth.synth_frames(B, H, W, seed=1000 + rank)
+        frames = torch.from_numpy(frames_h).to(dev)
+        (mult, nh, nw, vh, vw), = scale_geometry(H, W, (scale,))
+        geoms = [(nh, nw, vh, vw)]
+        maps = [synth.designed_pose_maps(nh // 8, nw // 8, args.persons, seed=i) for i in range(lo, hi)]
+        d_paf = torch.from_numpy(np.stack([m[0] for m in maps])).to(dev)
+        d_heat = torch.from_numpy(np.stack([m[1] for m in maps])).to(dev)
 
-        def __init__(self, s):
-            self.est = BodyEstimator(weights, "body25", device=local, scale_search=(args.scale,))
-            self.net = self.est.net
-            self.net.set_algo(args.algo)
-            if args.split_k:
-                self.net.set_split_k(2)
-            self.b = B // S
-            sl = slice(s * self.b, (s + 1) * self.b)
-            self.frames, self.paf, self.heat = frames[sl], d_paf[sl], d_heat[sl]
-            self.caps = rt.IslCaps(**self.est.caps)
-            self.lay = rt.body_layout(self.est.kind, self.caps)
-            self.d_res = torch.empty(self.b * self.lay.record_bytes, dtype=torch.uint8, device=dev)
-            self.h_res = torch.empty(self.b * self.lay.record_bytes, dtype=torch.uint8, pin_memory=True)
-            self.g = (rt.IslScaleGeom * 1)(rt.IslScaleGeom(*geoms[0]))
-            self.pp = (ctypes.c_void_p * 1)(self.paf.data_ptr())
-            self.hp = (ctypes.c_void_p * 1)(self.heat.data_ptr())
-            self.stream = main_stream if S == 1 else torch.cuda.Stream(dev)
-            self.sh = rt.stream_handle(self.stream)
-            # D2H of the records on a copy stream: it overlaps the next step's preprocess and
-            # net; the next post (which rewrites d_res) waits for it, and the timed region's
-            # closing device synchronize includes it
-            self.cs = torch.cuda.Stream(dev)
-            self.copied = None
+        class Lane:
+            """One sub-batch on its own stream with its own net arena; lanes overlap on the GPU."""
 
-    lanes = [Lane(s) for s in range(S)]
-    ev = []
+            def __init__(self, s):
+                self.est = BodyEstimator(weights, "body25", device=local, scale_search=(scale,))
+                self.net = self.est.net
+                self.net.set_algo(args.algo)
+                if args.split_k:
+                    self.net.set_split_k(2)
+                self.b = B // S
+                sl = slice(s * self.b, (s + 1) * self.b)
+                self.frames, self.paf, self.heat = frames[sl], d_paf[sl], d_heat[sl]
+                self.caps = rt.IslCaps(**self.est.caps)
+                self.lay = rt.body_layout(self.est.kind, self.caps)
+                self.d_res = torch.empty(self.b * self.lay.record_bytes, dtype=torch.uint8, device=dev)
+                self.h_res = torch.empty(self.b * self.lay.record_bytes, dtype=torch.uint8, pin_memory=True)
+                self.g = (rt.IslScaleGeom * 1)(rt.IslScaleGeom(*geoms[0]))
+                self.pp = (ctypes.c_void_p * 1)(self.paf.data_ptr())
+                self.hp = (ctypes.c_void_p * 1)(self.heat.data_ptr())
+                self.stream = main_stream if S == 1 else torch.cuda.Stream(dev)
+                self.sh = rt.stream_handle(self.stream)
+                # D2H of the records on a copy stream: it overlaps the next step's preprocess and
+                # net; the next post (which rewrites d_res) waits for it, and the timed region's
+                # closing device synchronize includes it
+                self.cs = torch.cuda.Stream(dev)
+                self.copied = None
 
-    def step(timed):
-        # timed: stage events (net / post windows) on this step; timing events are kept
-        # off the other steps, like the per-op events (each costs a dispatch gap)
-        def mark(stream):
-            e = torch.cuda.Event(enable_timing=timed)
-            e.record(stream)
-            return e
-        ref = mark(main_stream)
-        marks = []
-        for ln in lanes:
-            if ln.stream is not main_stream:
-                ln.stream.wait_event(ref)
-            ln.net.preprocess(ln.frames, mult, stream=ln.stream)
-            e0 = mark(ln.stream) if timed else None
-            ln.net.run(stream=ln.stream)
-            e1 = mark(ln.stream) if timed else None
-            if ln.copied is not None:
-                ln.stream.wait_event(ln.copied)
-            rt.check(L.isl_body_post(ln.net.h, ln.b, H, W, 1, ln.g, ln.pp, ln.hp, ctypes.byref(ln.caps),
-                                     rt.ptr(ln.d_res), ln.sh), "post")
-            e2 = mark(ln.stream)
-            marks.append((e0, e1, e2))
-            ln.cs.wait_event(e2)
-            with torch.cuda.stream(ln.cs):
-                ln.h_res.copy_(ln.d_res, non_blocking=True)
-            ln.copied = torch.cuda.Event()
-            ln.copied.record(ln.cs)
-        for ln in lanes:
-            if ln.stream is not main_stream:
-                main_stream.wait_stream(ln.stream)
-        if timed:
-            ev.append((ref, marks))
+        lanes = [Lane(s) for s in range(S)]
+        ev = []
 
-    def net_window_ms(ref, marks):
-        # conv stage wall time of one step: first net start -> last net end over all lanes
-        return max(ref.elapsed_time(m[1]) for m in marks) - min(ref.elapsed_time(m[0]) for m in marks)
-
-    def post_window_ms(ref, marks):
-        # post kernels of one step (isl_body_post: resize/blur/NMS, peaks, PAF scoring, assembly)
-        return max(ref.elapsed_time(m[2]) for m in marks) - min(ref.elapsed_time(m[1]) for m in marks)
-
-    for _ in range(args.warmup):
-        step(False)
-    torch.cuda.synchronize(dev)
-    # validate one step's records (no overflow / errors) outside the timed region, and
-    # count the (A, B) candidate pairs the PAF kernel scores (sum over limbs of nA * nB)
-    pairs = 0
-    for ln in lanes:
-        host = ln.h_res.numpy()
-        for f in range(ln.b):
-            o = f * ln.lay.record_bytes + ln.lay.status
-            st = int(host[o:o + 4].view(np.int32)[0])
-            assert st == 0, "post status %d on frame %d" % (st, f)
-            o = f * ln.lay.record_bytes + ln.lay.n_peaks
-            npk = host[o:o + 128].view(np.int32)
-            pairs += sum(int(npk[a]) * int(npk[b]) for a, b in synth.BODY25_LIMBS)
-        assert ln.net.range_ok(), "split-fp16 range exceeded in warmup"
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        # per-op HIP events (each lane's stream) on the last timed step only: an event
-        # between every launch costs ~8 us of dispatch gap (1.8 % of the step when every
-        # step carried them, tools/gpu_optiming.sh); one instrumented step of K still gives
-        # the per-launch averages of every kernel, inside the timed region
-        last = i == args.steps - 1
-        if last and not args.no_op_timing:
+        def step(timed):
+            # timed: stage events (net / post windows) on this step; timing events are kept
+            # off the other steps, like the per-op events (each costs a dispatch gap)
+            def mark(stream):
+                e = torch.cuda.Event(enable_timing=timed)
+                e.record(stream)
+                return e
+            ref = mark(main_stream)
+            marks = []
             for ln in lanes:
-                ln.net.set_timing(True)
-        step(last)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    for ln in lanes:
-        ln.net.set_timing(False)
-    # range guard over the timed steps (outside the timed region): a set flag would mean a
-    # batch needed the fp32 recompute the timed loop did not do
-    range_timed = sum(0 if ln.net.range_ok() else 1 for ln in lanes)
-    range_trips = sum(ln.net.range_trips() for ln in lanes)
-    ops = [ln.net.timing() for ln in lanes]
-    net_ms = float(np.mean([net_window_ms(r, m) for r, m in ev]))
-    post_ms = float(np.mean([post_window_ms(r, m) for r, m in ev]))
-    e2e = e2e_rate(args, lanes[0].est, frames_h, maps, dev) if args.e2e_steps > 0 else None
-    g = gather_floats([elapsed, net_ms, post_ms, B * args.steps / elapsed, lo, hi,
-                       e2e["frames_per_s"] if e2e else 0.0, local], world)
-    elapsed, net_ms, post_ms = float(g[:, 0].max()), float(g[:, 1].max()), float(g[:, 2].max())
+                if ln.stream is not main_stream:
+                    ln.stream.wait_event(ref)
+                ln.net.preprocess(ln.frames, mult, stream=ln.stream)
+                e0 = mark(ln.stream) if timed else None
+                ln.net.run(stream=ln.stream)
+                e1 = mark(ln.stream) if timed else None
+                if ln.copied is not None:
+                    ln.stream.wait_event(ln.copied)
+                rt.check(L.isl_body_post(ln.net.h, ln.b, H, W, 1, ln.g, ln.pp, ln.hp, ctypes.byref(ln.caps),
+                                         rt.ptr(ln.d_res), ln.sh), "post")
+                e2 = mark(ln.stream)
+                marks.append((e0, e1, e2))
+                ln.cs.wait_event(e2)
+                with torch.cuda.stream(ln.cs):
+                    ln.h_res.copy_(ln.d_res, non_blocking=True)
+                ln.copied = torch.cuda.Event()
+                ln.copied.record(ln.cs)
+            for ln in lanes:
+                if ln.stream is not main_stream:
+                    main_stream.wait_stream(ln.stream)
+            if timed:
+                ev.append((ref, marks))
+
+        def net_window_ms(ref, marks):
+            # conv stage wall time of one step: first net start -> last net end over all lanes
+            return max(ref.elapsed_time(m[1]) for m in marks) - min(ref.elapsed_time(m[0]) for m in marks)
+
+        def post_window_ms(ref, marks):
+            # post kernels of one step (isl_body_post: resize/blur/NMS, peaks, PAF scoring, assembly)
+            return max(ref.elapsed_time(m[2]) for m in marks) - min(ref.elapsed_time(m[1]) for m in marks)
+
+        for _ in range(warmup):
+            step(False)
+        torch.cuda.synchronize(dev)
+        # validate one step's records (no overflow / errors) outside the timed region, and
+        # count the (A, B) candidate pairs the PAF kernel scores (sum over limbs of nA * nB)
+        pairs = 0
+        for ln in lanes:
+            host = ln.h_res.numpy()
+            for f in range(ln.b):
+                o = f * ln.lay.record_bytes + ln.lay.status
+                st = int(host[o:o + 4].view(np.int32)[0])
+                assert st == 0, "post status %d on frame %d" % (st, f)
+                o = f * ln.lay.record_bytes + ln.lay.n_peaks
+                npk = host[o:o + 128].view(np.int32)
+                pairs += sum(int(npk[a]) * int(npk[b]) for a, b in synth.BODY25_LIMBS)
+            assert ln.net.range_ok(), "split-fp16 range exceeded in warmup"
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            # per-op HIP events (each lane's stream) on the last timed step only: an event
+            # between every launch costs ~8 us of dispatch gap (1.8 % of the step when every
+            # step carried them, tools/gpu_optiming.sh); one instrumented step of K still gives
+            # the per-launch averages of every kernel, inside the timed region
+            last = i == steps - 1
+            if last and op_timing:
+                for ln in lanes:
+                    ln.net.set_timing(True)
+            step(last)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        elapsed = time.perf_counter() - t0
+        for ln in lanes:
+            ln.net.set_timing(False)
+        # range guard over the timed steps (outside the timed region): a set flag would mean a
+        # batch needed the fp32 recompute the timed loop did not do
+        range_timed = sum(0 if ln.net.range_ok() else 1 for ln in lanes)
+        range_trips = sum(ln.net.range_trips() for ln in lanes)
+        ops = [ln.net.timing() for ln in lanes] if op_timing else None
+        net_ms = float(np.mean([net_window_ms(r, m) for r, m in ev]))
+        post_ms = float(np.mean([post_window_ms(r, m) for r, m in ev]))
+        g = gather_floats([elapsed, net_ms, post_ms, B * steps / elapsed, lo, hi, local], world)
+        return {"elapsed": float(g[:, 0].max()), "net_ms": float(g[:, 1].max()), "post_ms": float(g[:, 2].max()),
+                "g": g, "ops": ops, "pairs": pairs, "range_timed": range_timed, "range_trips": range_trips,
+                "lanes": lanes, "frames_h": frames_h, "maps": maps, "mult": mult, "nh": nh, "nw": nw,
+                "B": B, "steps": steps, "fps": B * world * steps / float(g[:, 0].max())}
+
+    B, S = args.batch, args.streams
+    m = measure(args.scale, B, args.steps, args.warmup, S, not args.no_op_timing)
+    e2e = e2e_rate(args, m["lanes"][0].est, m["frames_h"], m["maps"], dev) if args.e2e_steps > 0 else None
+    # Mode R (SURVEY 8: the reference scripts' net size, scale_search=[0.5], body.py:41): the
+    # same step at batch 32 and at batch 1 (the scripts' one-frame-per-call pattern), in the
+    # same invocation, with their own roofline -- a sub-object, not the headline value
+    mode_r = None
+    if args.mode_r and args.scale == 1.0 and not args.no_op_timing:
+        mode_r = {}
+        for key, bb, st, wu in (("batch32", 32, args.steps, max(1, args.warmup)),
+                                ("batch1", 1, max(30, args.steps), max(3, args.warmup))):
+            mr = measure(0.5, bb, st, wu, 1, True)
+            rf = roofline_of(mr["ops"])
+            mode_r[key] = {"frames_per_s": round(mr["fps"], 2), "batch_per_gpu": bb, "steps": st, "warmup": wu,
+                           "ms_per_step": round(mr["elapsed"] / st * 1e3, 3), "net_hw": [mr["nh"], mr["nw"]],
+                           "net_ms_per_step": round(mr["net_ms"], 3), "post_ms_per_step": round(mr["post_ms"], 3),
+                           "roofline": {k: rf[k] for k in ("bound", "kernel", "achieved", "peak", "unit", "frac",
+                                                           "launches", "avg_launch_us", "all_convs_tflops",
+                                                           "ms_per_step_by_kind")},
+                           "range_guard_trips_in_timed_steps": mr["range_timed"]}
+            del mr
+        mode_r["basis"] = ("scale_search=[0.5] (net 184x328), same step as the headline (preprocess + body_25 + "
+                           "post on designed maps + D2H), timed in this invocation after it; frac as the headline's")
     if rank != 0:
         return
-    total_frames = B * world * args.steps
-    fps = total_frames / elapsed
+    g = m["g"]
+    elapsed, net_ms, post_ms, ops = m["elapsed"], m["net_ms"], m["post_ms"], m["ops"]
+    nh, nw, mult = m["nh"], m["nw"], m["mult"]
+    fps = m["fps"]
     if args.no_op_timing:
         print(json.dumps({"metric": METRIC, "value": round(fps, 2), "unit": "frames/s", "n_gpus": world,
                           "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": round(elapsed / args.steps * 1e3, 3), "op_timing": False}))
         return
-    # per-kind sums over all lanes and timed steps (HIP events around every launch)
-    kinds = {}
-    for o in ops:
-        for k in set(o["kind"].tolist()):
-            m = o["kind"] == k
-            d = kinds.setdefault(int(k), {"ms": 0.0, "flops": 0.0, "mfma_flops": 0.0, "launches": 0})
-            d["ms"] += float(o["ms"][m].sum())
-            d["flops"] += float(o["flops"][m].sum())
-            d["mfma_flops"] += float(o["mfma_flops"][m].sum())
-            d["launches"] += int(m.sum()) * o["n_runs"]
-    dom = max(kinds, key=lambda k: kinds[k]["ms"])
-    dk = kinds[dom]
-    peak = KIND_PEAK.get(dom, PEAK_FP32_MFMA_TFLOPS)
-    sec = dk["ms"] * 1e-3
-    fp32_equiv = dk["flops"] / sec / 1e12                      # direct-conv FLOPs (SURVEY 8d) per second
-    achieved = ALG_FACTOR.get(dom, 1.0) * dk["flops"] / sec / 1e12   # MFMA work the algorithm needs, no padding
-    executed = dk["mfma_flops"] / sec / 1e12                   # what the matrix cores ran (tile padding included)
-    conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3, 4))
-    conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3, 4))
-    traffic = mfma_busy = clk = busy_s = clk_s = stage_busy = stage_busy_s = None
-    prof = os.path.join(REPO, "profiles", "conv_traffic.json")
-    if os.path.exists(prof):
-        pj = json.load(open(prof))
-        key = {1: "direct", 2: "wino", 3: "x3", 4: "wino_x3"}.get(dom, "x3")
-        traffic = pj.get(key + "_hbm_bytes_per_launch")
-        mfma_busy, clk = pj.get(key + "_mfma_busy_frac"), pj.get(key + "_effective_clock_ghz")
-        busy_s, clk_s = pj.get(key + "_mfma_busy_frac_at_stamp_clock"), pj.get(key + "_stamp_clock_ghz")
-        stage_busy = pj.get("conv_stage_mfma_busy_frac")
-        stage_busy_s = pj.get("conv_stage_mfma_busy_frac_at_stamp_clock")
+    rf = roofline_of(ops)
+    rf["op_timing"] = "per-op HIP events on the last of the %d timed steps (lane streams)" % args.steps
+    rf["net_ms_per_step"] = round(net_ms, 3)
     out = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -379,62 +385,28 @@ def gpu_main(args, rank, local, world):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": {3: "fp32 (split-fp16 x3 MFMA, fp32 accumulate)",
-                  4: "fp32 (split-fp16 x3 MFMA, fp32 accumulate)"}.get(dom, "fp32"),
+                  4: "fp32 (split-fp16 x3 MFMA, fp32 accumulate)"}.get(rf.pop("_dom"), "fp32"),
         "data": "synthetic (seeded uint8 frames, counter-hash weights; post fed designed %d-person maps)"
                 % args.persons,
         "config": {"workload": "configs[1]: body_25 single-scale %dx%d frames, batch %d per GPU, net input %dx%d"
                                % (H, W, B, nh, nw),
                    "batch_per_gpu": B, "frame_hw": [H, W], "scale_search": [args.scale], "net_hw": [nh, nw],
                    "streams_per_gpu": S, "conv_algo": args.algo, "split_k": bool(args.split_k),
+                   "x3_m16": os.environ.get("ISLPOSE_X3_M16", "default"),
                    "parallelism": "frame-sharded x%d (no collective)" % world},
         "ranks": {"world_observed": torch.distributed.get_world_size() if world > 1 else 1,
                   "per_rank_frames_per_s": [round(float(v), 2) for v in g[:, 3]],
                   "frame_shards": [[int(a), int(b)] for a, b in g[:, 4:6]],
-                  "rank_devices": [int(d) for d in g[:, 7]],
-                  "devices_shared": bool(len(set(int(d) for d in g[:, 7])) < world),
+                  "rank_devices": [int(d) for d in g[:, 6]],
+                  "devices_shared": bool(len(set(int(d) for d in g[:, 6])) < world),
                   "timing_collectives": "gloo (host): barrier + all_gather of per-rank times; no data-path collective"},
-        "roofline": {"bound": "mfma", "kernel": KIND[dom],
-                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "achieved_basis": "MFMA FLOPs the kernel's algorithm needs (direct-conv count 2*Cout*Cin*k*k*H*W "
-                                       "x %.4g: split-fp16 = 3 fp16 products per fp32 MAC, Winograd = 16/36, tile "
-                                       "padding excluded) / summed launch time; peak = dense MFMA peak of the dtype the "
-                                       "matrix cores run (fp16 2516.6 / fp32 157.3 TF)" % ALG_FACTOR.get(dom, 1.0),
-                     "fp32_equiv_tflops": round(fp32_equiv, 2),
-                     "fp32_equiv_vs_fp32_peak": round(fp32_equiv / PEAK_FP32_MFMA_TFLOPS, 4),
-                     "executed_tflops": round(executed, 2),
-                     "executed_frac": round(executed / peak, 4),
-                     "launches": dk["launches"], "avg_launch_us": round(dk["ms"] * 1e3 / dk["launches"], 2),
-                     "algorithmic_gflop_per_launch": round(dk["flops"] / dk["launches"] / 1e9, 3),
-                     "all_convs_tflops": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2),
-                     "ms_per_step_by_kind": {KIND[k]: round(v["ms"] / max(1, ops[0]["n_runs"]), 3) for k, v in kinds.items()},
-                     "op_timing": "per-op HIP events on the last of the %d timed steps (lane streams)" % args.steps,
-                     "net_ms_per_step": round(net_ms, 3),
-                     # PMC (profiles/conv_traffic.json, from tools/profile_round.sh): MFMA pipe busy
-                     # fraction of the dominant kernel's wall cycles, and the DVFS clock it ran at; the
-                     # conv stage adds conv1_1's write-bound conv_x3_rgb
-                     "mfma_busy_pmc": mfma_busy,
-                     "conv_stage_mfma_busy_pmc": stage_busy,
-                     "conv_stage_mfma_busy_pmc_at_stamp_clock": stage_busy_s,
-                     "effective_clock_ghz": clk,
-                     "frac_at_effective_clock": round(achieved / (peak * clk / 2.4), 4) if clk else None,
-                     # the GRBM-based clock reads high on sub-10 ms dispatches (MI355X_MICROARCH.md DVFS item 6);
-                     # the in-kernel clock of a stamp build (s_memtime / s_memrealtime) of the dominant shape:
-                     "mfma_busy_pmc_at_stamp_clock": busy_s,
-                     "stamp_clock_ghz": clk_s,
-                     "frac_at_stamp_clock": round(achieved / (peak * clk_s / 2.4), 4) if clk_s else None,
-                     "pmc_source": "profiles/conv_traffic.json (tools/profile_round.sh + tools/pmc_summary.py)",
-                     # the bare x3 inner loop (LDS fragment reads + 3 MFMAs per product, no staging,
-                     # no barriers) on every CU: what the chip sustains with this MFMA shape under its
-                     # power limit (the clock settles at ~1.55 GHz)
-                     "mfma_loop_ceiling_tflops": MFMA_LOOP_CEILING_TF if key == "x3" else None,
-                     "frac_of_mfma_loop_ceiling": round(achieved / MFMA_LOOP_CEILING_TF, 4) if key == "x3" else None,
-                     "ceiling_source": "tools/mfma_shape_bench.hip step32, profiles/r02/mfma_shape/mfma_shape_bench.txt"},
-        "range_guard": {"trips_in_timed_steps": range_timed, "trips_total": range_trips,
+        "roofline": rf,
+        "mode_r": mode_r,
+        "range_guard": {"trips_in_timed_steps": m["range_timed"], "trips_total": m["range_trips"],
                         "basis": "split-fp16 range flag (|x| >= 65504 in any conv output) checked after the "
                                  "timed steps; a trip means a batch must be recomputed on the fp32 kernels "
                                  "(isl_net_range_info counts them per net)"},
-        "post": post_fields(H, W, B, post_ms, pairs),
+        "post": post_fields(H, W, B, post_ms, m["pairs"]),
         "e2e": e2e,
         "cpu_baseline": None,
     }
@@ -442,6 +414,77 @@ def gpu_main(args, rank, local, world):
         out["cpu_baseline"] = cpu_baseline(args, mult, nh, nw)
     print(json.dumps(out))
     sys.stdout.flush()
+
+
+def roofline_of(ops):
+    """Roofline fields of the dominant kernel class from per-op HIP-event timings (summed
+    over lanes and recorded runs): achieved = the MFMA FLOPs its algorithm needs / summed
+    launch time, against the dense peak of the dtype the matrix cores run."""
+    kinds = {}
+    for o in ops:
+        for k in set(o["kind"].tolist()):
+            msk = o["kind"] == k
+            d = kinds.setdefault(int(k), {"ms": 0.0, "flops": 0.0, "mfma_flops": 0.0, "launches": 0})
+            d["ms"] += float(o["ms"][msk].sum())
+            d["flops"] += float(o["flops"][msk].sum())
+            d["mfma_flops"] += float(o["mfma_flops"][msk].sum())
+            d["launches"] += int(msk.sum()) * o["n_runs"]
+    dom = max(kinds, key=lambda k: kinds[k]["ms"])
+    dk = kinds[dom]
+    peak = KIND_PEAK.get(dom, PEAK_FP32_MFMA_TFLOPS)
+    sec = dk["ms"] * 1e-3
+    fp32_equiv = dk["flops"] / sec / 1e12                      # direct-conv FLOPs (SURVEY 8d) per second
+    achieved = ALG_FACTOR.get(dom, 1.0) * dk["flops"] / sec / 1e12   # MFMA work the algorithm needs, no padding
+    executed = dk["mfma_flops"] / sec / 1e12                   # what the matrix cores ran (tile padding included)
+    conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3, 4))
+    conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3, 4))
+    key = {1: "direct", 2: "wino", 3: "x3", 4: "wino_x3"}.get(dom, "x3")
+    traffic = mfma_busy = clk = busy_s = clk_s = stage_busy = stage_busy_s = src = None
+    prof = os.path.join(REPO, "profiles", "conv_traffic.json")
+    if os.path.exists(prof):
+        pj = json.load(open(prof))
+        traffic = pj.get(key + "_hbm_bytes_per_launch")
+        mfma_busy, clk = pj.get(key + "_mfma_busy_frac"), pj.get(key + "_effective_clock_ghz")
+        busy_s, clk_s = pj.get(key + "_mfma_busy_frac_at_stamp_clock"), pj.get(key + "_stamp_clock_ghz")
+        stage_busy = pj.get("conv_stage_mfma_busy_frac")
+        stage_busy_s = pj.get("conv_stage_mfma_busy_frac_at_stamp_clock")
+        src = pj.get("source")
+    runs = max(1, ops[0]["n_runs"])
+    return {"bound": "mfma", "kernel": KIND[dom], "_dom": dom,
+            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "achieved_basis": "MFMA FLOPs the kernel's algorithm needs (direct-conv count 2*Cout*Cin*k*k*H*W "
+                              "x %.4g: split-fp16 = 3 fp16 products per fp32 MAC, Winograd = 16/36, tile "
+                              "padding excluded) / summed launch time; peak = dense MFMA peak of the dtype the "
+                              "matrix cores run (fp16 2516.6 / fp32 157.3 TF)" % ALG_FACTOR.get(dom, 1.0),
+            "fp32_equiv_tflops": round(fp32_equiv, 2),
+            "fp32_equiv_vs_fp32_peak": round(fp32_equiv / PEAK_FP32_MFMA_TFLOPS, 4),
+            "executed_tflops": round(executed, 2),
+            "executed_frac": round(executed / peak, 4),
+            "launches": dk["launches"], "avg_launch_us": round(dk["ms"] * 1e3 / dk["launches"], 2),
+            "algorithmic_gflop_per_launch": round(dk["flops"] / dk["launches"] / 1e9, 3),
+            "all_convs_tflops": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2),
+            "ms_per_step_by_kind": {KIND[k]: round(v["ms"] / runs, 3) for k, v in kinds.items()},
+            # PMC (profiles/conv_traffic.json, from tools/profile_round.sh): MFMA pipe busy
+            # fraction of the dominant kernel's wall cycles, and the DVFS clock it ran at; the
+            # conv stage adds conv1_1's write-bound conv_x3_rgb
+            "mfma_busy_pmc": mfma_busy,
+            "conv_stage_mfma_busy_pmc": stage_busy,
+            "conv_stage_mfma_busy_pmc_at_stamp_clock": stage_busy_s,
+            "effective_clock_ghz": clk,
+            "frac_at_effective_clock": round(achieved / (peak * clk / 2.4), 4) if clk else None,
+            # the GRBM-based clock reads high on sub-10 ms dispatches (MI355X_MICROARCH.md DVFS item 6);
+            # the in-kernel clock of a stamp build (s_memtime / s_memrealtime) of the dominant shape:
+            "mfma_busy_pmc_at_stamp_clock": busy_s,
+            "stamp_clock_ghz": clk_s,
+            "frac_at_stamp_clock": round(achieved / (peak * clk_s / 2.4), 4) if clk_s else None,
+            "pmc_source": src or "profiles/conv_traffic.json (tools/profile_round.sh + tools/pmc_summary.py)",
+            # the bare x3 inner loop (LDS fragment reads + 3 MFMAs per product, no staging,
+            # no barriers) on every CU: what the chip sustains with this MFMA shape under its
+            # power limit (the clock settles at ~1.55 GHz)
+            "mfma_loop_ceiling_tflops": MFMA_LOOP_CEILING_TF if key == "x3" else None,
+            "frac_of_mfma_loop_ceiling": round(achieved / MFMA_LOOP_CEILING_TF, 4) if key == "x3" else None,
+            "ceiling_source": "tools/mfma_shape_bench.hip step32, profiles/r02/mfma_shape/mfma_shape_bench.txt"}
 
 
 def post_fields(H, W, B, post_ms, pairs):

@@ -54,6 +54,7 @@
 //         compiled only with -DISLPOSE_DEV, never into libislpose.so).
 //   32768 pooled input (ConvLaunch::vin): the input is the pair-max buffer of the 2x2
 //         pool before this layer; staging takes the row-pair max (x3_vin_ok).
+//   131072 the row union on v_mfma_f32_16x16x32_f16 (products folded into K, x3_m16).
 // conv_x3_rgb: the 3-channel first layers (conv1_1) with K packed as the 27 real
 // (ky, kx, c) values instead of 9 taps x 16 channels.
 #include <algorithm>
@@ -159,6 +160,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   static_assert(WSLAB % 64 == 0, "weight slab is whole 1 KiB DMA pieces");
   static_assert(BPX <= SEGMAX, "segment must hold a tile");
   constexpr bool UNION = (VAR & 512) != 0;
+  // VAR 131072: the row-union loop on v_mfma_f32_16x16x32_f16 (see the M16 loop below)
+  constexpr bool M16 = (VAR & 131072) != 0;
+  static_assert(!M16 || (UNION && KS == 3 && WAVES_M == 2 && WAVES_N == 8 && WM == 2 && WN == 2),
+                "16x16x32 form: the 128-channel row-union block (16 waves of 64co x 64px)");
   // VAR 65536: one input buffer (two barriers per step) so that a wider pixel tile fits
   // beside the double-buffered weight slabs (7x7 on 384 pixels: the 56 KiB slab per step
   // is amortised over 1.5x the pixels)
@@ -250,7 +255,217 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       }
   };
 
-  if constexpr (UNION) {
+  if constexpr (M16) {
+    // Row union on v_mfma_f32_16x16x32_f16, two taps per K step.
+    // Per 16x16 (co x px) block a lane carries K group g = lane >> 4 (8 fp16 values of
+    // chunk g & 1 of the pair).  The three products of a tap fold into K:
+    //   M(tap):   [Ahi c0 | Ahi c1 | Alo c0 | Alo c1] x [Bhi c0 | Bhi c1 | Bhi c0 | Bhi c1]
+    //             = x_hi w_hi + x_hi w_lo of the tap, every K lane used;
+    //   X(a, b):  [Ahi c0 @a | Ahi c1 @a | Ahi c0 @b | Ahi c1 @b] x [Blo c0 @a | .. | Blo c1 @b]
+    //             = the x_lo w_hi terms of two taps.
+    // A K step is two consecutive taps of the (pair, ky, kx) sequence -- M, M, X: 48 MFMAs
+    // per wave, none padded (a step of one kernel row has 3 taps, i.e. half an X left
+    // over).  Pairs come in twos (host: even pair count) so the 9 taps of a pair pair up
+    // across the pair boundary: in every 9 steps, step 4 reads pair 2k's last tap and pair
+    // 2k+1's first, each from its own union run.  Weights: the packed [pair][ky][kx][hi|lo]
+    // [h][BCO] array in tap order, 16 KiB per step by LDS-DMA (DMA waves 10-15, one step
+    // ahead).  Input: the 3-row union run of a pair, double-buffered; loader waves 0-9
+    // stage the next pair a quarter per step (steps 0-3 of a 9-step cycle pair 2k+1, steps
+    // 5-8 pair 2k+2), stored at the step end, so a run is complete before the first step
+    // that reads it and is overwritten only after the last step that read it has passed
+    // its barrier.  Same sums as the 32x32x16 loop up to the fp32 accumulation order.
+    static_assert(NWAVES == 16, "role split sized for 16-wave blocks");
+    constexpr int LOADER_WAVES = 10, DMA_WAVES = NWAVES - LOADER_WAVES;
+    constexpr int WS2 = 2 * 4 * BCO;                            // one step: 2 taps x [hi|lo][h][BCO]
+    constexpr int NP = WS2 / 64;
+    constexpr int DPW = (NP + DMA_WAVES - 1) / DMA_WAVES;
+    constexpr int SEGUP = (x3_segu_max() + 1 + 15) / 16 * 16;   // plane stride: a multiple of 256 B
+    constexpr int XSLABU = 2 * 2 * SEGUP;                       // [hi|lo][h][px]
+    static_assert((2 * WS2 + 2 * XSLABU) * 16 <= 160 * 1024, "LDS");
+    const bool loader = wave_u < LOADER_WAVES;
+    const int Pw = P * Wi;
+    const int segu = Lb - La + 2 * Pw + 2 * P + 1;
+    const long long ubase = (long long)La - Pw - P;
+    const int quarter = (2 * segu + 3) / 4;                     // staging items per step (<= 428)
+    // staging item of this thread in quarter q (q uniform, run-time): chunk of the pair
+    // ih, pixel of the run px (-1: idle)
+    auto item = [&](int q, int& ih, int& px) __attribute__((always_inline)) {
+      const int it = q * quarter + tid;
+      const bool ok = tid < quarter && it < 2 * segu;
+      ih = ok && it >= segu ? 1 : 0;
+      px = ok ? it - ih * segu : -1;
+    };
+    f32x4 ru[2];
+    auto load_q = [&](int c2, int q) __attribute__((always_inline)) {
+      int ih, px;
+      item(q, ih, px);
+      if (px >= 0) {
+        const int c = min(2 * c2 + ih, a.cin_chunks - 1);
+        if constexpr (VIN) {
+          const int u = (int)ubase + px, yy = x3_div(u, inv_wi);
+          float4 l4, h4;
+          x3_vin_load(in_f + (size_t)c * a.in_chs, yy, u - yy * Wi, a, l4, h4);
+          ru[0] = f32x4{l4.x, l4.y, l4.z, l4.w};
+          ru[1] = f32x4{h4.x, h4.y, h4.z, h4.w};
+        } else {
+          const float* src = in_f + (size_t)c * a.in_chs + (size_t)(ubase + px) * 8;
+          ru[0] = *(const f32x4*)src;
+          ru[1] = *(const f32x4*)(src + 4);
+        }
+      }
+    };
+    auto store_q = [&](int q, int bx) __attribute__((always_inline)) {
+      int ih, px;
+      item(q, ih, px);
+      f16x8* sx = smem + 2 * WS2 + bx * XSLABU;
+      f16x8 hi, lo;
+      x3_split8(ru[0], ru[1], hi, lo);
+      if (px < 0) px = SEGUP - 1;                                  // idle items: the dummy slot
+      sx[(0 * 2 + ih) * SEGUP + px] = hi;
+      sx[(1 * 2 + ih) * SEGUP + px] = lo;
+    };
+    const int T2 = a.pairs * KS * KS / 2;                       // steps (pairs even)
+    auto issue_w = [&](int st, int bw) __attribute__((always_inline)) {
+      const f16x8* src = a.wpk + ((size_t)co_t * T2 + st) * WS2;
+      f16x8* dst = smem + bw * WS2;
+#pragma unroll
+      for (int k = 0; k < DPW; ++k) {
+        const int q = (wave_u - LOADER_WAVES) * DPW + k;
+        if (NP % DMA_WAVES == 0 || q < NP)
+          __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
+                                           (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
+      }
+    };
+    const int g = lane >> 4, r16 = lane & 15, gc = g & 1;
+    const bool g_lo = g < 2;
+    int rel16[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = min(m0 + wave_n * 64 + j * 16 + r16, mlast);
+      const int y = m / a.W, x = m - y * a.W;
+      rel16[j] = (y + a.in_pad) * Wi + x + a.in_pad - La;
+    }
+    f32x4 acc4[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc4[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // B fragments of the 4 pixel blocks held, A streamed per channel block
+    auto mfma4x4 = [&](const f16x8* w, const f16x8 (&B)[4]) __attribute__((always_inline)) {
+      f16x8 A = w[0];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f16x8 An = w[16 * (i < 3 ? i + 1 : 3)];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[j], acc4[i][j], 0, 0, 0);
+        A = An;
+      }
+    };
+    const f16x8* wlane = smem + wave_m * 64 + r16;
+    const f16x8* xlane = smem + 2 * WS2 + gc * SEGUP;
+    // tap tau of the sequence -> its input offset (pair run, row, column) in units
+    auto tap_off = [&](int tau) __attribute__((always_inline)) {
+      const int p = tau / 9, r = tau - 9 * p, ky = r / 3, kx = r - 3 * ky;
+      return (p & 1) * XSLABU + ky * Wi + kx;
+    };
+    // prologue: weights of step 0, the whole union run of pair 0
+    if (!loader) issue_w(0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      load_q(0, q);
+      store_q(q, 0);
+    }
+    __syncthreads();
+    for (int st = 0; st < T2; ++st) {
+      const int bw = st & 1;
+      const int o0 = __builtin_amdgcn_readfirstlane(tap_off(2 * st));
+      const int o1 = __builtin_amdgcn_readfirstlane(tap_off(2 * st + 1));
+      const int cyc = st / 9, j9 = st - 9 * cyc;
+      // staging of this step: a quarter of pair 2 cyc + 1 (steps 0-3) or 2 cyc + 2 (5-8)
+      const int spair = j9 < 4 ? 2 * cyc + 1 : 2 * cyc + 2, sq = j9 < 4 ? j9 : j9 - 5;
+      const bool stage = loader && j9 != 4 && spair < a.pairs;
+      if (!loader && st + 1 < T2) issue_w(st + 1, bw ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
+      {   // M of the first tap
+        f16x8 B[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) B[j] = xlane[o0 + rel16[j]];
+        mfma4x4(wlane + bw * WS2 + g * BCO, B);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (stage) load_q(spair, sq);
+      __builtin_amdgcn_sched_barrier(0);
+      {   // M of the second tap
+        f16x8 B[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) B[j] = xlane[o1 + rel16[j]];
+        mfma4x4(wlane + bw * WS2 + (4 + g) * BCO, B);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      {   // X of both taps: lanes g < 2 the first, g >= 2 the second
+        const int ox = g_lo ? o0 : o1;
+        f16x8 B[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) B[j] = xlane[2 * SEGUP + ox + rel16[j]];
+        mfma4x4(wlane + bw * WS2 + ((g_lo ? 0 : 4) + gc) * BCO, B);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (stage) store_q(sq, spair & 1);
+      __syncthreads();
+    }
+    // epilogue of the 16x16 blocks: lane = pixel r16 of block j, channels 4g..4g+3 of block i
+    const int Wo = a.hpool ? a.W / 2 : a.W + 2 * a.out_pad;
+    float* out_f = a.out + (size_t)n * a.out_fs;
+    bool bad = false;
+    float* ebias = (float*)smem;                  // [BCO] bias, [BCO] slope
+    for (int i = tid; i < BCO; i += NT) {         // the K loop ended on a barrier: LDS is free
+      ebias[i] = a.bias[co_t * BCO + i];
+      ebias[BCO + i] = a.act == ACT_PRELU ? a.slope[co_t * BCO + i] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + wave_n * 64 + j * 16 + r16;
+      if (m > mlast) continue;
+      const int y = m / a.W, x = m - y * a.W;
+      float* op = a.hpool ? out_f + (size_t)(y * Wo + (x >> 1)) * 8
+                          : out_f + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int cl = wave_m * 64 + i * 16 + 4 * g, co = co_t * BCO + cl;
+        const f32x4 b = *(const f32x4*)(ebias + cl);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc4[i][j][e] * a.wscale_inv + b[e];
+        if (a.act == ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        } else if (a.act == ACT_PRELU) {
+          const f32x4 sl = *(const f32x4*)(ebias + BCO + cl);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bad |= !(__builtin_fabsf(v[e]) < 65504.f);
+        if (a.hpool) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = fmaxf(v[e], __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v[e]), 0xB1, 0xF, 0xF, false)));
+          if (x & 1) continue;
+        }
+        float* oc = op + (size_t)(co >> 3) * a.out_chs + (co & 7);
+        if (co + 3 < a.cout) {
+          *(f32x4*)oc = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (co + e < a.cout) oc[e] = v[e];
+        }
+      }
+    }
+    if (bad) atomicOr(a.range_flag, 1);
+    return;
+  } else if constexpr (UNION) {
     // Row union, role split.  The KS input rows of a chunk pair are staged once, as
     // one run covering rows -P..+P of the tile, a third per ky step (ky then only
     // offsets the B reads by ky*Wi); for tiles spanning several image rows (46x82,
@@ -996,6 +1211,14 @@ static bool x3_union(const ConvLaunch& c) {
   return x3_union_run(c) <= x3_segu_max();
 }
 
+// The row union on v_mfma_f32_16x16x32_f16 (VAR 131072) for 128-channel tiles with an even
+// number of chunk pairs.  ISLPOSE_X3_M16=0|1 (read per launch: A/B in one process).
+static bool x3_m16(const ConvLaunch& c) {
+  const char* e = getenv("ISLPOSE_X3_M16");
+  const bool on = e && e[0] == '1';
+  return on && c.ks == 3 && c.bco == 128 && ((c.cin_chunks + 1) / 2) % 2 == 0;
+}
+
 // K-range plan of a launch on the 128-pixel family: S ranges, computed across S blocks
 // per tile (split-K, partials through the workspace) when the plain grid has fewer
 // blocks than CUs, else in one block (tools/gpu_across.sh: across wins 10-50 % at
@@ -1040,11 +1263,14 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
         }
       }
 #endif
+      const bool m16 = c.bco == 128 && x3_m16(c);
       if (c.vin) {
+        if (m16) return launch_t<KS, 2, 8, 2, 2, 512 | 32768 | 131072, 4>(c, s);
         if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 32768, 4>(c, s);
         set_error("conv_x3: pooled-input staging without a variant (x3_vin_ok)");
         return hipErrorInvalidValue;
       }
+      if (m16) return launch_t<KS, 2, 8, 2, 2, 512 | 131072, 4>(c, s);
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 512, 4>(c, s);
         case 96: return launch_t<KS, 1, 16, 3, 1, 512, 4>(c, s);

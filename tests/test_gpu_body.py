@@ -411,3 +411,30 @@ def test_colliding_pyramid_scales_serialised(w25):
         _, p1, h1 = one.run_scales(frames, keep_maps=True)
         torch.cuda.synchronize()
         assert torch.equal(pafs[i], p1[0]) and torch.equal(heats[i], h1[0]), s
+
+
+def test_x3_m16_union_vs_oracle(net25, w25, monkeypatch):
+    """The row union on v_mfma_f32_16x16x32_f16 (VAR 131072, ISLPOSE_X3_M16=1; two taps per
+    K step, the three split products folded into K) at the timed configuration: the 46x82
+    and 92x164 3x3 layers with 128-channel tiles take it (asserted through
+    isl_net_op_info); the maps stay within 1e-5 of the 32x32x16 kernel's (the same sums in
+    another fp32 order) and within the 1e-4 bar of the oracle."""
+    n, h, w = 32, 368, 656
+    x = _inputs(n, h, w, seed=4242)
+    xt = torch.from_numpy(x).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_M16", "0")
+    paf0, heat0 = net25.forward(xt)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("ISLPOSE_X3_M16", "1")
+    paf1, heat1 = net25.forward(xt)
+    torch.cuda.synchronize()
+    var = {name: rt.decode_variant(v) for name, v in net25.op_variants()}
+    m16 = [k for k, v in var.items() if v.get("var", 0) & 131072]
+    assert "conv3_2" in m16 and "conv4_1" in m16 and "Mconv2_stage1_L2_1" in m16, m16
+    assert all(var[k]["bco"] == 128 and var[k]["union"] for k in m16)
+    assert _rel(paf1.cpu().numpy(), paf0.cpu().numpy()) < 1e-5
+    assert _rel(heat1.cpu().numpy(), heat0.cpu().numpy()) < 1e-5
+    fn = cpu_ref.make_net_fn("body25", w25)
+    for f in (0, 31):
+        rp, rh = fn(x[f:f + 1])
+        assert _rel(paf1[f:f + 1].cpu().numpy(), rp) < TOL and _rel(heat1[f:f + 1].cpu().numpy(), rh) < TOL

@@ -99,7 +99,12 @@ int main(int argc, char** argv) {
       pos = e + 1;
       ConvLaunch c = L;
       auto launch = [&]() -> hipError_t {
-        if (a == "x3") { c.bco = bco; c.wpk = wd; return launch_conv_x3(c, 0); }
+        // x3m: the row union on 16x16x32 MFMAs (ISLPOSE_X3_M16=1, read per launch); x3: off
+        if (a == "x3" || a == "x3m") {
+          setenv("ISLPOSE_X3_M16", a == "x3m" ? "1" : "0", 1);
+          c.bco = bco; c.wpk = wd;
+          return launch_conv_x3(c, 0);
+        }
         if (a == "direct") { c.bco = bco; c.wpk = wd; return launch_conv(c, 0); }
         if (a == "wino" && wb && ks == 3) { c.bco = wb; c.wpk = wu; return launch_wino(c, 0); }
         if (a == "wx3" && ks == 3) { c.wx3 = wux; return launch_wino_x3(c, 0); }
@@ -114,7 +119,7 @@ int main(int argc, char** argv) {
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       const double us = ms * 1e3 / iters;
-      const double fac = a == "x3" ? 3.0 : a == "wx3" ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
+      const double fac = (a == "x3" || a == "x3m") ? 3.0 : a == "wx3" ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
       printf("  round %d %-7s %9.1f us  fp32-equiv %7.1f TF  alg-MFMA %7.1f TF\n", r, a.c_str(), us,
              flops / us / 1e6, fac * flops / us / 1e6);
     }

@@ -173,7 +173,9 @@ int isl_net_timing(isl_net* net, int max_ops, int* n_ops, int* n_runs, double* o
  * "maxpool2") and, for the last isl_net_run / isl_net_forward, which conv kernel variant
  * each ran: for ISL_ALGO_X3 convs the variant code of csrc/internal.h x3_variant_code
  * (VAR bits: 512 row union, 1024 in-block K ranges, 2048 split-K, 4096 two pairs per
- * step, 32768 pooled-input staging, 65536 one input buffer, 262144 conv1_1 kernel;
+ * step, 8192 folds its producers' split-K partials, 32768 pooled-input staging, 65536 one
+ * input buffer, 131072 16x16x32 row union, 262144 conv1_1 kernel, 524288 split-K partials
+ * left to its consumers (no reduce launch);
  * tile pixels / 32 at bits 20-24, output channels / 32 at bits 25-28, ks / 2 at 29-30);
  * -1 for a pool folded into the next conv's staging; 0 otherwise.  index < the op
  * count (isl_net_timing's *n_ops). */

@@ -88,6 +88,7 @@ struct X3Args {
   unsigned long long* dbg;      // VAR 16384 (development): s_memtime stamps of block 0
   int hpool;                    // ConvLaunch::hpool: out is the [n][chunk][H][W/2][8] pair-max buffer
   int vin;                      // ConvLaunch::vin: in is the [n][chunk][2H][W][8] pair-max buffer of a pool
+  const X3Fold* fold;           // VAR 8192: per input chunk, the split-K partials it is folded from
 };
 
 // u / d for 0 <= u < 2^20, d >= 1, through the fp32 reciprocal r = 1/d: (u + 0.5) / d sits
@@ -177,6 +178,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr bool SPLIT = (VAR & 2048) != 0;
   constexpr bool STAMP = (VAR & 16384) != 0;
   constexpr bool VIN = (VAR & 32768) != 0;      // ConvLaunch::vin (pooled-input staging)
+  // VAR 8192: input chunks whose producer left split-K partial sums (ConvLaunch::fold) are
+  // staged as the reduction x3_splitk_reduce would have stored them
+  constexpr bool FOLD = (VAR & 8192) != 0;
+  static_assert(!(FOLD && (VIN || UNION || M16 || KS > 3 || PPS > 1)), "fold: the generic loop of 1x1 / 3x3 layers");
   static_assert(!(UNION && (RANGED || SPLIT)), "K ranges run on the generic loop");
   static_assert(PPS == 1 || !(UNION || RANGED || SPLIT), "two pairs per step: plain generic loop only");
   __shared__ f16x8 smem[SMEM];
@@ -590,14 +595,61 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       if (it >= 2 * PPS * seg) ipx[i] = -1;   // idle
     }
     f32x4 raw[IT][2];
+    bool fold_bad = false;
     auto load_x = [&](int t) __attribute__((always_inline)) {
       const int c2 = t / KS, ky = t - c2 * KS;
       const long long row = (long long)(La + (ky - P) * Wi - P);
+      X3Fold fe[2];
+      if constexpr (FOLD) {   // the step's two chunks (uniform)
+        fe[0] = a.fold[min(2 * c2, a.cin_chunks - 1)];
+        fe[1] = a.fold[min(2 * c2 + 1, a.cin_chunks - 1)];
+      }
 #pragma unroll
       for (int i = 0; i < IT; ++i) {
         const int c = 2 * PPS * c2 + ih[i];
         if (ipx[i] >= 0 && c < a.cin_chunks) {
-          if constexpr (VIN) {   // padded (row, column) of the item, recomputed per step
+          if (FOLD && (ih[i] ? fe[1].ws : fe[0].ws)) {
+            // x3_splitk_reduce's arithmetic on the producer's partials: ranges summed in
+            // order, x 2^-s + bias, activation (the same bits it would have stored); the
+            // padding ring reads as zeros; the value is range-checked here
+            const X3Fold& f = ih[i] ? fe[1] : fe[0];
+            const int u = (int)row + ipx[i], yy = x3_div(u, inv_wi), y = yy - a.in_pad, x = u - yy * Wi - a.in_pad;
+            if (y < 0 || y >= a.H || x < 0 || x >= a.W) {
+              raw[i][0] = raw[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            } else {
+              const float* p = f.ws + (size_t)n * f.fstride + (size_t)(y * a.W + x) * 8;
+              f32x4 s0 = *(const f32x4*)p, s1 = *(const f32x4*)(p + 4);
+              for (int k = 1; k < f.S; ++k) {
+                s0 += *(const f32x4*)(p + k * f.sstride);
+                s1 += *(const f32x4*)(p + k * f.sstride + 4);
+              }
+              const f32x4 b0 = *(const f32x4*)f.bias, b1 = *(const f32x4*)(f.bias + 4);
+              f32x4 v0, v1;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                v0[e] = s0[e] * f.scale + b0[e];
+                v1[e] = s1[e] * f.scale + b1[e];
+              }
+              if (f.act == ACT_RELU) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  v0[e] = v0[e] > 0.f ? v0[e] : 0.f;
+                  v1[e] = v1[e] > 0.f ? v1[e] : 0.f;
+                }
+              } else if (f.act == ACT_PRELU) {
+                const f32x4 l0 = *(const f32x4*)f.slope, l1 = *(const f32x4*)(f.slope + 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  v0[e] = v0[e] >= 0.f ? v0[e] : v0[e] * l0[e];
+                  v1[e] = v1[e] >= 0.f ? v1[e] : v1[e] * l1[e];
+                }
+              }
+#pragma unroll
+              for (int e = 0; e < 4; ++e) fold_bad |= !(__builtin_fabsf(v0[e]) < 65504.f) || !(__builtin_fabsf(v1[e]) < 65504.f);
+              raw[i][0] = v0;
+              raw[i][1] = v1;
+            }
+          } else if constexpr (VIN) {   // padded (row, column) of the item, recomputed per step
             const int u = (int)row + ipx[i], yy = x3_div(u, inv_wi);
             float4 l4, h4;
             x3_vin_load(in_f + (size_t)c * a.in_chs, yy, u - yy * Wi, a, l4, h4);
@@ -692,6 +744,9 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       for (int wm = 0; wm < WM; ++wm)
 #pragma unroll
         for (int wn = 0; wn < WN; ++wn) acc[wm][wn] = tot[wm][wn];
+    }
+    if constexpr (FOLD) {
+      if (fold_bad) atomicOr(a.range_flag, 1);
     }
   }
 
@@ -1029,6 +1084,8 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
     a.in_chs = (long long)2 * c.H * c.W * 8;
   }
   a.vin = c.vin;
+  a.fold = c.fold;
+  if ((c.fold != nullptr) != ((VAR & 8192) != 0)) { set_error("conv_x3: fold variant mismatch"); return hipErrorInvalidValue; }
   if (c.vin != ((VAR & 32768) != 0)) { set_error("conv_x3: pooled-input variant mismatch"); return hipErrorInvalidValue; }
   a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
   a.in_fs = a.in_chs * (c.in_cs / 8);
@@ -1065,8 +1122,13 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN, VAR, OCC>), dim3(a.nblocks),
                      dim3(WAVES_M * WAVES_N * 64), 0, s, a);
   if constexpr (SPLIT) {
-    const long long nt = (long long)c.n * ((c.cout + 3) / 4) * c.H * c.W;
-    hipLaunchKernelGGL(x3_splitk_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, a);
+    // fold_out: every consumer sums the partials in its staging (X3Fold), no reduce launch
+    if (!c.fold_out) {
+      const long long nt = (long long)c.n * ((c.cout + 3) / 4) * c.H * c.W;
+      hipLaunchKernelGGL(x3_splitk_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, a);
+    }
+  } else {
+    if (c.fold_out) { set_error("conv_x3: fold_out without split-K across blocks"); return hipErrorInvalidValue; }
   }
   return hipGetLastError();
 }
@@ -1324,6 +1386,22 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   static const int more = getenv("ISLPOSE_X3_S8") ? atoi(getenv("ISLPOSE_X3_S8")) : 1;
   if (more) {
     {
+      if constexpr (KS <= 3) {
+        if (c.fold) {   // consumers of folded split-K partials (x3_fold_ok)
+          switch (c.bco) {
+            case 128:
+              if (split) return launch_t<KS, 2, 4, 2, 1, 2048 | 8192, 2>(c, s);
+              if (ranged) return launch_t<KS, 2, 4, 2, 1, 1024 | 8192, 2>(c, s);
+              return launch_t<KS, 2, 4, 2, 1, 8192, 2>(c, s);
+            case 96:
+              if (split) return launch_t<KS, 3, 4, 1, 1, 2048 | 8192, 2>(c, s);
+              if (ranged) return launch_t<KS, 3, 4, 1, 1, 1024 | 8192, 2>(c, s);
+              return launch_t<KS, 3, 4, 1, 1, 8192, 2>(c, s);
+          }
+          set_error("conv_x3: fold without a variant (x3_fold_ok)");
+          return hipErrorInvalidValue;
+        }
+      }
       switch (c.bco) {
         case 128:   // 8 waves of 64co x 32px
           if (split) return launch_t<KS, 2, 4, 2, 1, 2048, 2>(c, s);
@@ -1372,6 +1450,18 @@ double conv_x3_mfma_flops(const ConvLaunch& c) {
   const double co = (double)((c.cout + c.bco - 1) / c.bco) * c.bco;
   const double px = std::ceil((double)c.H * c.W / tile_pixels(c, BPX, x3_segmax(BPX))) * BPX;
   return 3.0 * 2.0 * co * (((c.cin_chunks + 1) / 2) * 16.0) * c.ks * c.ks * px * c.n;
+}
+
+int x3_split_ranges(const ConvLaunch& c, bool* across_blocks) {
+  const X3Ranges r = x3_ranges(c);
+  if (across_blocks) *across_blocks = r.across_blocks;
+  return r.S;
+}
+
+bool x3_fold_ok(const ConvLaunch& c) {
+  static const int more = getenv("ISLPOSE_X3_S8") ? atoi(getenv("ISLPOSE_X3_S8")) : 1;
+  return more && x3_fits(c) && c.ks <= 3 && !c.vin && !c.hpool && (c.bco == 128 || c.bco == 96) &&
+         !x3_big_tiles(c) && (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) < (1 << 20);
 }
 
 size_t x3_splitk_ws_floats(const ConvLaunch& c) {

@@ -24,6 +24,19 @@ struct Act {
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_PRELU = 2 };
 
+// One input chunk of a split-fp16 conv whose producer left split-K partial sums instead
+// of its output (ConvLaunch::fold, conv_x3 VAR 8192): the consumer's staging sums them in
+// range order and applies the producer's epilogue, exactly as x3_splitk_reduce would have
+// (the reduce launch is skipped).  ws == nullptr: the chunk is read from the buffer.
+struct X3Fold {
+  const float* ws;          // partials of this chunk: + n * fstride + m * 8 + k * sstride (range k)
+  long long fstride, sstride;
+  const float* bias;        // 8 values of the chunk
+  const float* slope;       // 8 PReLU slopes (act == ACT_PRELU)
+  float scale;              // the producer's 2^-s
+  int S, act, pad_;
+};
+
 // One convolution launch.
 struct ConvLaunch {
   const float* in;  int in_pad, in_cs, in_coff;
@@ -56,6 +69,11 @@ struct ConvLaunch {
   // pair on the fly (the ring, in_pad wide, reads as zeros), so the pool kernel and its
   // output buffer are skipped.  in_pad / in_cs / in_coff describe the pooled buffer.
   int vin = 0;
+  // Split-K fold (conv_x3 only).  fold: device table [cin_chunks] of X3Fold for this conv's
+  // input chunks (a consumer); fold_out: this conv's across-block partial sums are consumed
+  // by folding consumers, so its x3_splitk_reduce launch is skipped (a producer).
+  const X3Fold* fold = nullptr;
+  int fold_out = 0;
 };
 
 // Pixels per tile of the flattened-raster conv kernels: BPX, or fewer when the
@@ -101,12 +119,18 @@ double conv_x3_mfma_flops(const ConvLaunch& c);
 // (pixels / 32 at bits 20-24, output channels / 32 at bits 25-28) and the kernel radius
 // (ks / 2) at bits 29-30.
 constexpr int X3V_RGB = 1 << 18;
+constexpr int X3V_FOLD_OUT = 1 << 19;   // a split-K producer whose reduce was folded into its consumers
 constexpr int x3_variant_code(int var, int ks, int bpx, int bco) {
   return (var & 0xfffff) | ((bpx / 32) << 20) | ((bco / 32) << 25) | ((ks / 2) << 29);
 }
 int x3_last_variant();
 // floats of split-K workspace launch_conv_x3 would use for c (0 = no split)
 size_t x3_splitk_ws_floats(const ConvLaunch& c);
+// K ranges launch_conv_x3 would use for c: S, and whether they run across blocks (split-K
+// through the workspace) -- the producers a consumer can fold
+int x3_split_ranges(const ConvLaunch& c, bool* across_blocks);
+// whether launch_conv_x3 would run c on its generic loop (the loop that can fold)
+bool x3_fold_ok(const ConvLaunch& c);
 // Split-fp16 Winograd F(2x2,3x3) (wino_x3.hip): 3x3 layers with cout % 4 == 0;
 // c.wx3 then holds the split transformed filters [co_tile][pair][xi][hi|lo][h][64][8].
 hipError_t launch_wino_x3(const ConvLaunch& c, hipStream_t s);

@@ -215,6 +215,15 @@ struct isl_net {
     size_t tab_bytes = 0;
     float* ks = nullptr;
     size_t ks_floats = 0;
+    // split-K fold plan for the current batch size (plan_fold): per op, the offset of a
+    // producer's partial sums in fold_mem (-1: none) and of a consumer's X3Fold table in
+    // fold_tab (-1: none)
+    int fold_n = -1, fold_mode = -1;
+    std::vector<long long> fold_ws_off, fold_tab_off;
+    float* fold_mem = nullptr;
+    size_t fold_mem_floats = 0;
+    X3Fold* fold_tab = nullptr;
+    size_t fold_tab_n = 0;
   };
   std::map<long long, Arena> plans;
   Arena* cur = nullptr;        // the arena of the current plan
@@ -666,6 +675,8 @@ static void drop_arena(isl_net* net, std::map<long long, isl_net::Arena>::iterat
   (void)hipFree(it->second.base);
   if (it->second.tab) (void)hipFree(it->second.tab);
   if (it->second.ks) (void)hipFree(it->second.ks);
+  if (it->second.fold_mem) (void)hipFree(it->second.fold_mem);
+  if (it->second.fold_tab) (void)hipFree(it->second.fold_tab);
   net->plans_bytes -= it->second.bytes;
   if (net->arena == it->second.base) {
     net->arena = nullptr;
@@ -786,6 +797,148 @@ static bool pool_into_next_conv(const isl_net* net, size_t k) {
   return true;
 }
 
+// ISLPOSE_X3_FOLD=0: every split-K producer runs its x3_splitk_reduce launch (A/B; read per run)
+static bool fold_enabled() {
+  const char* e = getenv("ISLPOSE_X3_FOLD");
+  return !(e && e[0] == '0');
+}
+
+// The conv launch of op k before the per-run adjustments (pools, wide 1x1 tiles, fold)
+static ConvLaunch basic_launch(const isl_net* net, const Op& op) {
+  const Act& in = net->act[op.in];
+  const Act& out = net->act[op.out];
+  const ConvLayer& c = net->layers[op.layer];
+  ConvLaunch L;
+  L.in = in.base; L.in_pad = in.pad; L.in_cs = in.cs; L.in_coff = op.in_coff;
+  L.out = out.base; L.out_pad = out.pad; L.out_cs = out.cs; L.out_coff = op.out_coff;
+  L.wpk = c.d_w; L.bias = c.d_b; L.slope = c.d_s;
+  L.n = in.n; L.H = in.H; L.W = in.W; L.ks = c.k; L.cin_chunks = c.cin_phys / 8;
+  L.cout = c.cout; L.bco = c.bco; L.act = c.act;
+  L.wx3 = c.d_wx3; L.wscale_inv = c.x3_inv; L.range_flag = net->d_flag;
+  L.allow_split = net->split_k;
+  return L;
+}
+
+// Split-K fold plan of the current arena at its batch size (small grids, e.g. batch-1
+// Mode R frames, where every 23x41 stage layer splits its canonical K ranges across
+// blocks): a producer whose output slice is read only by convs on the generic loop -- no
+// net output, no pool, cout a multiple of 8 -- keeps its partial sums in a region of its
+// own and skips its reduce launch; each consumer's X3Fold table points its chunks at them.
+// Same bits: the consumer's staging performs the reduce's arithmetic.
+static int plan_fold(isl_net* net, hipStream_t s) {
+  isl_net::Arena& ar = *net->cur;
+  const int mode = (net->algo == ISL_ALGO_X3 && net->split_k > 0 && fold_enabled()) ? 1 : 0;
+  if (ar.fold_n == net->pn && ar.fold_mode == mode) return ISL_OK;
+  const size_t nops = net->ops.size();
+  ar.fold_ws_off.assign(nops, -1);
+  ar.fold_tab_off.assign(nops, -1);
+  ar.fold_n = net->pn;
+  ar.fold_mode = mode;
+  if (!mode) return ISL_OK;
+  auto is_conv_x3 = [&](size_t k) { return net->ops[k].type == 0 && x3_fits(basic_launch(net, net->ops[k])); };
+  // a consumer may fold only on the generic loop with no pool on either side
+  auto consumer_ok = [&](size_t j) {
+    if (!is_conv_x3(j)) return false;
+    const Op& op = net->ops[j];
+    if (j > 0 && net->ops[j - 1].type == 1 && net->ops[j - 1].out == op.in) return false;
+    if (j + 1 < nops && net->ops[j + 1].type == 1 && net->ops[j + 1].in == op.out) return false;
+    const ConvLayer& c = net->layers[op.layer];
+    if (c.d_wrgb) return false;
+    return x3_fold_ok(basic_launch(net, op));
+  };
+  struct Prod { size_t k; int S; long long off; std::vector<size_t> cons; };
+  std::vector<Prod> prods;
+  long long total = 0;
+  for (size_t k = 0; k < nops; ++k) {
+    const Op& op = net->ops[k];
+    if (!is_conv_x3(k)) continue;
+    const ConvLayer& c = net->layers[op.layer];
+    if (c.cout % 8 || c.d_wrgb) continue;
+    ConvLaunch L = basic_launch(net, op);
+    bool across = false;
+    const int S = x3_split_ranges(L, &across);
+    if (S < 2 || !across) continue;
+    const int lo = op.out_coff, hi = op.out_coff + c.cout;
+    auto overlaps = [&](const OutRef& o) { return o.buf == op.out && o.coff < hi && o.coff + o.C > lo; };
+    if (overlaps(net->out0) || (net->n_out > 1 && overlaps(net->out1))) continue;
+    bool ok = true;
+    std::vector<size_t> cons;
+    for (size_t j = k + 1; j < nops && ok; ++j) {
+      const Op& oj = net->ops[j];
+      if (oj.type == 1) {   // a pool reading the slice
+        if (oj.in == op.out) ok = false;
+        if (oj.out == op.out) break;
+        continue;
+      }
+      const ConvLayer& cj = net->layers[oj.layer];
+      if (oj.in == op.out && oj.in_coff < hi && oj.in_coff + cj.cin_phys > lo) {
+        if (consumer_ok(j)) cons.push_back(j);
+        else ok = false;
+      }
+      if (oj.out == op.out && oj.out_coff < hi && oj.out_coff + cj.cout > lo) break;   // overwritten
+    }
+    if (!ok || cons.empty()) continue;
+    const long long floats = (long long)S * L.n * ((c.cout + 7) / 8) * 8 * L.H * L.W;
+    prods.push_back({k, S, total, cons});
+    total += (floats + 63) / 64 * 64;
+  }
+  if (prods.empty()) return ISL_OK;
+  if ((size_t)total > ar.fold_mem_floats) {
+    if (ar.fold_mem) HIP_OK(hipFree(ar.fold_mem));   // waits for queued work that may still read it
+    ar.fold_mem = nullptr;
+    ar.fold_mem_floats = 0;
+    HIP_OK(hipMalloc(&ar.fold_mem, (size_t)total * sizeof(float)));
+    ar.fold_mem_floats = (size_t)total;
+  }
+  // consumer tables: one X3Fold per input chunk of every consumer
+  std::vector<X3Fold> tab;
+  std::map<size_t, long long> cons_off;
+  for (const Prod& p : prods)
+    for (size_t j : p.cons)
+      if (!cons_off.count(j)) {
+        cons_off[j] = (long long)tab.size();
+        const ConvLayer& cj = net->layers[net->ops[j].layer];
+        tab.resize(tab.size() + cj.cin_phys / 8, X3Fold{nullptr, 0, 0, nullptr, nullptr, 1.f, 0, 0, 0});
+      }
+  for (const Prod& p : prods) {
+    const Op& op = net->ops[p.k];
+    const ConvLayer& c = net->layers[op.layer];
+    const Act& o = net->act[op.out];
+    const long long plane = (long long)o.H * o.W * 8, c8 = (c.cout + 7) / 8;
+    ar.fold_ws_off[p.k] = p.off;
+    for (size_t j : p.cons) {
+      const Op& oj = net->ops[j];
+      const ConvLayer& cj = net->layers[oj.layer];
+      for (int ch = 0; ch < cj.cin_phys / 8; ++ch) {
+        const int pc = oj.in_coff + 8 * ch;              // physical channel of the buffer
+        if (pc < op.out_coff || pc >= op.out_coff + c.cout) continue;
+        const int cc = (pc - op.out_coff) / 8;           // the producer's chunk
+        X3Fold& f = tab[cons_off[j] + ch];
+        f.ws = ar.fold_mem + p.off + cc * plane;
+        f.fstride = c8 * plane;
+        f.sstride = (long long)o.n * c8 * plane;
+        f.bias = c.d_b + cc * 8;
+        f.slope = c.act == ACT_PRELU ? c.d_s + cc * 8 : nullptr;
+        f.scale = c.x3_inv;
+        f.S = p.S;
+        f.act = c.act;
+      }
+    }
+  }
+  for (auto& kv : cons_off) ar.fold_tab_off[kv.first] = kv.second;
+  if (tab.size() > ar.fold_tab_n) {
+    if (ar.fold_tab) HIP_OK(hipFree(ar.fold_tab));
+    ar.fold_tab = nullptr;
+    ar.fold_tab_n = 0;
+    HIP_OK(hipMalloc(&ar.fold_tab, tab.size() * sizeof(X3Fold)));
+    ar.fold_tab_n = tab.size();
+  }
+  // stream-ordered: a run queued before on this stream has read the old table (same arena,
+  // same stream); the host vector is staged by HIP before the call returns
+  HIP_OK(hipMemcpyAsync(ar.fold_tab, tab.data(), tab.size() * sizeof(X3Fold), hipMemcpyHostToDevice, s));
+  return ISL_OK;
+}
+
 static int run_ops(isl_net* net, hipStream_t s) {
   isl_net::TimedRun* tr = nullptr;
   if (net->timing) {
@@ -796,6 +949,11 @@ static int run_ops(isl_net* net, hipStream_t s) {
     HIP_OK(hipEventRecord(tr->ev[0], s));
   }
   net->op_variant.assign(net->ops.size(), 0);
+  {
+    const int rc = plan_fold(net, s);
+    if (rc) return rc;
+  }
+  const isl_net::Arena& far = *net->cur;
   bool fused = false;   // the previous conv wrote the pair-max buffer of this pool
   int vin_buf = -1;     // this conv stages from that buffer (the pool op was skipped)
   const bool fuse_pools = fused_pool_enabled(), pool_input = fuse_pools && pool_input_enabled();
@@ -874,6 +1032,15 @@ static int run_ops(isl_net* net, hipStream_t s) {
       }
       L.ws = ar.ks;
       L.ws_floats = ar.ks_floats;
+      if (far.fold_ws_off[k] >= 0) {   // a fold producer: its own partial-sum region, no reduce
+        L.ws = far.fold_mem + far.fold_ws_off[k];
+        L.ws_floats = need;
+        L.fold_out = 1;
+      }
+      if (far.fold_tab_off[k] >= 0) {   // a fold consumer
+        if (L.vin || L.hpool || !x3_fold_ok(L)) return fail(ISL_E_STATE, "split-K fold: consumer off the generic loop");
+        L.fold = far.fold_tab + far.fold_tab_off[k];
+      }
       if (c.d_wrgb && x3_rgb_fits(L) && rgb_kernel_enabled() && !L.vin) {
         L.wx3 = c.d_wrgb;
         HIP_OK(launch_conv_x3_rgb(L, s));
@@ -882,7 +1049,7 @@ static int run_ops(isl_net* net, hipStream_t s) {
         HIP_OK(launch_conv_x3(L, s));
         kind = 3; mf = conv_x3_mfma_flops(L);
       }
-      net->op_variant[k] = x3_last_variant();
+      net->op_variant[k] = x3_last_variant() | (L.fold_out ? X3V_FOLD_OUT : 0);
     } else {
       HIP_OK(launch_conv(L, s));
       mf = conv_mfma_flops(L);
@@ -1012,6 +1179,8 @@ int isl_net_destroy(isl_net* net) {
   for (auto& kv : net->plans) {
     if (kv.second.tab) (void)hipFree(kv.second.tab);
     if (kv.second.ks) (void)hipFree(kv.second.ks);
+    if (kv.second.fold_mem) (void)hipFree(kv.second.fold_mem);
+    if (kv.second.fold_tab) (void)hipFree(kv.second.fold_tab);
   }
   for (auto& kv : net->plans) (void)hipFree(kv.second.base);
   if (net->scratch) (void)hipFree(net->scratch);

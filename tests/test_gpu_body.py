@@ -438,3 +438,24 @@ def test_x3_m16_union_vs_oracle(net25, w25, monkeypatch):
     for f in (0, 31):
         rp, rh = fn(x[f:f + 1])
         assert _rel(paf1[f:f + 1].cpu().numpy(), rp) < TOL and _rel(heat1[f:f + 1].cpu().numpy(), rh) < TOL
+
+
+@pytest.mark.parametrize("n,h,w", [(1, 184, 328), (2, 184, 328), (1, 184, 200)])
+def test_splitk_fold_bit_identical(net25, n, h, w, monkeypatch):
+    """Split-K producers whose partial sums the consumers fold into their staging
+    (ConvLaunch::fold, no x3_splitk_reduce launch) give the same bits as the reduce launch
+    (ISLPOSE_X3_FOLD=0): the staging performs the reduce's arithmetic.  At batch 1-2 and
+    Mode R's 184x328 input, the 23x41 stage layers split across blocks and fold (asserted
+    through isl_net_op_info)."""
+    x = torch.from_numpy(_inputs(n, h, w, seed=3 * h + n)).cuda()
+    paf1, heat1 = net25.forward(x)
+    torch.cuda.synchronize()
+    var = [rt.decode_variant(v) for _, v in net25.op_variants()]
+    assert sum(1 for v in var if v.get("fold_out")) >= 60, sum(1 for v in var if v.get("fold_out"))
+    assert sum(1 for v in var if v.get("fold")) >= 60
+    monkeypatch.setenv("ISLPOSE_X3_FOLD", "0")
+    paf0, heat0 = net25.forward(x)
+    torch.cuda.synchronize()
+    var0 = [rt.decode_variant(v) for _, v in net25.op_variants()]
+    assert not any(v.get("fold") or v.get("fold_out") for v in var0)
+    assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)

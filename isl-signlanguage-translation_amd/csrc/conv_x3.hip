@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr int SEGMAX = x3_segmax(BPX);
   // VAR 4096 (1x1 layers, 256-channel tiles): two chunk pairs per K step
   constexpr int PPS = (VAR & 4096) ? 2 : 1;
-  static_assert(PPS == 1 || KS == 1, "two pairs per step: 1x1 layers only");
+  static_assert(PPS == 1 || KS <= 3, "two pairs per step: 1x1 / 3x3 layers");
   constexpr int WSLAB1 = KS * 2 * 2 * BCO;       // one pair: [kx][hi|lo][h][BCO]
   constexpr int WSLAB = PPS * WSLAB1;            // 16-byte units per step
   constexpr int SEGP = SEGMAX + 1;               // + one dummy slot idle staging items write to
@@ -171,7 +171,8 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr bool SIB = (VAR & 65536) != 0;
   constexpr int SEGUP = x3_segu_max() + 1;       // + dummy slot
   constexpr int XSLABU = 2 * 2 * SEGUP;          // [hi|lo][h][px]
-  constexpr int SMEM = UNION ? 2 * WSLAB + 2 * XSLABU : SIB ? 2 * WSLAB + XSLAB : 2 * BUF;
+  constexpr int SMEM = UNION ? 2 * WSLAB + 2 * XSLABU : SIB ? 2 * WSLAB + XSLAB
+                     : (VAR & 128) ? 3 * WSLAB + 2 * XSLAB : 2 * BUF;
   static_assert(!(SIB && UNION), "one input buffer: generic loop only");
   static_assert(SMEM * 16 <= 160 * 1024, "LDS");
   constexpr bool RANGED = (VAR & 1024) != 0;
@@ -181,9 +182,20 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   // VAR 8192: input chunks whose producer left split-K partial sums (ConvLaunch::fold) are
   // staged as the reduction x3_splitk_reduce would have stored them
   constexpr bool FOLD = (VAR & 8192) != 0;
+  // VAR 256: a 64-channel block of weights packed for 128-channel tiles (small grids: two
+  // independent blocks per 128-channel tile, so one block's step latency overlaps the
+  // other's MFMAs); its slab rows are the halves of the packed 128-channel rows
+  constexpr bool HALFCO = (VAR & 256) != 0;
+  static_assert(!HALFCO || (BCO == 64 && !UNION && !M16 && PPS == 1), "half-tile blocks: generic loop, 64 channels");
+  // VAR 128: the generic loop with weights and inputs prefetched two K steps ahead (three
+  // weight buffers, two register slots), a raw s_barrier with counted vmcnt waits instead of
+  // __syncthreads (which drains every LDS-DMA in flight): small grids, whose short steps
+  // otherwise wait out one L2 round trip each
+  constexpr bool DEEP = (VAR & 128) != 0;
+  static_assert(!DEEP || (!UNION && !M16 && !SIB && !FOLD && !VIN && !(VAR & 16384)), "deep prefetch: plain generic loop");
   static_assert(!(FOLD && (VIN || UNION || M16 || KS > 3 || PPS > 1)), "fold: the generic loop of 1x1 / 3x3 layers");
   static_assert(!(UNION && (RANGED || SPLIT)), "K ranges run on the generic loop");
-  static_assert(PPS == 1 || !(UNION || RANGED || SPLIT), "two pairs per step: plain generic loop only");
+  static_assert(PPS == 1 || !(UNION || M16 || HALFCO || DEEP || FOLD || VIN), "two pairs per step: generic loop");
   __shared__ f16x8 smem[SMEM];
 
   // XCD-aware tile order (conv.hip): co-tiles of a pixel tile, then neighbouring
@@ -618,11 +630,22 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
               raw[i][0] = raw[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
             } else {
               const float* p = f.ws + (size_t)n * f.fstride + (size_t)(y * a.W + x) * 8;
-              f32x4 s0 = *(const f32x4*)p, s1 = *(const f32x4*)(p + 4);
-              for (int k = 1; k < f.S; ++k) {
-                s0 += *(const f32x4*)(p + k * f.sstride);
-                s1 += *(const f32x4*)(p + k * f.sstride + 4);
+              // every range's partial in flight at once (S <= 8, uniform), then the sum in
+              // range order
+              f32x4 q0[8], q1[8];
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const float* pk = p + (k < f.S ? k : 0) * f.sstride;
+                q0[k] = *(const f32x4*)pk;
+                q1[k] = *(const f32x4*)(pk + 4);
               }
+              f32x4 s0 = q0[0], s1 = q1[0];
+#pragma unroll
+              for (int k = 1; k < 8; ++k)
+                if (k < f.S) {
+                  s0 += q0[k];
+                  s1 += q1[k];
+                }
               const f32x4 b0 = *(const f32x4*)f.bias, b1 = *(const f32x4*)(f.bias + 4);
               f32x4 v0, v1;
 #pragma unroll
@@ -666,8 +689,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
         }
       }
     };
-    auto wbuf = [&](int buf) __attribute__((always_inline)) { return smem + buf * (SIB ? WSLAB : BUF); };
-    auto xbuf = [&](int buf) __attribute__((always_inline)) { return SIB ? smem + 2 * WSLAB : smem + buf * BUF + WSLAB; };
+    auto wbuf = [&](int buf) __attribute__((always_inline)) { return smem + buf * (SIB || DEEP ? WSLAB : BUF); };
+    auto xbuf = [&](int buf) __attribute__((always_inline)) {
+      return SIB ? smem + 2 * WSLAB : DEEP ? smem + 3 * WSLAB + buf * XSLAB : smem + buf * BUF + WSLAB;
+    };
     auto store_x = [&](int buf) __attribute__((always_inline)) {
       f16x8* s = xbuf(buf);
 #pragma unroll
@@ -680,14 +705,25 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       }
     };
     auto issue_w = [&](int t, int buf) __attribute__((always_inline)) {
-      const f16x8* src = a.wpk + ((size_t)co_t * T + t) * WSLAB;
+      // HALFCO: the 128-channel packing, rows of 128 units; this block takes half of each
+      const f16x8* src = HALFCO ? a.wpk + ((size_t)(co_t >> 1) * T + t) * (2 * WSLAB) + (co_t & 1) * 64
+                                : a.wpk + ((size_t)co_t * T + t) * WSLAB;
       f16x8* dst = wbuf(buf);
 #pragma unroll
       for (int q0 = 0; q0 < WSLAB / 64; q0 += NWAVES) {
         const int q = q0 + wave_u;
-        if ((WSLAB / 64) % NWAVES == 0 || q < WSLAB / 64)
-          __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
+        if ((WSLAB / 64) % NWAVES == 0 || q < WSLAB / 64) {
+          const f16x8* sp = src + q * (HALFCO ? 128 : 64);
+          if constexpr (PPS == 2 && KS > 1) {
+            // step (pair pair c2, ky): row ky of pairs 2 c2 and 2 c2 + 1, not adjacent in the
+            // [pair][ky][kx] packing -- piece q of the slab from pair 2 c2 + q / NP1
+            constexpr int NP1 = WSLAB1 / 64;
+            const int c2 = t / KS, ky = t - c2 * KS, pp = q / NP1;
+            sp = a.wpk + (((size_t)co_t * a.pairs + 2 * c2 + pp) * KS + ky) * WSLAB1 + (q - pp * NP1) * 64;
+          }
+          __builtin_amdgcn_global_load_lds((const void*)(sp + lane),
                                            (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
+        }
       }
     };
     auto compute = [&](int buf) __attribute__((always_inline)) {
@@ -699,28 +735,25 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
         for (int kx = 0; kx < KS; ++kx) tap(sw, sx, PPS * SEGP, kx);
       }
     };
+    auto compute_deep = [&](int wb, int xb) __attribute__((always_inline)) {
+      const f16x8* sw = wbuf(wb) + h * BCO + wave_m * WM * 32 + l32;
+      const f16x8* sx = xbuf(xb) + h * SEGP;
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx) tap(sw, sx, SEGP, kx);
+    };
     // K ranges: [t0, t1) of this block (SPLIT: one range), range length R steps
     int t0 = 0, t1 = T, R = T;
     if constexpr (SPLIT || RANGED) {
+      // PPS == 2: the host checks that every range has an even number of pairs
       const int pps = (a.pairs + a.ksplit - 1) / a.ksplit;
-      R = pps * KS;
+      R = pps / PPS * KS;
       if constexpr (SPLIT) {
         t0 = ks_i * R;
-        t1 = min(a.pairs, (ks_i + 1) * pps) * KS;
+        t1 = min(a.pairs, (ks_i + 1) * pps) / PPS * KS;
       }
     }
     f32x16 tot[RANGED ? WM : 1][RANGED ? WN : 1];
-    issue_w(t0, 0);
-    load_x(t0);
-    store_x(0);
-    __syncthreads();
-    for (int t = t0; t < t1; ++t) {
-      const int buf = (t - t0) & 1;
-      if (t + 1 < t1) {
-        issue_w(t + 1, buf ^ 1);
-        load_x(t + 1);
-      }
-      compute(buf);
+    auto range_end = [&](int t) __attribute__((always_inline)) {
       if constexpr (RANGED) {
         // end of a range: its sum (from zero) joins the total, ranges in order
         if (t + 1 == t1 || (t + 1) % R == 0) {
@@ -735,9 +768,132 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
             }
         }
       }
+    };
+    if constexpr (DEEP) {
+      // Role split (as the row union's): loader waves [0, NL) register-stage the input runs
+      // two steps ahead and write the split run of step t + 1 at the end of step t; DMA
+      // waves [NL, NWAVES) stream the weight slabs two steps ahead into a ring of three.
+      // No wave does both, so hipcc never drains a loader's loads in front of its LDS
+      // writes (the LDS-DMA aliasing rule); the DMA waves wait with a counted vmcnt, and the
+      // block meets at a raw s_barrier (__syncthreads would drain every DMA in flight).
+      constexpr int NL = NWAVES / 2, ND = NWAVES - NL;
+      constexpr int NP = WSLAB / 64, DPW = (NP + ND - 1) / ND;     // weight pieces, per DMA wave
+      constexpr int ITL = (2 * SEGMAX + NL * 64 - 1) / (NL * 64);   // staging items per loader thread
+      const bool loader = wave_u < NL;
+      int lih[ITL], lpx[ITL];
+#pragma unroll
+      for (int k = 0; k < ITL; ++k) {
+        const int it = tid + k * NL * 64;
+        lih[k] = min(it / seg, 1);
+        lpx[k] = loader && it < 2 * seg ? it - lih[k] * seg : -1;
+      }
+      f32x4 rs[2][ITL][2];                                          // two register slots
+      auto dload = [&](int t, int sl) __attribute__((always_inline)) {
+        const int c2 = t / KS, ky = t - c2 * KS;
+        const long long row = (long long)(La + (ky - P) * Wi - P);
+#pragma unroll
+        for (int k = 0; k < ITL; ++k) {
+          // a missing odd chunk stages the last real one (its packed weights are zero)
+          const int c = min(2 * c2 + lih[k], a.cin_chunks - 1);
+          if (lpx[k] >= 0) {
+            const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + lpx[k]) * 8;
+            rs[sl][k][0] = *(const f32x4*)src;
+            rs[sl][k][1] = *(const f32x4*)(src + 4);
+          }
+        }
+      };
+      auto dstore = [&](int xb, int sl) __attribute__((always_inline)) {
+        f16x8* sx = xbuf(xb);
+#pragma unroll
+        for (int k = 0; k < ITL; ++k) {
+          if (lpx[k] < 0) continue;
+          f16x8 hi, lo;
+          x3_split8(rs[sl][k][0], rs[sl][k][1], hi, lo);
+          sx[(0 * 2 + lih[k]) * SEGP + lpx[k]] = hi;
+          sx[(1 * 2 + lih[k]) * SEGP + lpx[k]] = lo;
+        }
+      };
+      auto dissue = [&](int t, int wb) __attribute__((always_inline)) {
+        const f16x8* src = HALFCO ? a.wpk + ((size_t)(co_t >> 1) * T + t) * (2 * WSLAB) + (co_t & 1) * 64
+                                  : a.wpk + ((size_t)co_t * T + t) * WSLAB;
+        f16x8* dst = wbuf(wb);
+#pragma unroll
+        for (int k = 0; k < DPW; ++k) {
+          // every DMA wave issues DPW pieces (a spare repeats the last piece: the same bytes
+          // to the same place), so the counted wait below is exact
+          const int q = min((wave_u - NL) * DPW + k, NP - 1);
+          __builtin_amdgcn_global_load_lds((const void*)(src + q * (HALFCO ? 128 : 64) + lane),
+                                           (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
+        }
+      };
+      // the whole loop once per role (ROLE: the loader's), so hipcc's wait-count pass never
+      // merges a DMA in flight into a loader's path (it would drain before its LDS writes)
+      auto run = [&](auto role) __attribute__((always_inline)) {
+        constexpr bool LOADER = decltype(role)::value;
+        // this wave's DMA of the next step has landed (`later`: one more step of pieces may
+        // stay in flight), its LDS writes are done, then the block barrier
+        auto wait_barrier = [&](bool later) __attribute__((always_inline)) {
+          if constexpr (!LOADER) {
+            if (later) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(DPW) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        const bool two = t0 + 1 < t1;
+        if constexpr (LOADER) {
+          dload(t0, 0);
+          if (two) dload(t0 + 1, 1);
+          dstore(0, 0);
+        } else {
+          dissue(t0, 0);
+          if (two) dissue(t0 + 1, 1);
+        }
+        wait_barrier(two);
+        // step t (i = t - t0): weights in ring buffer i % 3, input in buffer i & 1 from
+        // register slot i & 1; it stages step t + 2 into what step t - 1 used
+        auto step = [&](int t, int sl) __attribute__((always_inline)) {
+          const int i = t - t0;
+          const bool pre = t + 2 < t1;
+          if (pre) {
+            if constexpr (LOADER) dload(t + 2, sl);
+            else dissue(t + 2, (i + 2) % 3);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          compute_deep(i % 3, sl);
+          range_end(t);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (LOADER) {
+            if (t + 1 < t1) dstore(sl ^ 1, sl ^ 1);
+          }
+          wait_barrier(pre);
+        };
+        for (int t = t0; t < t1; t += 2) {
+          step(t, 0);
+          if (t + 1 < t1) step(t + 1, 1);
+        }
+      };
+      if (loader) run(std::true_type{});
+      else run(std::false_type{});
+    } else {
+    issue_w(t0, 0);
+    load_x(t0);
+    store_x(0);
+    __syncthreads();
+    for (int t = t0; t < t1; ++t) {
+      const int buf = (t - t0) & 1;
+      if (t + 1 < t1) {
+        issue_w(t + 1, buf ^ 1);
+        load_x(t + 1);
+      }
+      compute(buf);
+      range_end(t);
       if constexpr (SIB) __syncthreads();         // every wave is done with the one input buffer
       if (t + 1 < t1) store_x(buf ^ 1);
       __syncthreads();
+    }
     }
     if constexpr (RANGED) {
 #pragma unroll
@@ -1064,7 +1220,8 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   constexpr int SEGCAP = x3_segmax(BPX);
   constexpr bool SPLIT = (VAR & 2048) != 0, RANGED = (VAR & 1024) != 0;
   if (c.in_pad < P) { set_error("conv_x3: input ring narrower than kernel radius"); return hipErrorInvalidValue; }
-  if (c.bco != BCO) { set_error("conv_x3: tile mismatch"); return hipErrorInvalidValue; }
+  constexpr bool HALFCO = (VAR & 256) != 0;
+  if (c.bco != (HALFCO ? 2 * BCO : BCO)) { set_error("conv_x3: tile mismatch"); return hipErrorInvalidValue; }
   if ((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 7) { set_error("conv_x3: slice not on a chunk"); return hipErrorInvalidValue; }
   if (!c.wx3 || !c.range_flag) { set_error("conv_x3: split weights / range flag missing"); return hipErrorInvalidValue; }
   if ((SPLIT || RANGED) && c.ksplit < 2) { set_error("conv_x3: K ranges without a range count"); return hipErrorInvalidValue; }
@@ -1097,7 +1254,7 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   a.wscale_inv = c.wscale_inv;
   a.in_pad = c.in_pad; a.out_pad = c.out_pad;
   a.H = c.H; a.W = c.W; a.cin_chunks = c.cin_chunks; a.pairs = (c.cin_chunks + 1) / 2; a.cout = c.cout;
-  a.co_tiles = (c.cout + BCO - 1) / BCO;
+  a.co_tiles = HALFCO ? 2 * ((c.cout + 2 * BCO - 1) / (2 * BCO)) : (c.cout + BCO - 1) / BCO;
   a.tpx = tile_pixels(c, BPX, SEGCAP);
   if (c.hpool && (a.tpx & 1)) --a.tpx;          // pair-max epilogue: tiles start on even pixels
   a.px_tiles = (c.H * c.W + a.tpx - 1) / a.tpx;
@@ -1160,6 +1317,34 @@ static int device_cus() {
 // scale) sum their chunk pairs in S ranges, so that a batch-1 frame can spread them
 // over S blocks (split-K) and a large batch can keep them in one block, with the same
 // bits.  Every range is ceil(pairs / S) pairs long and non-empty.
+// Small grids (the 128-pixel family) with 128-channel tiles on two 64-channel blocks of 4
+// waves each (VAR 256).  ISLPOSE_X3_HALFCO=0|1 (read per launch; A/B).
+static bool x3_halfco(const ConvLaunch& c) {
+  const char* e = getenv("ISLPOSE_X3_HALFCO");
+  return e && e[0] == '1' && c.ks <= 7 && !c.fold;
+}
+
+// Small grids (the 128-pixel family) with the inputs and weights prefetched two K steps
+// ahead (VAR 128).  ISLPOSE_X3_DEEP=0|1 (read per launch; A/B).
+static bool x3_deep(const ConvLaunch& c) {
+  const char* e = getenv("ISLPOSE_X3_DEEP");
+  return e && e[0] == '1' && c.ks <= 3 && !c.fold && !c.vin && (c.bco == 128 || c.bco == 96);
+}
+
+static int x3_canonical_ranges(const ConvLaunch& c);
+
+// Small grids (the 128-pixel family) with two chunk pairs per K step (VAR 4096): a step's
+// MFMAs double against its one L2 round trip and one barrier.  Needs an even number of pairs
+// in every K range (the canonical ranges of the layer shape, or the whole K).
+// ISLPOSE_X3_PPS2=0|1 (read per launch; A/B).
+static bool x3_pps2(const ConvLaunch& c) {
+  const char* e = getenv("ISLPOSE_X3_PPS2");
+  if (!(e && e[0] == '1') || c.ks > 3 || c.fold || c.vin || (c.bco != 128 && c.bco != 96)) return false;
+  const int pairs = (c.cin_chunks + 1) / 2, S = c.ksplit > 1 ? c.ksplit : 1;
+  const int pps = (pairs + S - 1) / S;
+  return pairs % 2 == 0 && pps % 2 == 0;
+}
+
 static int x3_canonical_ranges(const ConvLaunch& c) {
   const int pairs = (c.cin_chunks + 1) / 2;
   if (!c.allow_split || c.H * c.W > 1024 || pairs < 4) return 1;
@@ -1401,6 +1586,39 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
           set_error("conv_x3: fold without a variant (x3_fold_ok)");
           return hipErrorInvalidValue;
         }
+      }
+      if constexpr (KS <= 3) {
+        if (x3_deep(c)) {   // prefetch two K steps ahead
+          switch (c.bco) {
+            case 128:
+              if (split) return launch_t<KS, 2, 4, 2, 1, 2048 | 128, 1>(c, s);
+              if (ranged) return launch_t<KS, 2, 4, 2, 1, 1024 | 128, 1>(c, s);
+              return launch_t<KS, 2, 4, 2, 1, 128, 1>(c, s);
+            case 96:
+              if (split) return launch_t<KS, 3, 4, 1, 1, 2048 | 128, 1>(c, s);
+              if (ranged) return launch_t<KS, 3, 4, 1, 1, 1024 | 128, 1>(c, s);
+              return launch_t<KS, 3, 4, 1, 1, 128, 1>(c, s);
+          }
+        }
+      }
+      if constexpr (KS <= 3) {
+        if (x3_pps2(c)) {   // two chunk pairs per K step: twice the MFMAs between barriers
+          switch (c.bco) {
+            case 128:
+              if (split) return launch_t<KS, 2, 4, 2, 1, 2048 | 4096, 2>(c, s);
+              if (ranged) return launch_t<KS, 2, 4, 2, 1, 1024 | 4096, 2>(c, s);
+              return launch_t<KS, 2, 4, 2, 1, 4096, 2>(c, s);
+            case 96:
+              if (split) return launch_t<KS, 3, 4, 1, 1, 2048 | 4096, 2>(c, s);
+              if (ranged) return launch_t<KS, 3, 4, 1, 1, 1024 | 4096, 2>(c, s);
+              return launch_t<KS, 3, 4, 1, 1, 4096, 2>(c, s);
+          }
+        }
+      }
+      if (c.bco == 128 && x3_halfco(c)) {   // two blocks of 4 waves (64co x 32px) per 128-channel tile
+        if (split) return launch_t<KS, 1, 4, 2, 1, 2048 | 256, 4>(c, s);
+        if (ranged) return launch_t<KS, 1, 4, 2, 1, 1024 | 256, 4>(c, s);
+        return launch_t<KS, 1, 4, 2, 1, 256, 4>(c, s);
       }
       switch (c.bco) {
         case 128:   // 8 waves of 64co x 32px

@@ -797,10 +797,12 @@ static bool pool_into_next_conv(const isl_net* net, size_t k) {
   return true;
 }
 
-// ISLPOSE_X3_FOLD=0: every split-K producer runs its x3_splitk_reduce launch (A/B; read per run)
+// ISLPOSE_X3_FOLD=1: split-K producers leave their partials to folding consumers (A/B; read
+// per run).  Off by default: at batch 1 (Mode R) the consumers' staging re-reads S partials
+// per element and kernel row, and the frame ran 427 -> 315 frames/s (profiles/r03/fold_ab/)
 static bool fold_enabled() {
   const char* e = getenv("ISLPOSE_X3_FOLD");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 // The conv launch of op k before the per-run adjustments (pools, wide 1x1 tiles, fold)
@@ -827,7 +829,8 @@ static ConvLaunch basic_launch(const isl_net* net, const Op& op) {
 // Same bits: the consumer's staging performs the reduce's arithmetic.
 static int plan_fold(isl_net* net, hipStream_t s) {
   isl_net::Arena& ar = *net->cur;
-  const int mode = (net->algo == ISL_ALGO_X3 && net->split_k > 0 && fold_enabled()) ? 1 : 0;
+  // the plan depends on the batch size and on the K-range mode (which layers split)
+  const int mode = (net->algo == ISL_ALGO_X3 && fold_enabled()) ? net->split_k : 0;
   if (ar.fold_n == net->pn && ar.fold_mode == mode) return ISL_OK;
   const size_t nops = net->ops.size();
   ar.fold_ws_off.assign(nops, -1);

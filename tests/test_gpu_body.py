@@ -446,8 +446,9 @@ def test_splitk_fold_bit_identical(net25, n, h, w, monkeypatch):
     (ConvLaunch::fold, no x3_splitk_reduce launch) give the same bits as the reduce launch
     (ISLPOSE_X3_FOLD=0): the staging performs the reduce's arithmetic.  At batch 1-2 and
     Mode R's 184x328 input, the 23x41 stage layers split across blocks and fold (asserted
-    through isl_net_op_info)."""
+    through isl_net_op_info).  The fold is an A/B switch (ISLPOSE_X3_FOLD=1), off by default."""
     x = torch.from_numpy(_inputs(n, h, w, seed=3 * h + n)).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_FOLD", "1")
     paf1, heat1 = net25.forward(x)
     torch.cuda.synchronize()
     var = [rt.decode_variant(v) for _, v in net25.op_variants()]
@@ -459,3 +460,43 @@ def test_splitk_fold_bit_identical(net25, n, h, w, monkeypatch):
     var0 = [rt.decode_variant(v) for _, v in net25.op_variants()]
     assert not any(v.get("fold") or v.get("fold_out") for v in var0)
     assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
+
+
+@pytest.mark.parametrize("n", [1, 32])
+def test_x3_halfco_small_grids_bit_identical(net25, n, monkeypatch):
+    """Small grids (Mode R's 23x41 stage layers: canonical K ranges in one block at batch
+    32, across blocks at batch 1) on two 64-channel blocks per 128-channel tile (VAR 256,
+    ISLPOSE_X3_HALFCO=1): every output channel's sum is the same sequence of MFMAs, so the
+    maps are bit-identical to the 128-channel blocks'."""
+    x = torch.from_numpy(_inputs(n, 184, 328, seed=91 + n)).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_HALFCO", "0")
+    paf0, heat0 = net25.forward(x)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("ISLPOSE_X3_HALFCO", "1")
+    paf1, heat1 = net25.forward(x)
+    torch.cuda.synchronize()
+    var = [rt.decode_variant(v) for _, v in net25.op_variants()]
+    assert sum(1 for v in var if v.get("var", 0) & 256) >= 40
+    assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
+
+
+def test_x3_pps2_small_grids(net25, w25, monkeypatch):
+    """Small grids with two chunk pairs per K step (VAR 4096 on the 128-pixel family,
+    ISLPOSE_X3_PPS2=1): a frame's maps are still batch-invariant (the canonical K ranges
+    keep their pair boundaries; batch 20 in-block == each frame alone across blocks, bit for
+    bit), within 1e-5 of the one-pair steps (another fp32 order), within the 1e-4 bar of the
+    oracle; the 23x41 stage layers take the variant (isl_net_op_info)."""
+    frames = _inputs(20, 184, 328, seed=77)
+    monkeypatch.setenv("ISLPOSE_X3_PPS2", "1")
+    paf, heat = net25.forward(torch.from_numpy(frames).cuda())
+    var = [rt.decode_variant(v) for _, v in net25.op_variants()]
+    assert sum(1 for v in var if v.get("pairs2") and v.get("bpx") == 128) >= 60
+    for i in (0, 7, 19):
+        p1, h1 = net25.forward(torch.from_numpy(frames[i:i + 1]).cuda())
+        assert torch.equal(p1[0], paf[i]) and torch.equal(h1[0], heat[i]), i
+    monkeypatch.setenv("ISLPOSE_X3_PPS2", "0")
+    p0, h0 = net25.forward(torch.from_numpy(frames).cuda())
+    torch.cuda.synchronize()
+    assert _rel(paf.cpu().numpy(), p0.cpu().numpy()) < 1e-5 and _rel(heat.cpu().numpy(), h0.cpu().numpy()) < 1e-5
+    rp, rh = cpu_ref.make_net_fn("body25", w25)(frames[:1])
+    assert _rel(paf[:1].cpu().numpy(), rp) < TOL and _rel(heat[:1].cpu().numpy(), rh) < TOL

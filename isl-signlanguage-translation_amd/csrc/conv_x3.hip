@@ -89,6 +89,7 @@ struct X3Args {
   int hpool;                    // ConvLaunch::hpool: out is the [n][chunk][H][W/2][8] pair-max buffer
   int vin;                      // ConvLaunch::vin: in is the [n][chunk][2H][W][8] pair-max buffer of a pool
   const X3Fold* fold;           // VAR 8192: per input chunk, the split-K partials it is folded from
+  int abl;                      // development (-DISLPOSE_DEV, ISLPOSE_X3_ABL): generic-loop ablations
 };
 
 // u / d for 0 <= u < 2^20, d >= 1, through the fp32 reciprocal r = 1/d: (u + 0.5) / d sits
@@ -882,17 +883,24 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     load_x(t0);
     store_x(0);
     __syncthreads();
+#ifdef ISLPOSE_DEV
+    // timing-only ablations (tools/convbench, ISLPOSE_X3_ABL bits): 1 no compute, 2 no input
+    // staging, 4 no weight DMA, 8 no barrier -- wrong results, development build only
+    const int abl = a.abl;
+#else
+    constexpr int abl = 0;
+#endif
     for (int t = t0; t < t1; ++t) {
       const int buf = (t - t0) & 1;
       if (t + 1 < t1) {
-        issue_w(t + 1, buf ^ 1);
-        load_x(t + 1);
+        if (!(abl & 4)) issue_w(t + 1, buf ^ 1);
+        if (!(abl & 2)) load_x(t + 1);
       }
-      compute(buf);
+      if (!(abl & 1)) compute(buf);
       range_end(t);
       if constexpr (SIB) __syncthreads();         // every wave is done with the one input buffer
-      if (t + 1 < t1) store_x(buf ^ 1);
-      __syncthreads();
+      if (t + 1 < t1 && !(abl & 2)) store_x(buf ^ 1);
+      if (!(abl & 8)) __syncthreads();
     }
     }
     if constexpr (RANGED) {
@@ -1228,7 +1236,7 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   if (SPLIT && !c.ws) { set_error("conv_x3: split-K without workspace"); return hipErrorInvalidValue; }
   if ((VAR & 16384) && !c.dbg) { set_error("conv_x3: stamp build without a stamp buffer"); return hipErrorInvalidValue; }
   if ((VAR & 4096) && ((c.cin_chunks + 1) / 2) % 2) { set_error("conv_x3: two pairs per step needs an even pair count"); return hipErrorInvalidValue; }
-  X3Args a;
+  X3Args a{};
   a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
   if (c.vin) {   // the pool's pair-max buffer: [n][chunk][2H][W][8], unpadded
     if (c.in_coff) { set_error("conv_x3: pooled-input staging reads whole buffers"); return hipErrorInvalidValue; }
@@ -1242,6 +1250,11 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   }
   a.vin = c.vin;
   a.fold = c.fold;
+#ifdef ISLPOSE_DEV
+  a.abl = getenv("ISLPOSE_X3_ABL") ? atoi(getenv("ISLPOSE_X3_ABL")) : 0;
+#else
+  a.abl = 0;
+#endif
   if ((c.fold != nullptr) != ((VAR & 8192) != 0)) { set_error("conv_x3: fold variant mismatch"); return hipErrorInvalidValue; }
   if (c.vin != ((VAR & 32768) != 0)) { set_error("conv_x3: pooled-input variant mismatch"); return hipErrorInvalidValue; }
   a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
@@ -1331,16 +1344,25 @@ static bool x3_deep(const ConvLaunch& c) {
   return e && e[0] == '1' && c.ks <= 3 && !c.fold && !c.vin && (c.bco == 128 || c.bco == 96);
 }
 
-static int x3_canonical_ranges(const ConvLaunch& c);
-
 // Small grids (the 128-pixel family) with two chunk pairs per K step (VAR 4096): a step's
-// MFMAs double against its one L2 round trip and one barrier.  Needs an even number of pairs
-// in every K range (the canonical ranges of the layer shape, or the whole K).
-// ISLPOSE_X3_PPS2=0|1 (read per launch; A/B).
+// MFMAs double against its barrier and its L2 round trip.  Only for layers with canonical K
+// ranges (they never run the big-tile kernels, whose one-pair order the other layers must
+// keep for batch-invariant bits), an even number of pairs in every range, and one channel
+// tile (c512 lost 7 %).  Per layer (tools/convbench, 23x41 at batch 32) c128 -3 %, c96 -8 %,
+// c384 / c288 -1.5 % time, but the whole of Mode R moved by +-1 % (batch 32 +0.5 %, batch 1
+// -1.2 %, profiles/r03/pps2_ab/), so it is off by default.  ISLPOSE_X3_PPS2=1: on (A/B; read
+// per launch).
+static int x3_canonical_ranges(const ConvLaunch& c);
 static bool x3_pps2(const ConvLaunch& c) {
+  // the fold A/B (ISLPOSE_X3_FOLD=1) runs its consumers on one-pair steps, so every layer of a
+  // frame keeps one order at every batch size only with PPS2 off there
   const char* e = getenv("ISLPOSE_X3_PPS2");
-  if (!(e && e[0] == '1') || c.ks > 3 || c.fold || c.vin || (c.bco != 128 && c.bco != 96)) return false;
-  const int pairs = (c.cin_chunks + 1) / 2, S = c.ksplit > 1 ? c.ksplit : 1;
+  const char* f = getenv("ISLPOSE_X3_FOLD");
+  if (!(e && e[0] == '1') || (f && f[0] == '1') || c.ks > 3 || c.vin || (c.bco != 128 && c.bco != 96) ||
+      c.cout > c.bco)
+    return false;
+  const int S = x3_canonical_ranges(c), pairs = (c.cin_chunks + 1) / 2;
+  if (S < 2 || c.ksplit != S) return false;
   const int pps = (pairs + S - 1) / S;
   return pairs % 2 == 0 && pps % 2 == 0;
 }

@@ -448,6 +448,9 @@ def test_splitk_fold_bit_identical(net25, n, h, w, monkeypatch):
     Mode R's 184x328 input, the 23x41 stage layers split across blocks and fold (asserted
     through isl_net_op_info).  The fold is an A/B switch (ISLPOSE_X3_FOLD=1), off by default."""
     x = torch.from_numpy(_inputs(n, h, w, seed=3 * h + n)).cuda()
+    # fold consumers run one-pair steps; the reference run must too (two-pair steps sum
+    # in another order)
+    monkeypatch.setenv("ISLPOSE_X3_PPS2", "0")
     monkeypatch.setenv("ISLPOSE_X3_FOLD", "1")
     paf1, heat1 = net25.forward(x)
     torch.cuda.synchronize()
@@ -469,6 +472,7 @@ def test_x3_halfco_small_grids_bit_identical(net25, n, monkeypatch):
     ISLPOSE_X3_HALFCO=1): every output channel's sum is the same sequence of MFMAs, so the
     maps are bit-identical to the 128-channel blocks'."""
     x = torch.from_numpy(_inputs(n, 184, 328, seed=91 + n)).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_PPS2", "0")   # it takes precedence over the half tiles
     monkeypatch.setenv("ISLPOSE_X3_HALFCO", "0")
     paf0, heat0 = net25.forward(x)
     torch.cuda.synchronize()

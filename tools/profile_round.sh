@@ -3,7 +3,7 @@
 # usage: bash tools/profile_round.sh <tag>      (outputs under gpurun_out/<tag>)
 export TMPDIR=/tmp
 T=${1:-r2p}; O=gpurun_out/$T; mkdir -p $O
-B="python3 bench.py --no-cpu --e2e-steps 0 --steps 3 --warmup 1"
+B="python3 bench.py --no-cpu --no-mode-r --e2e-steps 0 --steps 3 --warmup 1"
 timeout -k 10 300 python3 bench.py > $O/bench.json 2> $O/bench.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $B > $O/trace.log 2>&1 &&
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- $B > $O/fetch.log 2>&1 &&

@@ -440,6 +440,36 @@ def test_x3_m16_union_vs_oracle(net25, w25, monkeypatch):
         assert _rel(paf1[f:f + 1].cpu().numpy(), rp) < TOL and _rel(heat1[f:f + 1].cpu().numpy(), rh) < TOL
 
 
+@pytest.mark.parametrize("n,h,w", [(32, 368, 656), (12, 368, 656), (9, 376, 664)])
+def test_x3_t16_union_vs_oracle(net25, w25, monkeypatch, n, h, w):
+    """The row union on v_mfma_f32_16x16x32_f16 with two taps per K32 block (VAR 64,
+    ISLPOSE_X3_T16=1: [kx0 | kx1] of every (pair, ky) step, the kx2 taps of consecutive steps
+    paired, across the pair boundary at every third step): the 46x82 and 92x164 3x3 layers with
+    128-channel tiles take it (asserted through isl_net_op_info), including the pooled-input
+    and pair-max-epilogue forms; the maps stay within 1e-5 of the 32x32x16 kernel's (the same
+    sums in another fp32 order) and within the 1e-4 bar of the oracle."""
+    x = _inputs(n, h, w, seed=4243 + n)
+    xt = torch.from_numpy(x).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_T16", "0")
+    paf0, heat0 = net25.forward(xt)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("ISLPOSE_X3_T16", "1")
+    paf1, heat1 = net25.forward(xt)
+    torch.cuda.synchronize()
+    var = {name: rt.decode_variant(v) for name, v in net25.op_variants()}
+    t16 = [k for k, v in var.items() if v.get("t16")]
+    if n == 32:
+        assert "conv3_2" in t16 and "conv4_1" in t16 and "Mconv2_stage1_L2_1" in t16, t16
+        assert var["conv4_1"]["vin"] and "conv3_4" in t16, t16
+    assert t16 and all(var[k]["bco"] == 128 and var[k]["union"] for k in t16)
+    assert _rel(paf1.cpu().numpy(), paf0.cpu().numpy()) < 1e-5
+    assert _rel(heat1.cpu().numpy(), heat0.cpu().numpy()) < 1e-5
+    fn = cpu_ref.make_net_fn("body25", w25)
+    for f in (0, n - 1):
+        rp, rh = fn(x[f:f + 1])
+        assert _rel(paf1[f:f + 1].cpu().numpy(), rp) < TOL and _rel(heat1[f:f + 1].cpu().numpy(), rh) < TOL
+
+
 @pytest.mark.parametrize("n,h,w", [(1, 184, 328), (2, 184, 328), (1, 184, 200)])
 def test_splitk_fold_bit_identical(net25, n, h, w, monkeypatch):
     """Split-K producers whose partial sums the consumers fold into their staging

@@ -170,17 +170,11 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   // beside the double-buffered weight slabs (7x7 on 384 pixels: the 56 KiB slab per step
   // is amortised over 1.5x the pixels)
   constexpr bool SIB = (VAR & 65536) != 0;
-  // VAR 64: the row union on v_mfma_f32_16x16x32_f16 with two TAPS per K32 block (the x3
-  // fragments reused as in the 32x32x16 loop; see the T16 loop below)
-  constexpr bool T16 = (VAR & 64) != 0;
-  static_assert(!T16 || (UNION && !M16 && KS == 3 && WAVES_M == 2 && WAVES_N == 8 && WM == 2 && WN == 2),
-                "tap-pair 16x16x32 form: the 128-channel row-union block (16 waves of 64co x 64px)");
-  constexpr int SEGUP = T16 ? (x3_segu_max() + 1 + 15) / 16 * 16 : x3_segu_max() + 1;   // + dummy slot
+  constexpr int SEGUP = x3_segu_max() + 1;       // + dummy slot
   constexpr int XSLABU = 2 * 2 * SEGUP;          // [hi|lo][h][px]
   constexpr int SMEM = UNION ? 2 * WSLAB + 2 * XSLABU : SIB ? 2 * WSLAB + XSLAB
                      : (VAR & 128) ? 3 * WSLAB + 2 * XSLAB : 2 * BUF;
   static_assert(!(SIB && UNION), "one input buffer: generic loop only");
-  static_assert(!T16 || SMEM * 16 == (6 * 4 * BCO + 2 * XSLABU) * 16, "T16: weight buffers of 2 + 4 taps");
   static_assert(SMEM * 16 <= 160 * 1024, "LDS");
   constexpr bool RANGED = (VAR & 1024) != 0;
   constexpr bool SPLIT = (VAR & 2048) != 0;
@@ -279,256 +273,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       }
   };
 
-  if constexpr (T16) {
-    // Row union on v_mfma_f32_16x16x32_f16, two taps per K32 block.
-    // A 16x16 (co x px) block's lane carries K group g = lane >> 4: chunk g & 1 of the pair at
-    // tap slot g >> 1, so one K32 block is two taps x 16 channels and the three split
-    // products keep the 32x32x16 loop's fragment reuse -- per block and wave 8 A + 8 B
-    // fragment reads for 48 MFMAs (4 co x 4 px blocks x hi.hi, hi.lo, lo.hi), the same LDS
-    // bytes per FLOP, and no padded MFMA.
-    // Steps stay (pair, ky) with one barrier each; a step has 3 taps, so they alternate:
-    //   even step t: the block [kx0 | kx1] of (pair, ky);
-    //   odd step t:  the block [kx0 | kx1] of (pair, ky) and the block [kx2 of step t-1 | kx2
-    //                of step t] -- within a pair (ky 0+1, ky 1+2), or across the pair boundary
-    //                (ky 2 of an even pair + ky 0 of the next; pairs come in twos).
-    // Weights: the standard packing is tap-linear ([pair][ky][kx][hi|lo][h][BCO]), so an even
-    // step's slab is taps 3t, 3t+1 (16 KiB) and an odd step's taps 3t-1 .. 3t+2 (32 KiB), each
-    // one contiguous LDS-DMA by waves 12-15 one step ahead into its own buffer.
-    // Input: the 3-row union run of a pair, double-buffered, staged by waves 0-11 during the
-    // previous pair's steps in three parts stored at the step ends: part 0 = run positions
-    // [0, 2 Wi) of both chunks, part 1 / 2 = chunk 0 / 1 from 2 Wi on.  The cross-pair block of
-    // step 3q (q odd) still reads pair q-1's rows ky 2 (positions >= 2 Wi) while part 0 of pair
-    // q+1 lands in that buffer -- disjoint positions.
-    static_assert(NWAVES == 16, "role split sized for 16-wave blocks");
-    constexpr int LOADER_WAVES = 12, DMA_WAVES = NWAVES - LOADER_WAVES;
-    constexpr int TAPU = 4 * BCO;                               // one tap: [hi|lo][h][BCO] units
-    f16x8* const wb0 = smem;                                    // even steps: 2 taps
-    f16x8* const wb1 = smem + 2 * TAPU;                         // odd steps: 4 taps
-    f16x8* const xbase = smem + 6 * TAPU;                       // union runs: [pair & 1][hi|lo][h][px]
-    const bool loader = wave_u < LOADER_WAVES;
-    const int w2 = 2 * Wi;
-    const int segu = Lb - La + w2 + 3;                          // rows -1..+1 of the tile, one run
-    const int rest = segu - w2;
-    const long long ubase = (long long)La - Wi - 1;
-    // staging item of this thread in part k (uniform): chunk ih, run position px (-1: idle)
-    auto item = [&](int lt, int k, int& ih, int& px) __attribute__((always_inline)) {
-      if (k == 0) {
-        ih = lt >= w2 ? 1 : 0;
-        px = lt < 2 * w2 ? lt - ih * w2 : -1;
-      } else {
-        ih = k - 1;
-        px = lt < rest ? w2 + lt : -1;
-      }
-    };
-    f32x4 ru[2];
-    auto load_p = [&](int lt, int q, int k) __attribute__((always_inline)) {
-      int ih, px;
-      item(lt, k, ih, px);
-      if (px >= 0) {
-        // a missing odd chunk stages the last real chunk again: its packed weights are zero
-        const int c = min(2 * q + ih, a.cin_chunks - 1);
-        if constexpr (VIN) {
-          const int u = (int)ubase + px, yy = x3_div(u, inv_wi);
-          float4 l4, h4;
-          x3_vin_load(in_f + (size_t)c * a.in_chs, yy, u - yy * Wi, a, l4, h4);
-          ru[0] = f32x4{l4.x, l4.y, l4.z, l4.w};
-          ru[1] = f32x4{h4.x, h4.y, h4.z, h4.w};
-        } else {
-          const float* src = in_f + (size_t)c * a.in_chs + (size_t)(ubase + px) * 8;
-          ru[0] = *(const f32x4*)src;
-          ru[1] = *(const f32x4*)(src + 4);
-        }
-      }
-    };
-    auto store_p = [&](int lt, int q, int k) __attribute__((always_inline)) {
-      int ih, px;
-      item(lt, k, ih, px);
-      f16x8* sx = xbase + (q & 1) * XSLABU;
-      f16x8 hi, lo;
-      x3_split8(ru[0], ru[1], hi, lo);
-      if (px < 0) px = SEGUP - 1;                                // idle items: the dummy slot
-      sx[(0 * 2 + ih) * SEGUP + px] = hi;
-      sx[(1 * 2 + ih) * SEGUP + px] = lo;
-    };
-    // the weight slab of step t (parity ODD) into its buffer, by the DMA waves
-    auto issue = [&](int t, auto odd_) __attribute__((always_inline)) {
-      constexpr bool ODD = decltype(odd_)::value;
-      constexpr int NPC = (ODD ? 4 : 2) * TAPU / 64, PER = NPC / DMA_WAVES;
-      static_assert(NPC % DMA_WAVES == 0, "whole pieces per DMA wave");
-      const f16x8* src = a.wpk + ((size_t)co_t * T * KS + (ODD ? 3 * t - 1 : 3 * t)) * TAPU;
-      f16x8* dst = ODD ? wb1 : wb0;
-#pragma unroll
-      for (int k = 0; k < PER; ++k) {
-        const int q = (wave_u - LOADER_WAVES) * PER + k;
-        __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
-                                         (__attribute__((address_space(3))) void*)(dst + q * 64), 16, 0, 0);
-      }
-    };
-    const int g = lane >> 4, r16 = lane & 15, gh = g & 1, gs = g >> 1;
-    int rel16[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = min(m0 + wave_n * 64 + j * 16 + r16, mlast);
-      const int y = m / a.W, x = m - y * a.W;
-      rel16[j] = (y + a.in_pad) * Wi + x + a.in_pad - La;
-    }
-    f32x4 acc4[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc4[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // one K32 block: aw = this lane's hi A unit of co block 0 (lo at + 2 BCO), bx = its hi B
-    // plane (lo at + 2 SEGUP)
-    // Two passes keep the operands within the 4-waves-per-SIMD register budget: the hi B
-    // fragments with every A (hi.hi, lo.hi), then the lo B fragments with the hi A re-read
-    // (hi.lo): 20 fragment reads per 48 MFMAs instead of 16.  The A fragments are read one
-    // channel block ahead, fenced by sched_barriers: left free, hipcc hoists a whole block's
-    // 20 reads (80 VGPRs) above its MFMAs and spills.
-    auto block = [&](const f16x8* aw, const f16x8* bx) __attribute__((always_inline)) {
-      f16x8 B[4], Ah, Al;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) B[j] = bx[rel16[j]];
-      Ah = aw[0];
-      Al = aw[2 * BCO];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f16x8 Ahn, Aln;
-        if (i < 3) {
-          Ahn = aw[(i + 1) * 16];
-          Aln = aw[2 * BCO + (i + 1) * 16];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, B[j], acc4[i][j], 0, 0, 0);
-          acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Al, B[j], acc4[i][j], 0, 0, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        Ah = Ahn;
-        Al = Aln;
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) B[j] = bx[2 * SEGUP + rel16[j]];
-      Ah = aw[0];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        f16x8 Ahn;
-        if (i < 3) Ahn = aw[(i + 1) * 16];
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ah, B[j], acc4[i][j], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        Ah = Ahn;
-      }
-    };
-    const int alane = gh * BCO + wave_m * 64 + r16;              // + tap slot x TAPU
-    const f16x8* xlane = xbase + gh * SEGUP;                     // + (pair & 1) x XSLABU + offset
-    // prologue: weights of step 0, the whole union run of pair 0
-    if (!loader) issue(0, std::false_type{});
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      load_p(tid, 0, k);
-      store_p(tid, 0, k);
-    }
-    __syncthreads();
-    // step s (0..5) of the cycle of pairs c2 (even), c2 + 1
-    auto step = [&](int c2, auto s_) __attribute__((always_inline)) {
-      constexpr int s = decltype(s_)::value;
-      constexpr bool ODD = s & 1;
-      constexpr int ky = s % 3, pb = s / 3;                      // pair c2 + pb, union buffer pb
-      const int t = 3 * c2 + s;
-      if (!loader && t + 1 < T) issue(t + 1, std::integral_constant<bool, !ODD>{});
-      const int q = c2 + pb + 1;                                  // the pair staged now, part s % 3
-      const bool stage = loader && q < a.pairs;
-      // the lane's offsets, made opaque per step: every LDS address of a cycle's 9 blocks and 6
-      // staging parts is loop-invariant, and hoisting them all out of the pair loop spilled
-      int ao = alane, xo = 0, lt = tid;
-      asm volatile("" : "+v"(ao), "+v"(xo), "+v"(lt));
-      __builtin_amdgcn_sched_barrier(0);
-      if (!ODD && stage) load_p(lt, q, s % 3);
-      __builtin_amdgcn_sched_barrier(0);
-      // [kx0 | kx1] of (pair, ky): tap slots (ODD ? 1 : 0) + gs
-      block((ODD ? wb1 : wb0) + (ODD ? TAPU : 0) + ao + gs * TAPU,
-            xlane + pb * XSLABU + ky * Wi + xo + gs);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (ODD) {
-        if (stage) load_p(lt, q, s % 3);
-        __builtin_amdgcn_sched_barrier(0);
-        // [kx2 of step t-1 | kx2 of step t]: tap slots 0 / 3
-        constexpr int pbp = (s - 1) / 3, kyp = (s - 1) % 3;
-        block(wb1 + ao + gs * (3 * TAPU),
-              xlane + xo + pbp * XSLABU + kyp * Wi + 2 + gs * ((pb - pbp) * XSLABU + (ky - kyp) * Wi));
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (stage) store_p(lt, q, s % 3);
-      __syncthreads();
-    };
-    for (int c2 = 0; c2 < a.pairs; c2 += 2) {
-      step(c2, std::integral_constant<int, 0>{});
-      step(c2, std::integral_constant<int, 1>{});
-      step(c2, std::integral_constant<int, 2>{});
-      step(c2, std::integral_constant<int, 3>{});
-      step(c2, std::integral_constant<int, 4>{});
-      step(c2, std::integral_constant<int, 5>{});
-    }
-    // epilogue of the 16x16 blocks: lane = pixel r16 of block j, channels 4g..4g+3 of block i
-    const int Wo = a.hpool ? a.W / 2 : a.W + 2 * a.out_pad;
-    float* out_f = a.out + (size_t)n * a.out_fs;
-    bool bad = false;
-    float* ebias = (float*)smem;                  // [BCO] bias, [BCO] slope
-    for (int i = tid; i < BCO; i += NT) {         // the K loop ended on a barrier: LDS is free
-      ebias[i] = a.bias[co_t * BCO + i];
-      ebias[BCO + i] = a.act == ACT_PRELU ? a.slope[co_t * BCO + i] : 0.f;
-    }
-    __syncthreads();
-    // the epilogue's per-lane coordinates from an opaque lane index: hipcc otherwise computes
-    // them (loop-invariant) before the K loop and spills them across it
-    int le = lane;
-    asm volatile("" : "+v"(le));
-    const int er16 = le & 15, eg = le >> 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + wave_n * 64 + j * 16 + er16;
-      if (m > mlast) continue;
-      const int y = m / a.W, x = m - y * a.W;
-      float* op = a.hpool ? out_f + (size_t)(y * Wo + (x >> 1)) * 8
-                          : out_f + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int cl = wave_m * 64 + i * 16 + 4 * eg, co = co_t * BCO + cl;
-        const f32x4 b = *(const f32x4*)(ebias + cl);
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc4[i][j][e] * a.wscale_inv + b[e];
-        if (a.act == ACT_RELU) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-        } else if (a.act == ACT_PRELU) {
-          const f32x4 sl = *(const f32x4*)(ebias + BCO + cl);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bad |= !(__builtin_fabsf(v[e]) < 65504.f);
-        if (a.hpool) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            v[e] = fmaxf(v[e], __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v[e]), 0xB1, 0xF, 0xF, false)));
-          if (x & 1) continue;
-        }
-        float* oc = op + (size_t)(co >> 3) * a.out_chs + (co & 7);
-        if (co + 3 < a.cout) {
-          *(f32x4*)oc = v;
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (co + e < a.cout) oc[e] = v[e];
-        }
-      }
-    }
-    if (bad) atomicOr(a.range_flag, 1);
-    return;
-  } else if constexpr (M16) {
+  if constexpr (M16) {
     // Row union on v_mfma_f32_16x16x32_f16, two taps per K step.
     // Per 16x16 (co x px) block a lane carries K group g = lane >> 4 (8 fp16 values of
     // chunk g & 1 of the pair).  The three products of a tap fold into K:
@@ -1044,32 +789,36 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
         lpx[k] = loader && it < 2 * seg ? it - lih[k] * seg : -1;
       }
       f32x4 rs[2][ITL][2];                                          // two register slots
+      // Every load and store is unconditional (idle items read pixel 0 and write the dummy
+      // slot; past the last step the loads and DMAs repeat the last step's), so the number of
+      // vector-memory operations in flight is the same on every path and hipcc's wait-count
+      // pass keeps the younger slot's loads in flight (counted vmcnt) instead of draining them.
       auto dload = [&](int t, int sl) __attribute__((always_inline)) {
+        t = min(t, t1 - 1);
         const int c2 = t / KS, ky = t - c2 * KS;
         const long long row = (long long)(La + (ky - P) * Wi - P);
 #pragma unroll
         for (int k = 0; k < ITL; ++k) {
           // a missing odd chunk stages the last real one (its packed weights are zero)
           const int c = min(2 * c2 + lih[k], a.cin_chunks - 1);
-          if (lpx[k] >= 0) {
-            const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + lpx[k]) * 8;
-            rs[sl][k][0] = *(const f32x4*)src;
-            rs[sl][k][1] = *(const f32x4*)(src + 4);
-          }
+          const float* src = in_f + (size_t)c * a.in_chs + (size_t)(row + max(lpx[k], 0)) * 8;
+          rs[sl][k][0] = *(const f32x4*)src;
+          rs[sl][k][1] = *(const f32x4*)(src + 4);
         }
       };
       auto dstore = [&](int xb, int sl) __attribute__((always_inline)) {
         f16x8* sx = xbuf(xb);
 #pragma unroll
         for (int k = 0; k < ITL; ++k) {
-          if (lpx[k] < 0) continue;
           f16x8 hi, lo;
           x3_split8(rs[sl][k][0], rs[sl][k][1], hi, lo);
-          sx[(0 * 2 + lih[k]) * SEGP + lpx[k]] = hi;
-          sx[(1 * 2 + lih[k]) * SEGP + lpx[k]] = lo;
+          const int px = lpx[k] < 0 ? SEGP - 1 : lpx[k];
+          sx[(0 * 2 + lih[k]) * SEGP + px] = hi;
+          sx[(1 * 2 + lih[k]) * SEGP + px] = lo;
         }
       };
       auto dissue = [&](int t, int wb) __attribute__((always_inline)) {
+        t = min(t, t1 - 1);
         const f16x8* src = HALFCO ? a.wpk + ((size_t)(co_t >> 1) * T + t) * (2 * WSLAB) + (co_t & 1) * 64
                                   : a.wpk + ((size_t)co_t * T + t) * WSLAB;
         f16x8* dst = wbuf(wb);
@@ -1098,53 +847,52 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
           __builtin_amdgcn_s_barrier();
           __builtin_amdgcn_sched_barrier(0);
         };
-        const bool two = t0 + 1 < t1;
         if constexpr (LOADER) {
           dload(t0, 0);
-          if (two) dload(t0 + 1, 1);
+          dload(t0 + 1, 1);
           dstore(0, 0);
         } else {
           dissue(t0, 0);
-          if (two) dissue(t0 + 1, 1);
+          dissue(t0 + 1, 1);
         }
-        wait_barrier(two);
+        wait_barrier(true);
         // step t (i = t - t0): weights in ring buffer i % 3, input in buffer i & 1 from
         // register slot i & 1; it stages step t + 2 into what step t - 1 used
         auto step = [&](int t, int sl) __attribute__((always_inline)) {
           const int i = t - t0;
-          const bool pre = t + 2 < t1;
-          if (pre) {
-            if constexpr (LOADER) dload(t + 2, sl);
-            else dissue(t + 2, (i + 2) % 3);
-          }
+          if constexpr (LOADER) dload(t + 2, sl);
+          else dissue(t + 2, (i + 2) % 3);
           __builtin_amdgcn_sched_barrier(0);
           compute_deep(i % 3, sl);
           range_end(t);
           __builtin_amdgcn_sched_barrier(0);
-          if constexpr (LOADER) {
-            if (t + 1 < t1) dstore(sl ^ 1, sl ^ 1);
-          }
-          wait_barrier(pre);
+          if constexpr (LOADER) dstore(sl ^ 1, sl ^ 1);
+          wait_barrier(true);
         };
         for (int t = t0; t < t1; t += 2) {
           step(t, 0);
           if (t + 1 < t1) step(t + 1, 1);
         }
+        // the spare DMAs past the last step land before the epilogue reuses the LDS
+        wait_barrier(false);
       };
       if (loader) run(std::true_type{});
       else run(std::false_type{});
     } else {
-    issue_w(t0, 0);
-    load_x(t0);
-    store_x(0);
-    __syncthreads();
 #ifdef ISLPOSE_DEV
     // timing-only ablations (tools/convbench, ISLPOSE_X3_ABL bits): 1 no compute, 2 no input
-    // staging, 4 no weight DMA, 8 no barrier -- wrong results, development build only
+    // staging, 4 no weight DMA, 8 no barrier, 16 no prologue staging (the epilogue bits 32 / 64
+    // are read there) -- wrong results, development build only
     const int abl = a.abl;
 #else
     constexpr int abl = 0;
 #endif
+    if (!(abl & 16)) {
+      issue_w(t0, 0);
+      load_x(t0);
+      store_x(0);
+    }
+    __syncthreads();
     for (int t = t0; t < t1; ++t) {
       const int buf = (t - t0) & 1;
       if (t + 1 < t1) {
@@ -1201,10 +949,17 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   const int Wo = a.hpool ? a.W / 2 : a.W + 2 * a.out_pad;
   float* out_f = a.out + (size_t)n * a.out_fs;
   bool bad = false;
+#ifdef ISLPOSE_DEV
+  // ablations (tools/convbench, ISLPOSE_X3_ABL): 64 no epilogue at all, 32 no bias load
+  if (a.abl & 64) return;
+  const bool abl_bias = (a.abl & 32) != 0;
+#else
+  constexpr bool abl_bias = false;
+#endif
   float* ebias = (float*)smem;                  // [BCO] bias, [BCO] slope
   for (int i = tid; i < BCO; i += NT) {         // the K loop ended on a barrier: LDS is free
-    ebias[i] = a.bias[co_t * BCO + i];
-    ebias[BCO + i] = a.act == ACT_PRELU ? a.slope[co_t * BCO + i] : 0.f;
+    ebias[i] = abl_bias ? 0.f : a.bias[co_t * BCO + i];
+    ebias[BCO + i] = !abl_bias && a.act == ACT_PRELU ? a.slope[co_t * BCO + i] : 0.f;
   }
   __syncthreads();
 #pragma unroll
@@ -1474,8 +1229,6 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
   if (bad) atomicOr(a.range_flag, 1);
 }
 
-static int x3_union_run(const ConvLaunch& c);
-
 template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, int VAR, int OCC>
 static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   constexpr int BCO = WAVES_M * WM * 32;
@@ -1493,11 +1246,6 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   if (SPLIT && !c.ws) { set_error("conv_x3: split-K without workspace"); return hipErrorInvalidValue; }
   if ((VAR & 16384) && !c.dbg) { set_error("conv_x3: stamp build without a stamp buffer"); return hipErrorInvalidValue; }
   if ((VAR & 4096) && ((c.cin_chunks + 1) / 2) % 2) { set_error("conv_x3: two pairs per step needs an even pair count"); return hipErrorInvalidValue; }
-  if ((VAR & 64) && (((c.cin_chunks + 1) / 2) % 2 || 4 * (c.W + 2 * c.in_pad) > 768 ||
-                     x3_union_run(c) - 2 * (c.W + 2 * c.in_pad) > 768)) {
-    set_error("conv_x3: tap-pair 16x16x32 union needs an even pair count and staging parts of <= 768 items");
-    return hipErrorInvalidValue;
-  }
   X3Args a{};
   a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
   if (c.vin) {   // the pool's pair-max buffer: [n][chunk][2H][W][8], unpadded
@@ -1750,18 +1498,6 @@ static bool x3_m16(const ConvLaunch& c) {
   return on && c.ks == 3 && c.bco == 128 && ((c.cin_chunks + 1) / 2) % 2 == 0;
 }
 
-// The row union on v_mfma_f32_16x16x32_f16 with two taps per K32 block (VAR 64) for
-// 128-channel tiles with an even number of chunk pairs, whose staging parts fit the 12
-// loader waves (4 Wi and the run past row 1 each <= 768 items).  ISLPOSE_X3_T16=0|1 (read
-// per launch: A/B in one process).
-static bool x3_t16(const ConvLaunch& c) {
-  const char* e = getenv("ISLPOSE_X3_T16");
-  const bool on = e && e[0] == '1';
-  const int Wi = c.W + 2 * c.in_pad, pairs = (c.cin_chunks + 1) / 2;
-  return on && c.ks == 3 && c.bco == 128 && pairs >= 2 && pairs % 2 == 0 && 4 * Wi <= 768 &&
-         x3_union_run(c) - 2 * Wi <= 768;
-}
-
 // K-range plan of a launch on the 128-pixel family: S ranges, computed across S blocks
 // per tile (split-K, partials through the workspace) when the plain grid has fewer
 // blocks than CUs, else in one block (tools/gpu_across.sh: across wins 10-50 % at
@@ -1807,15 +1543,12 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
       }
 #endif
       const bool m16 = c.bco == 128 && x3_m16(c);
-      const bool t16 = c.bco == 128 && !m16 && x3_t16(c);
       if (c.vin) {
-        if (t16) return launch_t<KS, 2, 8, 2, 2, 512 | 32768 | 64, 4>(c, s);
         if (m16) return launch_t<KS, 2, 8, 2, 2, 512 | 32768 | 131072, 4>(c, s);
         if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 32768, 4>(c, s);
         set_error("conv_x3: pooled-input staging without a variant (x3_vin_ok)");
         return hipErrorInvalidValue;
       }
-      if (t16) return launch_t<KS, 2, 8, 2, 2, 512 | 64, 4>(c, s);
       if (m16) return launch_t<KS, 2, 8, 2, 2, 512 | 131072, 4>(c, s);
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 512, 4>(c, s);

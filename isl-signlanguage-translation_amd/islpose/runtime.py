@@ -187,7 +187,7 @@ def decode_variant(code: int) -> dict:
             "ks": 2 * ((code >> 29) & 3) + 1, "rgb": bool(code & (1 << 18)),
             "union": bool(code & 512), "ranged": bool(code & 1024), "split": bool(code & 2048),
             "pairs2": bool(code & 4096), "vin": bool(code & 32768), "sib": bool(code & 65536),
-            "fold": bool(code & 8192), "m16": bool(code & 131072), "t16": bool(code & 64), "fold_out": bool(code & (1 << 19))}
+            "fold": bool(code & 8192), "m16": bool(code & 131072), "fold_out": bool(code & (1 << 19))}
 
 
 class Net:

@@ -440,34 +440,24 @@ def test_x3_m16_union_vs_oracle(net25, w25, monkeypatch):
         assert _rel(paf1[f:f + 1].cpu().numpy(), rp) < TOL and _rel(heat1[f:f + 1].cpu().numpy(), rh) < TOL
 
 
-@pytest.mark.parametrize("n,h,w", [(32, 368, 656), (12, 368, 656), (9, 376, 664)])
-def test_x3_t16_union_vs_oracle(net25, w25, monkeypatch, n, h, w):
-    """The row union on v_mfma_f32_16x16x32_f16 with two taps per K32 block (VAR 64,
-    ISLPOSE_X3_T16=1: [kx0 | kx1] of every (pair, ky) step, the kx2 taps of consecutive steps
-    paired, across the pair boundary at every third step): the 46x82 and 92x164 3x3 layers with
-    128-channel tiles take it (asserted through isl_net_op_info), including the pooled-input
-    and pair-max-epilogue forms; the maps stay within 1e-5 of the 32x32x16 kernel's (the same
-    sums in another fp32 order) and within the 1e-4 bar of the oracle."""
-    x = _inputs(n, h, w, seed=4243 + n)
-    xt = torch.from_numpy(x).cuda()
-    monkeypatch.setenv("ISLPOSE_X3_T16", "0")
-    paf0, heat0 = net25.forward(xt)
+@pytest.mark.parametrize("n", [1, 2, 32])
+def test_x3_deep_small_grids_bit_identical(net25, n, monkeypatch):
+    """Small grids (Mode R's 23x41 stage layers on the 128-pixel family: canonical K ranges in
+    one block at batch 32, across blocks at batch 1-2) with inputs and weights staged two K
+    steps ahead (VAR 128, ISLPOSE_X3_DEEP=1: loader / DMA role split, unconditional loads so
+    the waits are counted, raw barriers) run the same MFMA sequence as the default loop:
+    bit-identical maps, with the stage layers on the variant (isl_net_op_info)."""
+    x = torch.from_numpy(_inputs(n, 184, 328, seed=600 + n)).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_PPS2", "0")
+    monkeypatch.setenv("ISLPOSE_X3_DEEP", "0")
+    paf0, heat0 = net25.forward(x)
     torch.cuda.synchronize()
-    monkeypatch.setenv("ISLPOSE_X3_T16", "1")
-    paf1, heat1 = net25.forward(xt)
+    monkeypatch.setenv("ISLPOSE_X3_DEEP", "1")
+    paf1, heat1 = net25.forward(x)
     torch.cuda.synchronize()
-    var = {name: rt.decode_variant(v) for name, v in net25.op_variants()}
-    t16 = [k for k, v in var.items() if v.get("t16")]
-    if n == 32:
-        assert "conv3_2" in t16 and "conv4_1" in t16 and "Mconv2_stage1_L2_1" in t16, t16
-        assert var["conv4_1"]["vin"] and "conv3_4" in t16, t16
-    assert t16 and all(var[k]["bco"] == 128 and var[k]["union"] for k in t16)
-    assert _rel(paf1.cpu().numpy(), paf0.cpu().numpy()) < 1e-5
-    assert _rel(heat1.cpu().numpy(), heat0.cpu().numpy()) < 1e-5
-    fn = cpu_ref.make_net_fn("body25", w25)
-    for f in (0, n - 1):
-        rp, rh = fn(x[f:f + 1])
-        assert _rel(paf1[f:f + 1].cpu().numpy(), rp) < TOL and _rel(heat1[f:f + 1].cpu().numpy(), rh) < TOL
+    var = [rt.decode_variant(v) for _, v in net25.op_variants()]
+    assert sum(1 for v in var if v.get("var", 0) & 128) >= 60
+    assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
 
 
 @pytest.mark.parametrize("n,h,w", [(1, 184, 328), (2, 184, 328), (1, 184, 200)])

@@ -102,10 +102,10 @@ int main(int argc, char** argv) {
         // x3m: the row union on 16x16x32 MFMAs (ISLPOSE_X3_M16=1, read per launch); x3: off
         // x3h: small grids on two 64-channel blocks per 128-channel tile (ISLPOSE_X3_HALFCO=1)
         // x3p: small grids with two chunk pairs per K step (ISLPOSE_X3_PPS2=1)
-        // x3t: the row union on 16x16x32 MFMAs with two taps per K32 block (ISLPOSE_X3_T16=1)
-        if (a == "x3" || a == "x3m" || a == "x3h" || a == "x3p" || a == "x3t") {
+        // x3d: small grids with inputs and weights two K steps ahead (ISLPOSE_X3_DEEP=1)
+        if (a == "x3" || a == "x3m" || a == "x3h" || a == "x3p" || a == "x3d") {
+          setenv("ISLPOSE_X3_DEEP", a == "x3d" ? "1" : "0", 1);
           setenv("ISLPOSE_X3_M16", a == "x3m" ? "1" : "0", 1);
-          setenv("ISLPOSE_X3_T16", a == "x3t" ? "1" : "0", 1);
           setenv("ISLPOSE_X3_HALFCO", a == "x3h" ? "1" : "0", 1);
           setenv("ISLPOSE_X3_PPS2", a == "x3p" ? "1" : "0", 1);
           c.bco = bco; c.wpk = wd;
@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       const double us = ms * 1e3 / iters;
-      const double fac = (a == "x3" || a == "x3m" || a == "x3h" || a == "x3p" || a == "x3t") ? 3.0 : a == "wx3" ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
+      const double fac = (a == "x3" || a == "x3m" || a == "x3h" || a == "x3p" || a == "x3d") ? 3.0 : a == "wx3" ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
       printf("  round %d %-7s %9.1f us  fp32-equiv %7.1f TF  alg-MFMA %7.1f TF\n", r, a.c_str(), us,
              flops / us / 1e6, fac * flops / us / 1e6);
     }

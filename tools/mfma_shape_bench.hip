@@ -116,6 +116,56 @@ __global__ void __launch_bounds__(NT, 4) loop16(const f16x8* g, float* out, int 
   out[blockIdx.x * NT + threadIdx.x] = v;
 }
 
+// loop32 variants for the power question (is the LDS traffic or the barrier what keeps the
+// conv's clock / MFMA issue down?): RD = re-read the fragments from LDS every RD-th
+// iteration only (RD = 1 is loop32), BAR = a __syncthreads every 3 iterations (one conv
+// step: 36 MFMAs per wave between barriers).
+template <int RD, bool BAR>
+__global__ void __launch_bounds__(NT, 4) var32(const f16x8* g, float* out, int iters, unsigned long long* clk) {
+  __shared__ f16x8 s[LDS_UNITS];
+  for (int i = threadIdx.x; i < LDS_UNITS; i += NT) s[i] = g[(blockIdx.x * 131 + i) % (4 * LDS_UNITS)];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  f32x16 acc[2][2] = {};
+  unsigned long long t0 = 0, r0 = 0;
+  if (threadIdx.x == 0) { t0 = __builtin_amdgcn_s_memtime(); r0 = __builtin_amdgcn_s_memrealtime(); }
+  int off = (wave * 64 + lane) & (LDS_UNITS / 2 - 1);
+  f16x8 A[2][2], B[2][2];
+  for (int it = 0; it < iters; ++it) {
+    if (it % RD == 0) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int hl = 0; hl < 2; ++hl) {
+          A[m][hl] = s[(off + m * 32 + hl * 1024) & (LDS_UNITS - 1)];
+          B[m][hl] = s[(off + m * 32 + hl * 1024 + 2048 + 7) & (LDS_UNITS - 1)];
+        }
+      off = (off + 64) & (LDS_UNITS / 2 - 1);
+    }
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], B[n][0], acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][0], B[n][1], acc[m][n], 0, 0, 0);
+        acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[m][1], B[n][0], acc[m][n], 0, 0, 0);
+      }
+    if (BAR && it % 3 == 2) __syncthreads();
+  }
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    clk[0] = __builtin_amdgcn_s_memtime() - t0;
+    clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v += acc[m][n][r];
+  out[blockIdx.x * NT + threadIdx.x] = v;
+}
+
 // One 3x3 (pair, ky) step of the conv, both shapes, equal useful FLOPs per iteration:
 // 3 taps x 2 chunks x 3 terms = 18 fragment units of K = 8 per output tile.
 // step32: per tap A hi/lo x 2, B hi/lo x 2 reads, 4 tiles x 3 MFMAs (36 MFMAs, 24 reads).
@@ -276,6 +326,31 @@ int main(int argc, char** argv) {
              k == 0 ? "32x32x16" : "16x16x32", ms * 1e3 / 5, fl / (ms * 1e-3) / 1e12,
              c[1] ? (double)c[0] / c[1] * 0.1 : 0.0);
     }
+  }
+  // loop32 variants: fragments re-read every iteration / every 16th; a barrier every 3
+  if (argc > 4 && argv[4][0] == 'v') {
+    for (int r = 0; r < rounds; ++r) {
+      for (int k = 0; k < 4; ++k) {
+        CK(hipEventRecord(e0, 0));
+        for (int rep = 0; rep < 5; ++rep) {
+          if (k == 0) hipLaunchKernelGGL((var32<1, false>), dim3(blocks), dim3(NT), 0, 0, g, out, iters, clk);
+          else if (k == 1) hipLaunchKernelGGL((var32<16, false>), dim3(blocks), dim3(NT), 0, 0, g, out, iters, clk);
+          else if (k == 2) hipLaunchKernelGGL((var32<1, true>), dim3(blocks), dim3(NT), 0, 0, g, out, iters, clk);
+          else hipLaunchKernelGGL((var32<16, true>), dim3(blocks), dim3(NT), 0, 0, g, out, iters, clk);
+        }
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        unsigned long long c[2];
+        CK(hipMemcpy(c, clk, 16, hipMemcpyDeviceToHost));
+        const double fl = 5.0 * blocks * 16.0 * iters * 4 * 3 * 32768.0;
+        static const char* nm[4] = {"lds every iter", "lds every 16th", "lds + barrier/3", "regs + barrier/3"};
+        printf("round %d var32 %-17s: %.1f us/launch  %.1f TFLOP/s  in-kernel clock %.3f GHz\n", r, nm[k],
+               ms * 1e3 / 5, fl / (ms * 1e-3) / 1e12, c[1] ? (double)c[0] / c[1] * 0.1 : 0.0);
+      }
+    }
+    return 0;
   }
   // the conv-step pair: useful FLOPs per iteration per wave = 3 taps x 4 tiles x 3 x 32x32x16
   for (int r = 0; r < rounds; ++r) {

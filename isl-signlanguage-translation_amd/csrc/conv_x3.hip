@@ -1348,10 +1348,21 @@ static bool x3_halfco(const ConvLaunch& c) {
 }
 
 // Small grids (the 128-pixel family) with the inputs and weights prefetched two K steps
-// ahead (VAR 128).  ISLPOSE_X3_DEEP=0|1 (read per launch; A/B).
+// ahead (VAR 128): by default the 3x3 layers whose grid has at most one block per CU and
+// whose K ranges (if any) run in one block -- Mode R's 23x41 stage layers at batch 32, -5 to
+// -12 % per layer in the net (profiles/r03/deep_ab/).  Its ring of three weight slabs (98 KiB)
+// allows one block per CU, so grids with more blocks lose the second resident block (conv4_x
+// at batch 32: +12-16 %), and the 1x1 layers lost 25-30 %.  ISLPOSE_X3_DEEP=0 off, =1 every
+// 1x1 / 3x3 launch of the family, across-block ranges included (A/B; read per launch).
 static bool x3_deep(const ConvLaunch& c) {
   const char* e = getenv("ISLPOSE_X3_DEEP");
-  return e && e[0] == '1' && c.ks <= 3 && !c.fold && !c.vin && (c.bco == 128 || c.bco == 96);
+  if (c.fold || c.vin || (c.bco != 128 && c.bco != 96) || c.ks > 3) return false;
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  if (c.ks != 3 || (c.ksplit > 1 && c.ws)) return false;
+  const int tpx = tile_pixels(c, 128, x3_segmax(128));
+  const long long blocks = (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * ((c.cout + c.bco - 1) / c.bco);
+  return blocks <= device_cus();
 }
 
 // Small grids (the 128-pixel family) with two chunk pairs per K step (VAR 4096): a step's

@@ -44,7 +44,11 @@ int main(int argc, char** argv) {
             n = atoi(argv[6]), iters = atoi(argv[7]);
   const std::string algos = argc > 8 ? argv[8] : "x3,direct,wino";
   const int rounds = argc > 9 ? atoi(argv[9]) : 3;
-  const int cs_in = (cin + 7) / 8 * 8, cs_out = (cout + 7) / 8 * 8;
+  // CONVBENCH_CS=c: input and output are channel slices of c-channel buffers (the net's
+  // zero-copy concat: a stage conv reads [0, cin) and writes [cout, 2 cout) of 384-channel
+  // buffers)
+  const int cs_wide = getenv("CONVBENCH_CS") ? atoi(getenv("CONVBENCH_CS")) : 0;
+  const int cs_in = std::max(cs_wide, (cin + 7) / 8 * 8), cs_out = std::max(cs_wide, (cout + 7) / 8 * 8);
   const int pin = std::max(1, ks / 2), pout = 1;
   Act in, out;
   in.n = out.n = n; in.H = out.H = H; in.W = out.W = W;
@@ -53,7 +57,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&out.base, out.bytes()));
   // env CONVBENCH_BCO overrides the output-channel tile (timing of other tile families)
   const int bco = getenv("CONVBENCH_BCO") ? atoi(getenv("CONVBENCH_BCO")) : conv_bco_for(cout);
-  const int chunks = cs_in / 8, pairs = (chunks + 1) / 2, co_tiles = (cout + bco - 1) / bco;
+  const int chunks = (cin + 7) / 8, pairs = (chunks + 1) / 2, co_tiles = (cout + bco - 1) / bco;
   float* wd = dev_random<float>((size_t)co_tiles * chunks * ks * ks * 2 * bco * 4, -0.05f, 0.05f, 2);
   _Float16* wx = dev_random<_Float16>((size_t)co_tiles * pairs * ks * ks * 4 * bco * 8, -8192.f, 8192.f, 3);
   const int wb = wino_bco_for(cout);
@@ -67,7 +71,7 @@ int main(int argc, char** argv) {
   CK(hipMemset(flag, 0, 4));
   ConvLaunch L;
   L.in = in.base; L.in_pad = pin; L.in_cs = cs_in; L.in_coff = 0;
-  L.out = out.base; L.out_pad = pout; L.out_cs = cs_out; L.out_coff = 0;
+  L.out = out.base; L.out_pad = pout; L.out_cs = cs_out; L.out_coff = cs_wide >= 2 * cout ? (cout + 7) / 8 * 8 : 0;
   L.bias = bias; L.slope = slope; L.n = n; L.H = H; L.W = W; L.ks = ks; L.cin_chunks = chunks; L.cout = cout;
   L.act = ACT_PRELU; L.wx3 = wx; L.wscale_inv = 1.f / 16384.f; L.range_flag = flag;
   // CONVBENCH_SPLIT=1|2: the net's K-range mode (canonical ranges / latency split), with a workspace
@@ -86,6 +90,14 @@ int main(int argc, char** argv) {
     L.dbg = dbg;
   }
   const double flops = 2.0 * cout * cin * ks * ks * (double)H * W * n;
+  // the polluter of CONVBENCH_POLLUTE: a 1x1 layer on the same buffers (cin chunks of this
+  // shape, 32 output channels), default variant
+  const bool pollute = getenv("CONVBENCH_POLLUTE") && atoi(getenv("CONVBENCH_POLLUTE"));
+  ConvLaunch PL = L;
+  PL.ks = 1; PL.cout = 32; PL.bco = 32; PL.ws = nullptr; PL.ws_floats = 0; PL.allow_split = 0;
+  void* flush = nullptr;
+  const size_t flush_bytes = (size_t)1 << 30;
+  if (getenv("CONVBENCH_FLUSH") && atoi(getenv("CONVBENCH_FLUSH"))) CK(hipMalloc(&flush, flush_bytes));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -118,12 +130,30 @@ int main(int argc, char** argv) {
       };
       if (launch() != hipSuccess) continue;
       for (int i = 0; i < 2; ++i) CK(launch());
-      CK(hipEventRecord(e0, 0));
-      for (int i = 0; i < iters; ++i) CK(launch());
-      CK(hipEventRecord(e1, 0));
-      CK(hipEventSynchronize(e1));
-      float ms;
-      CK(hipEventElapsedTime(&ms, e0, e1));
+      float ms = 0.f;
+      if (flush || pollute) {
+        // CONVBENCH_FLUSH=1: caches cold before every launch (a 1 GiB memset evicts L2 and the
+        // Infinity Cache), each launch timed alone -- the net's first touch of a layer's weights.
+        // CONVBENCH_POLLUTE=1: a launch of the conv_x3 variant of another shape (a 1x1 layer)
+        // before every timed launch, as in the net, where kernels of other shapes alternate
+        for (int i = 0; i < iters; ++i) {
+          if (flush) CK(hipMemsetAsync(flush, i & 0xff, flush_bytes, 0));
+          if (pollute) CK(launch_conv_x3(PL, 0));
+          CK(hipEventRecord(e0, 0));
+          CK(launch());
+          CK(hipEventRecord(e1, 0));
+          CK(hipEventSynchronize(e1));
+          float m1;
+          CK(hipEventElapsedTime(&m1, e0, e1));
+          ms += m1;
+        }
+      } else {
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < iters; ++i) CK(launch());
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms, e0, e1));
+      }
       const double us = ms * 1e3 / iters;
       const double fac = (a == "x3" || a == "x3m" || a == "x3h" || a == "x3p" || a == "x3d") ? 3.0 : a == "wx3" ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
       printf("  round %d %-7s %9.1f us  fp32-equiv %7.1f TF  alg-MFMA %7.1f TF\n", r, a.c_str(), us,

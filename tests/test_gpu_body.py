@@ -493,6 +493,7 @@ def test_x3_halfco_small_grids_bit_identical(net25, n, monkeypatch):
     maps are bit-identical to the 128-channel blocks'."""
     x = torch.from_numpy(_inputs(n, 184, 328, seed=91 + n)).cuda()
     monkeypatch.setenv("ISLPOSE_X3_PPS2", "0")   # it takes precedence over the half tiles
+    monkeypatch.setenv("ISLPOSE_X3_DEEP", "0")   # and so does the deep-prefetch loop
     monkeypatch.setenv("ISLPOSE_X3_HALFCO", "0")
     paf0, heat0 = net25.forward(x)
     torch.cuda.synchronize()
@@ -511,6 +512,7 @@ def test_x3_pps2_small_grids(net25, w25, monkeypatch):
     bit), within 1e-5 of the one-pair steps (another fp32 order), within the 1e-4 bar of the
     oracle; the 23x41 stage layers take the variant (isl_net_op_info)."""
     frames = _inputs(20, 184, 328, seed=77)
+    monkeypatch.setenv("ISLPOSE_X3_DEEP", "0")   # it takes precedence over two pairs per step
     monkeypatch.setenv("ISLPOSE_X3_PPS2", "1")
     paf, heat = net25.forward(torch.from_numpy(frames).cuda())
     var = [rt.decode_variant(v) for _, v in net25.op_variants()]

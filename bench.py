@@ -82,6 +82,11 @@ def parse(argv=None):
     p.add_argument("--fail-rank", type=int, default=-1,
                    help="test only (with --dry-run): this rank exits 1 after the group is up, so the "
                         "launcher's fail-fast path is exercised (tests/test_bench_launch.py)")
+    p.add_argument("--post-overlap", action="store_true",
+                   help="the post of batch k on its own stream beside the net of batch k+1 "
+                        "(BodyEstimator.launch(post_stream=...)); measured +0.8 %% Mode N, +0-5 %% Mode R, "
+                        "+5 %% at batch 1, but the post then slows the concurrent convs (Mode N frac 0.446 -> "
+                        "0.439, Mode R 0.34 -> 0.29), so off by default (profiles/r03/post_overlap/)")
     p.add_argument("--no-mode-r", dest="mode_r", action="store_false",
                    help="skip the Mode R sub-measurement (net 184x328 at batch 32 and batch 1)")
     p.add_argument("--pg-timeout", type=float, default=120.0,
@@ -237,6 +242,19 @@ def gpu_main(args, rank, local, world):
                 self.hp = (ctypes.c_void_p * 1)(self.heat.data_ptr())
                 self.stream = main_stream if S == 1 else torch.cuda.Stream(dev)
                 self.sh = rt.stream_handle(self.stream)
+                # post overlap: the net writes this batch's low-res maps into one of two NCHW
+                # buffers (what BodyEstimator.launch(post_stream=...) keeps for the post), and
+                # the post of batch k runs on its own stream beside the net of batch k+1.  The
+                # post here reads the designed maps (see `data`); the unpack into the buffers
+                # and the buffer hand-over events are the product's own cost and ordering.
+                self.pstream = torch.cuda.Stream(dev) if args.post_overlap else self.stream
+                self.psh = rt.stream_handle(self.pstream)
+                nh8, nw8 = nh // 8, nw // 8
+                self.maps = [(torch.empty((self.b, 52, nh8, nw8), device=dev),
+                              torch.empty((self.b, 26, nh8, nw8), device=dev)) for _ in range(2)] \
+                    if args.post_overlap else None
+                self.maps_free = [None, None]
+                self.k = 0
                 # D2H of the records on a copy stream: it overlaps the next step's preprocess and
                 # net; the next post (which rewrites d_res) waits for it, and the timed region's
                 # closing device synchronize includes it
@@ -260,13 +278,24 @@ def gpu_main(args, rank, local, world):
                     ln.stream.wait_event(ref)
                 ln.net.preprocess(ln.frames, mult, stream=ln.stream)
                 e0 = mark(ln.stream) if timed else None
-                ln.net.run(stream=ln.stream)
-                e1 = mark(ln.stream) if timed else None
+                if ln.maps is not None:
+                    slot = ln.k & 1
+                    if ln.maps_free[slot] is not None:        # the post two batches back is done with it
+                        ln.stream.wait_event(ln.maps_free[slot])
+                    ln.net.run(ln.maps[slot][0], ln.maps[slot][1], stream=ln.stream)
+                else:
+                    ln.net.run(stream=ln.stream)
+                e1 = mark(ln.stream)
+                if ln.pstream is not ln.stream:
+                    ln.pstream.wait_event(e1)
                 if ln.copied is not None:
-                    ln.stream.wait_event(ln.copied)
+                    ln.pstream.wait_event(ln.copied)
                 rt.check(L.isl_body_post(ln.net.h, ln.b, H, W, 1, ln.g, ln.pp, ln.hp, ctypes.byref(ln.caps),
-                                         rt.ptr(ln.d_res), ln.sh), "post")
-                e2 = mark(ln.stream)
+                                         rt.ptr(ln.d_res), ln.psh), "post")
+                e2 = mark(ln.pstream)
+                if ln.maps is not None:
+                    ln.maps_free[ln.k & 1] = e2
+                    ln.k += 1
                 marks.append((e0, e1, e2))
                 ln.cs.wait_event(e2)
                 with torch.cuda.stream(ln.cs):
@@ -391,7 +420,8 @@ def gpu_main(args, rank, local, world):
         "config": {"workload": "configs[1]: body_25 single-scale %dx%d frames, batch %d per GPU, net input %dx%d"
                                % (H, W, B, nh, nw),
                    "batch_per_gpu": B, "frame_hw": [H, W], "scale_search": [args.scale], "net_hw": [nh, nw],
-                   "streams_per_gpu": S, "conv_algo": args.algo, "split_k": bool(args.split_k),
+                   "streams_per_gpu": S, "post_overlap": bool(args.post_overlap),
+                   "conv_algo": args.algo, "split_k": bool(args.split_k),
                    "x3_m16": os.environ.get("ISLPOSE_X3_M16", "default"),
                    "parallelism": "frame-sharded x%d (no collective)" % world},
         "ranks": {"world_observed": torch.distributed.get_world_size() if world > 1 else 1,
@@ -498,7 +528,8 @@ def post_fields(H, W, B, post_ms, pairs):
         "nms_effective_GBps": round(25 * H * W * 4 * B / (post_ms * 1e-3) / 1e9, 1),
         "paf_pairs_per_frame": round(pairs / B, 1),
         "paf_pairs_per_s": round(pairs / (post_ms * 1e-3), 1),
-        "basis": "HIP events around isl_body_post on the lane stream (fused resize+blur+NMS, peak lists, PAF "
+        "basis": "HIP events around isl_body_post on the post stream (with post_overlap it runs beside the next "
+                 "batch's net, so this window can stretch; fused resize+blur+NMS, peak lists, PAF "
                  "scoring, greedy matching, assembly; D2H excluded). nms_effective_GBps = SURVEY 8(d)'s NMS "
                  "bytes (25 x H x W x 4 B f32 heat per frame) / whole post time: the fused kernel never "
                  "materialises those planes, so this is an effective rate, not HBM traffic",

@@ -217,30 +217,45 @@ class BodyEstimator:
         return out[0] if single else out
 
     # -- pipelined (stream-ordered) form of estimate --------------------------------
-    def launch(self, frames_t):
+    def launch(self, frames_t, post_stream=None):
         """Enqueue estimate() on the current stream without waiting: nets, post, the
         records' copy to pinned host memory and a stream-ordered range check.  frames_t:
-        cuda uint8 [n,H,W,3].  finish(job) completes it; the net must not run again
-        before that (its arena holds the maps a capacity re-run reads)."""
+        cuda uint8 [n,H,W,3].  finish(job) completes it.
+
+        Without post_stream the net must not run again before finish (its arena holds the
+        maps the post and a capacity re-run read).  With post_stream the nets write this
+        batch's low-res maps into tensors of its own, the range check follows them on the
+        current stream, and the post and the records' copy run on post_stream: the next
+        launch's nets may start on the current stream at once, beside this post (the body
+        of a video's batch k+1 beside the post of batch k; bench.py's default step)."""
         import torch
         n, H, W, _ = frames_t.shape
-        geoms, pafs, heats = self.run_scales(frames_t)
+        geoms, pafs, heats = self.run_scales(frames_t, keep_maps=post_stream is not None)
+        flag = rt.flag_slot(self)
+        self.net.check_async(flag)
         caps = dict(self.caps)
         c = rt.IslCaps(**caps)
         lay = rt.body_layout(self.kind, c)
-        res = torch.empty(n * lay.record_bytes, dtype=torch.uint8, device=frames_t.device)
-        ns = len(geoms)
-        g = (rt.IslScaleGeom * ns)(*[rt.IslScaleGeom(*gg) for gg in geoms])
-        pp = (ctypes.c_void_p * ns)(*[rt.ptr(p).value for p in pafs])
-        hp = (ctypes.c_void_p * ns)(*[rt.ptr(h).value for h in heats])
-        rt.check(rt.lib().isl_body_post(self.net.h, n, H, W, ns, g, pp, hp, ctypes.byref(c), rt.ptr(res),
-                                       rt.stream_handle()), "isl_body_post")
-        host = torch.empty(res.shape, dtype=torch.uint8, pin_memory=True)
-        host.copy_(res, non_blocking=True)
-        flag = rt.flag_slot(self)
-        self.net.check_async(flag)
-        ev = torch.cuda.Event()
-        ev.record()
+        cur = torch.cuda.current_stream(frames_t.device)
+        ps = post_stream if post_stream is not None else cur
+        if ps is not cur:
+            ps.wait_stream(cur)
+        with torch.cuda.stream(ps):
+            res = torch.empty(n * lay.record_bytes, dtype=torch.uint8, device=frames_t.device)
+            ns = len(geoms)
+            g = (rt.IslScaleGeom * ns)(*[rt.IslScaleGeom(*gg) for gg in geoms])
+            pp = (ctypes.c_void_p * ns)(*[rt.ptr(p).value for p in pafs])
+            hp = (ctypes.c_void_p * ns)(*[rt.ptr(h).value for h in heats])
+            rt.check(rt.lib().isl_body_post(self.net.h, n, H, W, ns, g, pp, hp, ctypes.byref(c), rt.ptr(res),
+                                           rt.stream_handle(ps)), "isl_body_post")
+            host = torch.empty(res.shape, dtype=torch.uint8, pin_memory=True)
+            host.copy_(res, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(ps)
+        if ps is not cur:
+            for m in pafs + heats:
+                if m is not None:
+                    m.record_stream(ps)
         return dict(t=frames_t, n=n, H=H, W=W, geoms=geoms, pafs=pafs, heats=heats, caps=caps, lay=lay, res=res,
                     host=host, flag=flag, ev=ev)
 

@@ -209,6 +209,22 @@ def test_body_estimate_end_to_end(est25, w25):
         assert _rel(heats[0][i:i + 1].cpu().numpy(), rh) < TOL
 
 
+def test_launch_post_stream_equals_estimate(est25):
+    """BodyEstimator.launch(post_stream=...): the nets of three batches run back to back on
+    the current stream while each batch's post and records' copy run on a post stream beside
+    the next batch's nets (the maps in tensors of the batch, the range check on the net's
+    stream); finish() of each gives exactly estimate()'s candidate / subset, capacity re-runs
+    included (random-weight maps are dense)."""
+    ps = torch.cuda.Stream()
+    batches = [torch.from_numpy(synth.synth_frames(2, 368, 656, seed=40 + k)).cuda() for k in range(3)]
+    jobs = [est25.launch(b, post_stream=ps) for b in batches]
+    got = [est25.finish(j) for j in jobs]
+    for b, g in zip(batches, got):
+        ref = est25.estimate(b)
+        for (c0, s0), (c1, s1) in zip(ref, g):
+            assert np.array_equal(c0, c1) and np.array_equal(s0, s1)
+
+
 def test_designed_maps_batch_bit_exact(est25):
     """A batch of designed maps (P = 0..6 persons) through the GPU post == oracle post."""
     H, W = 368, 656

@@ -121,11 +121,18 @@ __device__ __forceinline__ float sample(const MapSrc& m, int f, int c, int y, in
 // HResizeCubic, stored in LDS), then every output combines 4 of those rows
 // (VResizeCubic) -- the same values OpenCV computes, with 4-5x fewer loads.
 constexpr int RS_TY = 64, RS_TX = 256, RS_MAXR = 40;   // 64 rows: amortise the horizontal pass
-__global__ void __launch_bounds__(256) resize_sep_kernel(MapSrc m, int nch, int oh, int ow, int ty_rows, int mode,
-                                                          float inv_div_f, void* out) {
-  __shared__ float s_h[RS_MAXR][RS_TX];
+// The vertical taps of the tile's output rows are computed once per block into LDS (they
+// depend on the row only; per thread they were most of the vertical pass's VALU work), and
+// the block is TX = 128 or 256 columns wide, whichever wastes fewer idle lanes on the
+// output width (launch_resize): the same values, bit for bit.
+template <int TX>
+__global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int oh, int ow, int ty_rows, int mode,
+                                                         float inv_div_f, void* out) {
+  __shared__ float s_h[RS_MAXR][TX];
+  __shared__ int4 s_yi[RS_TY];
+  __shared__ float4 s_be[RS_TY];
   const int plane = blockIdx.x, f = plane / nch, c = plane - f * nch;
-  const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * RS_TX + threadIdx.x;
+  const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * TX + threadIdx.x;
   const int ny = min(ty_rows, oh - y0);
   const float* b = m.base + (size_t)f * m.fs + chan_off(m, c);
   // source rows the tile needs: [r_lo, r_lo + nr)
@@ -137,6 +144,13 @@ __global__ void __launch_bounds__(256) resize_sep_kernel(MapSrc m, int nch, int 
     taps(y0 + ny - 1, m.scy, m.sh, hi, dummy);
     r_lo = lo[0];
     nr = hi[3] - r_lo + 1;
+    if ((int)threadIdx.x < ny) {
+      int yi[4];
+      float be[4];
+      taps(y0 + threadIdx.x, m.scy, m.sh, yi, be);
+      s_yi[threadIdx.x] = make_int4(yi[0] - r_lo, yi[1] - r_lo, yi[2] - r_lo, yi[3] - r_lo);
+      s_be[threadIdx.x] = make_float4(be[0], be[1], be[2], be[3]);
+    }
   }
   if (nr > RS_MAXR) __builtin_trap();   // the host sizes ty_rows so that this cannot happen
   if (x < ow) {
@@ -163,13 +177,12 @@ __global__ void __launch_bounds__(256) resize_sep_kernel(MapSrc m, int nch, int 
     if (m.identity) {
       v = s_h[t][threadIdx.x];
     } else {
-      int yi[4];
-      float be[4];
-      taps(y, m.scy, m.sh, yi, be);
-      const float h0 = s_h[yi[0] - r_lo][threadIdx.x], h1 = s_h[yi[1] - r_lo][threadIdx.x];
-      const float h2 = s_h[yi[2] - r_lo][threadIdx.x], h3 = s_h[yi[3] - r_lo][threadIdx.x];
-      v = simd ? h0 * be[0] + (h1 * be[1] + (h2 * be[2] + h3 * be[3]))   // VResizeCubicVec_32f body
-               : ((h0 * be[0] + h1 * be[1]) + h2 * be[2]) + h3 * be[3];   // scalar tail
+      const int4 yi = s_yi[t];
+      const float4 be = s_be[t];
+      const float h0 = s_h[yi.x][threadIdx.x], h1 = s_h[yi.y][threadIdx.x];
+      const float h2 = s_h[yi.z][threadIdx.x], h3 = s_h[yi.w][threadIdx.x];
+      v = simd ? h0 * be.x + (h1 * be.y + (h2 * be.z + h3 * be.w))   // VResizeCubicVec_32f body
+               : ((h0 * be.x + h1 * be.y) + h2 * be.z) + h3 * be.w;   // scalar tail
     }
     const size_t i = ((size_t)plane * oh + y) * ow + x;
     if (mode == 1) {
@@ -198,6 +211,8 @@ struct MapSrcN {   // up to MAX_SCALES (8) scales
 __global__ void __launch_bounds__(256) resize_acc_kernel(MapSrcN ms, int ns, int nch, int oh, int ow, int ty_rows,
                                                          float div_f, int quirk, double* out) {
   __shared__ float s_h[RS_MAXR][RS_TX];
+  __shared__ int4 s_yi[RA_TY];          // vertical taps of the tile's rows, per scale (as resize_sep_kernel)
+  __shared__ float4 s_be[RA_TY];
   const int plane = blockIdx.x, f = plane / nch, c = plane - f * nch;
   const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * RS_TX + threadIdx.x;
   const int ny = min(ty_rows, oh - y0);
@@ -218,6 +233,13 @@ __global__ void __launch_bounds__(256) resize_acc_kernel(MapSrcN ms, int ns, int
     }
     if (nr > RS_MAXR) __builtin_trap();   // the host sizes ty_rows so that this cannot happen
     __syncthreads();                      // the previous scale's vertical pass is done with s_h
+    if (!m.identity && (int)threadIdx.x < ny) {
+      int yi[4];
+      float be[4];
+      taps(y0 + threadIdx.x, m.scy, m.sh, yi, be);
+      s_yi[threadIdx.x] = make_int4(yi[0] - r_lo, yi[1] - r_lo, yi[2] - r_lo, yi[3] - r_lo);
+      s_be[threadIdx.x] = make_float4(be[0], be[1], be[2], be[3]);
+    }
     if (x < ow) {
       if (m.identity) {
         for (int r = 0; r < nr; ++r) s_h[r][threadIdx.x] = b[(size_t)(r_lo + r) * m.ys + (size_t)x * m.xs];
@@ -243,13 +265,12 @@ __global__ void __launch_bounds__(256) resize_acc_kernel(MapSrcN ms, int ns, int
         if (m.identity) {
           v = s_h[t][threadIdx.x];
         } else {
-          int yi[4];
-          float be[4];
-          taps(y0 + t, m.scy, m.sh, yi, be);
-          const float h0 = s_h[yi[0] - r_lo][threadIdx.x], h1 = s_h[yi[1] - r_lo][threadIdx.x];
-          const float h2 = s_h[yi[2] - r_lo][threadIdx.x], h3 = s_h[yi[3] - r_lo][threadIdx.x];
-          v = simd ? h0 * be[0] + (h1 * be[1] + (h2 * be[2] + h3 * be[3]))
-                   : ((h0 * be[0] + h1 * be[1]) + h2 * be[2]) + h3 * be[3];
+          const int4 yi = s_yi[t];
+          const float4 be = s_be[t];
+          const float h0 = s_h[yi.x][threadIdx.x], h1 = s_h[yi.y][threadIdx.x];
+          const float h2 = s_h[yi.z][threadIdx.x], h3 = s_h[yi.w][threadIdx.x];
+          v = simd ? h0 * be.x + (h1 * be.y + (h2 * be.z + h3 * be.w))
+                   : ((h0 * be.x + h1 * be.y) + h2 * be.z) + h3 * be.w;
         }
         const float q = v / div_f;      // heatmap / len(multiplier), float32
         // from np.zeros (0.0 + x included): hand.py:56, or body.py:80's doubling quirk
@@ -1957,8 +1978,13 @@ static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mo
     while (ty > 1 && (ty - 1) * m.scy + 5.0 > (double)RS_MAXR) --ty;
   const long long ty_tiles = (oh + ty - 1) / ty;
   if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "resize: output too tall");
-  hipLaunchKernelGGL(resize_sep_kernel, dim3(n * nch, (unsigned)ty_tiles, (ow + RS_TX - 1) / RS_TX), dim3(RS_TX), 0, s,
-                     m, nch, oh, ow, ty, mode, div_f, out);
+  // 128-column blocks where they leave fewer idle lanes (ow = 328: 384 vs 512 lanes)
+  if ((ow + 127) / 128 * 128 < (ow + RS_TX - 1) / RS_TX * RS_TX)
+    hipLaunchKernelGGL(resize_sep_kernel<128>, dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128), dim3(128), 0, s,
+                       m, nch, oh, ow, ty, mode, div_f, out);
+  else
+    hipLaunchKernelGGL(resize_sep_kernel<RS_TX>, dim3(n * nch, (unsigned)ty_tiles, (ow + RS_TX - 1) / RS_TX),
+                       dim3(RS_TX), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
   PHIP(hipGetLastError());
   return ISL_OK;
 }

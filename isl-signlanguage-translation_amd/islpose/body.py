@@ -257,23 +257,33 @@ class BodyEstimator:
                 if m is not None:
                     m.record_stream(ps)
         return dict(t=frames_t, n=n, H=H, W=W, geoms=geoms, pafs=pafs, heats=heats, caps=caps, lay=lay, res=res,
-                    host=host, flag=flag, ev=ev)
+                    host=host, flag=flag, ev=ev, ps=post_stream)
 
     def finish(self, job, details=False):
         """Wait for a launch() and decode it: the same results as estimate(), including
         the fp32 re-run of a batch that left the split-fp16 range and the post re-run
         with larger buffers on a capacity overflow."""
+        import contextlib
+        import torch
         job["ev"].synchronize()
         n, H, W = job["n"], job["H"], job["W"]
+        # a re-run's post goes where the launch's post went: the posts of later launches on a
+        # post stream share the net's post scratch with it
+        ps = job.get("ps")
+        on_ps = (lambda: torch.cuda.stream(ps)) if ps is not None else contextlib.nullcontext
         if int(job["flag"][0]) != 0:
             with self.net.algo_scope("direct"):
-                geoms, pafs, heats = self.run_scales(job["t"])
-                host, lay, caps = self.post(n, H, W, geoms, pafs, heats)
+                geoms, pafs, heats = self.run_scales(job["t"], keep_maps=ps is not None)
+                if ps is not None:
+                    ps.wait_stream(torch.cuda.current_stream(job["t"].device))
+                with on_ps():
+                    host, lay, caps = self.post(n, H, W, geoms, pafs, heats)
         else:
             host, lay, caps = job["host"].numpy(), job["lay"], job["caps"]
             grow = self._grow(host, lay, n, caps)
             if grow is not None:
-                host, lay, caps = self.post(n, H, W, job["geoms"], job["pafs"], job["heats"], caps=grow)
+                with on_ps():
+                    host, lay, caps = self.post(n, H, W, job["geoms"], job["pafs"], job["heats"], caps=grow)
         res = self.decode(host, lay, caps, n, details)
         return res if details else [(r.candidate, r.subset) for r in res]
 

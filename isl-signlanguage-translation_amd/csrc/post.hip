@@ -251,6 +251,7 @@ __global__ void __launch_bounds__(256) resize_acc_kernel(MapSrcN ms, int ns, int
         float a[4];
         taps(x, m.scx, m.sw, xi, a);
         const long long o0 = xi[0] * m.xs, o1 = xi[1] * m.xs, o2 = xi[2] * m.xs, o3 = xi[3] * m.xs;
+#pragma unroll 8
         for (int r = 0; r < nr; ++r) {
           const float* row = b + (size_t)(r_lo + r) * m.ys;
           s_h[r][threadIdx.x] = ((row[o0] * a[0] + row[o1] * a[1]) + row[o2] * a[2]) + row[o3] * a[3];

@@ -1,3 +1,4 @@
+# A/B of one-pair canonical K ranges (ISLPOSE_X3_RANGE1, a temporary switch since removed): neutral, see profiles/r03/range1.
 T=${1:-rng1}; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
 ISLPOSE_X3_RANGE1=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_body.py -x -v --timeout 300 --timeout-method thread \

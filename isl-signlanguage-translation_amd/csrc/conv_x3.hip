@@ -1341,10 +1341,17 @@ static int device_cus() {
 // over S blocks (split-K) and a large batch can keep them in one block, with the same
 // bits.  Every range is ceil(pairs / S) pairs long and non-empty.
 // Small grids (the 128-pixel family) with 128-channel tiles on two 64-channel blocks of 4
-// waves each (VAR 256).  ISLPOSE_X3_HALFCO=0|1 (read per launch; A/B).
+// waves each (VAR 256): by default the 1x1 / 3x3 layers whose K ranges are split across
+// blocks (grids below one block per CU: batch-1 Mode R, +4 % frames/s), where doubling the
+// grid buys more than the second staging of the input costs; with one block per CU (Mode R
+// batch 32) it loses 10-20 % (profiles/r03/halfco_ab/).  Same bits either way.
+// ISLPOSE_X3_HALFCO=0 off, =1 every 128-channel launch of the family (read per launch; A/B).
 static bool x3_halfco(const ConvLaunch& c) {
   const char* e = getenv("ISLPOSE_X3_HALFCO");
-  return e && e[0] == '1' && c.ks <= 7 && !c.fold;
+  if (c.ks > 7 || c.fold) return false;
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return c.ks <= 3 && c.ksplit > 1 && c.ws;
 }
 
 // Small grids (the 128-pixel family) with the inputs and weights prefetched two K steps

@@ -519,6 +519,15 @@ def test_x3_halfco_small_grids_bit_identical(net25, n, monkeypatch):
     var = [rt.decode_variant(v) for _, v in net25.op_variants()]
     assert sum(1 for v in var if v.get("var", 0) & 256) >= 40
     assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
+    # default: half tiles only where the K ranges are split across blocks (batch 1)
+    monkeypatch.delenv("ISLPOSE_X3_HALFCO")
+    paf2, heat2 = net25.forward(x)
+    torch.cuda.synchronize()
+    var = [rt.decode_variant(v) for _, v in net25.op_variants()]
+    halves = sum(1 for v in var if v.get("var", 0) & 256)
+    assert halves >= 40 if n == 1 else halves == 0
+    assert all(v.get("var", 0) & 2048 for v in var if v.get("var", 0) & 256)
+    assert torch.equal(paf0, paf2) and torch.equal(heat0, heat2)
 
 
 def test_x3_pps2_small_grids(net25, w25, monkeypatch):

@@ -142,6 +142,16 @@ int isl_net_get_algo(const isl_net* net);
  * Env ISLPOSE_X3_SPLITK=0|1|2 sets the mode at create time. */
 int isl_net_set_split_k(isl_net* net, int mode);
 
+/* Graph replay of the conv chain (not in the reference: it replaces the per-op launches of
+ * its torch module, src/model.py:171-207, with one HIP graph launch).  on = 1 (default):
+ * the first isl_net_run / isl_net_forward of a run key (batch size, K-range mode, conv
+ * algorithm, ISLPOSE_* environment) on an arena runs eagerly, the second captures the
+ * launches on a private stream and launches the graph on the caller's stream, later runs
+ * replay it -- the same kernels with the same arguments, the same bits.  Timed runs
+ * (isl_net_set_timing) stay eager; weight uploads and workspace growth drop the graphs.
+ * on = 0: every run eager.  Env ISLPOSE_NET_GRAPH=0 turns replay off process-wide. */
+int isl_net_set_graph(isl_net* net, int on);
+
 /* Range guard of ISL_ALGO_X3: waits for the device, returns ISL_E_RANGE if any
  * conv output since the last clear left the fp16 split range (the results of
  * those runs are then not fp32-accurate and must be recomputed with

@@ -17,6 +17,8 @@
 #include <string>
 #include <vector>
 
+#include <unistd.h>   // environ (run_key)
+
 #include "internal.h"
 #include "islpose.h"
 
@@ -224,6 +226,14 @@ struct isl_net {
     size_t fold_mem_floats = 0;
     X3Fold* fold_tab = nullptr;
     size_t fold_tab_n = 0;
+    // the conv chain replayed as a HIP graph (run_ops): per run key (batch, K-range mode,
+    // algorithm, ISLPOSE_* environment) the eager runs seen and the instantiated graph
+    struct Graph {
+      hipGraphExec_t exec = nullptr;
+      std::vector<int> op_variant;
+    };
+    std::map<unsigned long long, Graph> graphs;
+    std::map<unsigned long long, int> graph_seen;
   };
   std::map<long long, Arena> plans;
   Arena* cur = nullptr;        // the arena of the current plan
@@ -243,6 +253,10 @@ struct isl_net {
   bool timing = false;
   std::vector<TimedRun> timed;
   std::vector<int> op_variant;   // per op of the last run: x3_variant_code, -1 pool skipped (vin), 0 other
+  // graph replay of the conv chain (isl_net_set_graph; env ISLPOSE_NET_GRAPH=0 turns it off)
+  int graph = 1;
+  bool capturing = false;
+  hipStream_t cap_stream = nullptr;
   // conv algorithm (ISL_ALGO_*) and the split-fp16 range flag (isl_net_check)
   int algo = ISL_ALGO_X3;
   int split_k = 1;             // isl_net_set_split_k: K-range mode (env ISLPOSE_X3_SPLITK=0|1|2)
@@ -595,7 +609,10 @@ static std::vector<_Float16> pack_wino_x3(const ConvLayer& c, float* inv_scale) 
 }
 #endif
 
+static void drop_all_graphs(isl_net* net);
+
 static int upload_params(isl_net* net) {
+  drop_all_graphs(net);   // new weight scales: the captured launches' arguments are stale
   for (ConvLayer& c : net->layers) {
     if (!c.has_w || !c.has_b || (c.act == ACT_PRELU && !c.has_s))
       return fail(ISL_E_STATE, "parameter missing for layer " + c.name);
@@ -670,7 +687,21 @@ static size_t arena_budget() {
   return b;
 }
 
+// Instantiated graphs hold the pointers and scalars of the launches they captured: any
+// reallocation of a buffer they name (arena, split-K workspace, weights re-uploaded with new
+// scales) drops them.  hipGraphExecDestroy lets queued replays finish.
+static void drop_graphs(isl_net::Arena& ar) {
+  for (auto& kv : ar.graphs)
+    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+  ar.graphs.clear();
+}
+
+static void drop_all_graphs(isl_net* net) {
+  for (auto& kv : net->plans) drop_graphs(kv.second);
+}
+
 static void drop_arena(isl_net* net, std::map<long long, isl_net::Arena>::iterator it) {
+  drop_graphs(it->second);
   // hipFree waits for queued work that may still use the arena
   (void)hipFree(it->second.base);
   if (it->second.tab) (void)hipFree(it->second.tab);
@@ -942,7 +973,7 @@ static int plan_fold(isl_net* net, hipStream_t s) {
   return ISL_OK;
 }
 
-static int run_ops(isl_net* net, hipStream_t s) {
+static int run_ops_eager(isl_net* net, hipStream_t s) {
   isl_net::TimedRun* tr = nullptr;
   if (net->timing) {
     net->timed.emplace_back();
@@ -1026,6 +1057,8 @@ static int run_ops(isl_net* net, hipStream_t s) {
       const size_t need = x3_splitk_ws_floats(L);
       isl_net::Arena& ar = *net->cur;
       if (need > ar.ks_floats) {
+        if (net->capturing) return fail(ISL_E_STATE, "graph capture: split-K workspace growth");
+        drop_graphs(ar);   // they name the old workspace
         // grow-only; hipFree waits for the queued work that may still read the old one
         if (ar.ks) HIP_OK(hipFree(ar.ks));
         ar.ks = nullptr;
@@ -1065,6 +1098,69 @@ static int run_ops(isl_net* net, hipStream_t s) {
       HIP_OK(hipEventRecord(tr->ev[k + 1], s));
     }
   }
+  return ISL_OK;
+}
+
+// Graph replay of the conv chain.  At batch 1 (Mode R, the reference's per-frame calls) the
+// host enqueue of ~230 launches (selection logic + hipLaunchKernel, ~7.6 us each) took as
+// long as the GPU work, so the GPU waited on the host (tools/b1_host.py).  A run key fixes
+// everything the launches depend on besides the arena: batch size, K-range mode, algorithm
+// and the ISLPOSE_* switches read per launch.  The first run of a key is eager (it sizes the
+// workspaces), the second captures the chain on a private stream, instantiates it and
+// launches it on the caller's stream; later runs replay it.  The kernels, their order and
+// arguments are those of the eager run: the same bits.  Timed runs (isl_net_set_timing) and
+// the split-K fold (its plan uploads a table) stay eager.
+static unsigned long long run_key(const isl_net* net) {
+  unsigned long long h = 1469598103934665603ull;
+  auto mix = [&](unsigned long long v) { h = (h ^ v) * 1099511628211ull; };
+  mix((unsigned long long)net->pn);
+  mix((unsigned long long)net->split_k + 16 * (unsigned long long)net->algo);
+  for (char** e = environ; e && *e; ++e)
+    if (!strncmp(*e, "ISLPOSE_", 8))
+      for (const char* c = *e; *c; ++c) mix((unsigned char)*c);
+  return h;
+}
+
+static bool graph_enabled(const isl_net* net) {
+  const char* e = getenv("ISLPOSE_NET_GRAPH");
+  if (e && e[0] == '0') return false;
+  return net->graph && !net->timing && !fold_enabled();
+}
+
+static int run_ops(isl_net* net, hipStream_t s) {
+  if (!graph_enabled(net)) return run_ops_eager(net, s);
+  isl_net::Arena& ar = *net->cur;
+  const unsigned long long key = run_key(net);
+  auto g = ar.graphs.find(key);
+  if (g != ar.graphs.end()) {
+    net->op_variant = g->second.op_variant;
+    HIP_OK(hipGraphLaunch(g->second.exec, s));
+    return ISL_OK;
+  }
+  int& seen = ar.graph_seen[key];
+  if (seen++ < 1) return run_ops_eager(net, s);
+  if (!net->cap_stream) HIP_OK(hipStreamCreateWithFlags(&net->cap_stream, hipStreamNonBlocking));
+  HIP_OK(hipStreamBeginCapture(net->cap_stream, hipStreamCaptureModeRelaxed));
+  net->capturing = true;
+  const int rc = run_ops_eager(net, net->cap_stream);
+  net->capturing = false;
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(net->cap_stream, &graph);
+  hipGraphExec_t exec = nullptr;
+  hipError_t ei = hipErrorUnknown;
+  if (rc == ISL_OK && ec == hipSuccess && graph) ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  if (graph) (void)hipGraphDestroy(graph);
+  if (rc != ISL_OK || ec != hipSuccess || ei != hipSuccess) {
+    // nothing ran: the chain was only recorded.  Run it eagerly, and keep this key eager
+    (void)hipGetLastError();
+    if (exec) (void)hipGraphExecDestroy(exec);
+    seen = -(1 << 30);
+    return run_ops_eager(net, s);
+  }
+  isl_net::Arena::Graph& G = ar.graphs[key];
+  G.exec = exec;
+  G.op_variant = net->op_variant;
+  HIP_OK(hipGraphLaunch(exec, s));
   return ISL_OK;
 }
 
@@ -1179,6 +1275,8 @@ int isl_net_destroy(isl_net* net) {
   }
   if (net->d_flag) (void)hipFree(net->d_flag);
   if (net->d_trips) (void)hipFree(net->d_trips);
+  drop_all_graphs(net);
+  if (net->cap_stream) (void)hipStreamDestroy(net->cap_stream);
   for (auto& kv : net->plans) {
     if (kv.second.tab) (void)hipFree(kv.second.tab);
     if (kv.second.ks) (void)hipFree(kv.second.ks);
@@ -1396,6 +1494,13 @@ int isl_net_set_algo(isl_net* net, int algo) {
 }
 
 int isl_net_get_algo(const isl_net* net) { return net ? net->algo : fail(ISL_E_ARG, "net is NULL"); }
+
+int isl_net_set_graph(isl_net* net, int on) {
+  if (!net) return fail(ISL_E_ARG, "net is NULL");
+  if (on < 0 || on > 1) return fail(ISL_E_ARG, "graph mode must be 0 or 1");
+  net->graph = on;
+  return ISL_OK;
+}
 
 int isl_net_set_split_k(isl_net* net, int mode) {
   if (!net) return fail(ISL_E_ARG, "net is NULL");

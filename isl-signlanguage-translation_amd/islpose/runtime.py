@@ -26,7 +26,7 @@ EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destr
            "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops",
            "isl_sign_param_count", "isl_sign_classify", "isl_net_set_split_k", "isl_net_arena_info",
            "isl_debug_np_sum", "isl_hand_post_crops", "isl_net_check_async", "isl_net_range_info",
-           "isl_net_op_info"]
+           "isl_net_op_info", "isl_net_set_graph"]
 
 
 class IslCaps(ctypes.Structure):
@@ -93,6 +93,7 @@ def lib():
     L.isl_hand_post.argtypes = [vp, i32, i32, i32, i32, ctypes.POINTER(IslScaleGeom), ctypes.POINTER(vp), vp, vp]
     L.isl_sign_param_count.argtypes = [i32, i32, ctypes.POINTER(i64)]
     L.isl_net_set_split_k.argtypes = [vp, i32]
+    L.isl_net_set_graph.argtypes = [vp, i32]
     L.isl_net_arena_info.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i32)]
     L.isl_sign_classify.argtypes = [vp, i32, i32, i32, vp, i32, vp, vp]
     L.isl_debug_np_sum.argtypes = [vp, i64, vp, vp]
@@ -274,6 +275,12 @@ class Net:
         mode = {True: 2, False: 0}.get(mode, mode) if isinstance(mode, bool) else int(mode)
         check(lib().isl_net_set_split_k(self.h, mode), "isl_net_set_split_k")
         self.split_k = mode
+
+    def set_graph(self, on: bool):
+        """Replay the conv chain as a HIP graph after its first runs (isl_net_set_graph;
+        default on, env ISLPOSE_NET_GRAPH=0 turns it off): the same kernels and bits, without
+        the per-launch host cost that bounds batch-1 frames."""
+        check(lib().isl_net_set_graph(self.h, 1 if on else 0), "isl_net_set_graph")
 
     def algo_scope(self, algo: str):
         import contextlib

@@ -551,3 +551,42 @@ def test_x3_pps2_small_grids(net25, w25, monkeypatch):
     assert _rel(paf.cpu().numpy(), p0.cpu().numpy()) < 1e-5 and _rel(heat.cpu().numpy(), h0.cpu().numpy()) < 1e-5
     rp, rh = cpu_ref.make_net_fn("body25", w25)(frames[:1])
     assert _rel(paf[:1].cpu().numpy(), rp) < TOL and _rel(heat[:1].cpu().numpy(), rh) < TOL
+
+
+@pytest.mark.parametrize("n", [1, 4])
+def test_graph_replay_bit_identical(w25, n, monkeypatch):
+    """The conv chain replayed as a HIP graph (isl_net_set_graph, default on): the first run
+    of a key is eager, the second captures, later runs replay -- every run's maps equal the
+    eager net's bit for bit, the op variants are those of the eager run, a changed ISLPOSE_*
+    switch is a new key, and new weights drop the captured launches (their scales are kernel
+    arguments)."""
+    monkeypatch.delenv("ISLPOSE_NET_GRAPH", raising=False)
+    eager = rt.Net(rt.ISL_BODY25)
+    eager.load_weights(w25)
+    eager.set_graph(False)
+    g = rt.Net(rt.ISL_BODY25)
+    g.load_weights(w25)
+    xs = [torch.from_numpy(_inputs(n, 184, 328, seed=300 + k)).cuda() for k in range(4)]
+    ref = [eager.forward(x) for x in xs]
+    var0 = eager.op_variants()
+    for k, x in enumerate(xs):   # eager, capture, replay, replay
+        paf, heat = g.forward(x)
+        assert torch.equal(paf, ref[k][0]) and torch.equal(heat, ref[k][1]), k
+        assert g.op_variants() == var0, k
+    # another switch value: a new key (eager, then captured) with its own variants
+    monkeypatch.setenv("ISLPOSE_X3_DEEP", "0")
+    e2 = [eager.forward(x) for x in xs[:3]]
+    for k in range(3):
+        paf, heat = g.forward(xs[k])
+        assert torch.equal(paf, e2[k][0]) and torch.equal(heat, e2[k][1]), k
+    assert g.op_variants() == eager.op_variants()
+    monkeypatch.delenv("ISLPOSE_X3_DEEP")
+    # new weights (other power-of-two scales): the old graphs are dropped
+    w2 = {k: v * 0.5 for k, v in w25.items()}
+    eager.load_weights(w2)
+    g.load_weights(w2)
+    for k in range(3):
+        r = eager.forward(xs[k])
+        paf, heat = g.forward(xs[k])
+        assert torch.equal(paf, r[0]) and torch.equal(heat, r[1]), k
+    torch.cuda.synchronize()

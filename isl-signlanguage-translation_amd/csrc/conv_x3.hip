@@ -1186,21 +1186,49 @@ double conv_x3_rgb_mfma_flops(const ConvLaunch& c) {
 
 // Split-K reduction: the ranges' sums added in range order (the order of the in-block
 // ranges, so both give the same bits), then the epilogue of conv_x3_f16 (x 2^-s,
-// bias, activation, range check, masked stores).  One thread per (frame, 4-channel
-// group, pixel).
+// bias, activation, range check, masked stores).  One thread per (frame, chunk, pixel,
+// 4-channel half): neighbouring lanes read the two halves of a pixel's 32-byte chunk, so a
+// wave's loads and stores are contiguous.  The ranges' loads are all issued before the first
+// add (up to 8 in flight; the batch-1 frames' reduces had waited on one range at a time:
+// 5.0 us per launch at 23x41).
+template <int S>
+__device__ __forceinline__ f32x4 x3_sum_ranges(const float* p, size_t stride) {
+  f32x4 part[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) part[k] = __builtin_nontemporal_load((const f32x4*)(p + k * stride));
+  f32x4 sum = part[0];
+#pragma unroll
+  for (int k = 1; k < S; ++k) sum += part[k];
+  return sum;
+}
+
 __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
-  const int HW = a.H * a.W, g4 = (a.cout + 3) / 4;
+  const int HW = a.H * a.W, c8 = (a.cout + 7) / 8;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)a.nfr * g4 * HW) return;
-  const int m = (int)(i % HW);
-  const long long r = i / HW;
-  const int g = (int)(r % g4), n = (int)(r / g4);
-  const int co = 4 * g, c8 = (a.cout + 7) / 8;
+  if (i >= (long long)a.nfr * c8 * HW * 2) return;
+  const int h = (int)(i & 1);
+  const long long q = i >> 1;
+  const int m = (int)(q % HW);
+  const long long r = q / HW;
+  const int cc = (int)(r % c8), n = (int)(r / c8);
+  const int co = 8 * cc + 4 * h;
+  if (co >= a.cout) return;
   const size_t plane = (size_t)HW * 8;
-  const float* p = a.ws + ((size_t)n * c8 + (co >> 3)) * plane + (size_t)m * 8 + (co & 7);
+  const float* p = a.ws + ((size_t)n * c8 + cc) * plane + (size_t)m * 8 + 4 * h;
   const size_t split_stride = (size_t)a.nfr * c8 * plane;
-  f32x4 sum = *(const f32x4*)p;
-  for (int k = 1; k < a.ksplit; ++k) sum += *(const f32x4*)(p + k * split_stride);
+  f32x4 sum;
+  switch (a.ksplit) {   // uniform: one straight-line body per range count (loads in flight together)
+    case 2: sum = x3_sum_ranges<2>(p, split_stride); break;
+    case 3: sum = x3_sum_ranges<3>(p, split_stride); break;
+    case 4: sum = x3_sum_ranges<4>(p, split_stride); break;
+    case 5: sum = x3_sum_ranges<5>(p, split_stride); break;
+    case 6: sum = x3_sum_ranges<6>(p, split_stride); break;
+    case 7: sum = x3_sum_ranges<7>(p, split_stride); break;
+    case 8: sum = x3_sum_ranges<8>(p, split_stride); break;
+    default:
+      sum = *(const f32x4*)p;
+      for (int k = 1; k < a.ksplit; ++k) sum += *(const f32x4*)(p + k * split_stride);
+  }
   const f32x4 b = *(const f32x4*)(a.bias + co);
   f32x4 v;
 #pragma unroll
@@ -1217,8 +1245,8 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) bad |= co + e < a.cout && !(__builtin_fabsf(v[e]) < 65504.f);
   const int y = m / a.W, x = m - y * a.W, Wo = a.W + 2 * a.out_pad;
-  float* oc = a.out + (size_t)n * a.out_fs + (size_t)(co >> 3) * a.out_chs +
-              (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8 + (co & 7);
+  float* oc = a.out + (size_t)n * a.out_fs + (size_t)cc * a.out_chs +
+              (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8 + 4 * h;
   if (co + 3 < a.cout) {
     *(f32x4*)oc = v;
   } else {
@@ -1304,7 +1332,7 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   if constexpr (SPLIT) {
     // fold_out: every consumer sums the partials in its staging (X3Fold), no reduce launch
     if (!c.fold_out) {
-      const long long nt = (long long)c.n * ((c.cout + 3) / 4) * c.H * c.W;
+      const long long nt = (long long)c.n * ((c.cout + 7) / 8) * 2 * c.H * c.W;
       hipLaunchKernelGGL(x3_splitk_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, a);
     }
   } else {

@@ -1216,6 +1216,9 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
   const size_t plane = (size_t)HW * 8;
   const float* p = a.ws + ((size_t)n * c8 + cc) * plane + (size_t)m * 8 + 4 * h;
   const size_t split_stride = (size_t)a.nfr * c8 * plane;
+  // the epilogue's operands requested with the partials, not one round trip after them
+  const f32x4 b = *(const f32x4*)(a.bias + co);
+  const f32x4 sl = a.act == ACT_PRELU ? *(const f32x4*)(a.slope + co) : f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 sum;
   switch (a.ksplit) {   // uniform: one straight-line body per range count (loads in flight together)
     case 2: sum = x3_sum_ranges<2>(p, split_stride); break;
@@ -1229,7 +1232,6 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
       sum = *(const f32x4*)p;
       for (int k = 1; k < a.ksplit; ++k) sum += *(const f32x4*)(p + k * split_stride);
   }
-  const f32x4 b = *(const f32x4*)(a.bias + co);
   f32x4 v;
 #pragma unroll
   for (int e = 0; e < 4; ++e) v[e] = sum[e] * a.wscale_inv + b[e];
@@ -1237,7 +1239,6 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
   } else if (a.act == ACT_PRELU) {
-    const f32x4 sl = *(const f32x4*)(a.slope + co);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
   }

@@ -257,8 +257,11 @@ def gpu_main(args, rank, local, world):
                 self.k = 0
                 # D2H of the records on a copy stream: it overlaps the next step's preprocess and
                 # net; the next post (which rewrites d_res) waits for it, and the timed region's
-                # closing device synchronize includes it
-                self.cs = torch.cuda.Stream(dev)
+                # closing device synchronize includes it.  Small records (batch 1: ~0.1 MB, a
+                # ~5 us blit) are copied on the post's own stream instead: the cross-queue wait
+                # the copy stream needs costs more (~14 us between the net and the post)
+                self.cs = torch.cuda.Stream(dev) \
+                    if self.d_res.numel() > (1 << 20) or os.environ.get("ISLPOSE_BENCH_COPY_STREAM") == "1" else None
                 self.copied = None
 
         lanes = [Lane(s) for s in range(S)]
@@ -286,7 +289,7 @@ def gpu_main(args, rank, local, world):
                 else:
                     ln.net.run(stream=ln.stream)
                 e1 = mark(ln.stream)
-                if ln.pstream is not ln.stream:
+                if ln.pstream is not ln.stream:   # (a wait on the stream's own event is a barrier packet)
                     ln.pstream.wait_event(e1)
                 if ln.copied is not None:
                     ln.pstream.wait_event(ln.copied)
@@ -297,11 +300,15 @@ def gpu_main(args, rank, local, world):
                     ln.maps_free[ln.k & 1] = e2
                     ln.k += 1
                 marks.append((e0, e1, e2))
-                ln.cs.wait_event(e2)
-                with torch.cuda.stream(ln.cs):
-                    ln.h_res.copy_(ln.d_res, non_blocking=True)
-                ln.copied = torch.cuda.Event()
-                ln.copied.record(ln.cs)
+                if ln.cs is None:
+                    with torch.cuda.stream(ln.pstream):
+                        ln.h_res.copy_(ln.d_res, non_blocking=True)
+                else:
+                    ln.cs.wait_event(e2)
+                    with torch.cuda.stream(ln.cs):
+                        ln.h_res.copy_(ln.d_res, non_blocking=True)
+                    ln.copied = torch.cuda.Event()
+                    ln.copied.record(ln.cs)
             for ln in lanes:
                 if ln.stream is not main_stream:
                     main_stream.wait_stream(ln.stream)

@@ -215,6 +215,7 @@ struct isl_net {
     // different sizes may be in flight on different streams at once (the hand scales)
     void* tab = nullptr;
     size_t tab_bytes = 0;
+    std::vector<char> tab_host;   // what `tab` holds (upload_tab skips an identical table)
     float* ks = nullptr;
     size_t ks_floats = 0;
     // split-K fold plan for the current batch size (plan_fold): per op, the offset of a
@@ -1365,6 +1366,13 @@ int isl_net_forward(isl_net* net, const float* d_x, int n, int h, int w, float* 
 static int upload_tab(isl_net* net, hipStream_t s) {
   const size_t bytes = net->h_tab.size();
   isl_net::Arena& ar = *net->cur;
+  // the same frames geometry as the last upload into this arena's table (per-frame callers,
+  // a video's batches): the device copy already holds it.  Only upload_tab writes it, in
+  // stream order, so skipping the pageable copy (a blit plus a host-side stall) is safe
+  if (ar.tab && ar.tab_host == net->h_tab) {
+    net->d_tab = ar.tab;
+    return ISL_OK;
+  }
   if (bytes > ar.tab_bytes) {
     if (ar.tab) HIP_OK(hipFree(ar.tab));
     ar.tab = nullptr;
@@ -1373,6 +1381,7 @@ static int upload_tab(isl_net* net, hipStream_t s) {
     ar.tab_bytes = bytes;
   }
   HIP_OK(hipMemcpyAsync(ar.tab, net->h_tab.data(), bytes, hipMemcpyHostToDevice, s));
+  ar.tab_host = net->h_tab;
   net->d_tab = ar.tab;
   return ISL_OK;
 }

@@ -260,8 +260,9 @@ def gpu_main(args, rank, local, world):
                 # closing device synchronize includes it.  Small records (batch 1: ~0.1 MB, a
                 # ~5 us blit) are copied on the post's own stream instead: the cross-queue wait
                 # the copy stream needs costs more (~14 us between the net and the post)
-                self.cs = torch.cuda.Stream(dev) \
-                    if self.d_res.numel() > (1 << 20) or os.environ.get("ISLPOSE_BENCH_COPY_STREAM") == "1" else None
+                cs_env = os.environ.get("ISLPOSE_BENCH_COPY_STREAM")   # 1 / 0: force either (A/B)
+                use_cs = cs_env == "1" if cs_env in ("0", "1") else self.d_res.numel() > (1 << 20)
+                self.cs = torch.cuda.Stream(dev) if use_cs else None
                 self.copied = None
 
         lanes = [Lane(s) for s in range(S)]

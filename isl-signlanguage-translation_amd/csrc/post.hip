@@ -322,6 +322,11 @@ constexpr int NMS_SEG = 14;                        // g outputs per thread in th
 // with resize_sep_kernel's exact operation order.  Only scale 1/8 is fused.
 constexpr int NMS_SRC_ROWS = 16;
 constexpr int NMS_SRC_COLS = 48;                   // source columns (218 / 8 + 5 = 33 at scale 1/8; 42 at 1/5.9)
+// The wide window (Mode R at 368 x 656: the stage-2 resize is x2, a tile reads ~26 x 114 source
+// values): 72 KB of LDS per block, two blocks per CU, against writing and re-reading 0.8 GB of
+// full-resolution heat planes per 32 frames -- measured slower, opt-in (fused_wide_enabled).
+constexpr int NMS_WSRC_ROWS = 28;
+constexpr int NMS_WSRC_COLS = 120;
 
 // [min, max] of reflect_idx(i, n) over i in [lo, hi]
 __device__ __forceinline__ void reflect_range(int lo, int hi, int n, int* a, int* b) {
@@ -355,7 +360,7 @@ __device__ __forceinline__ void fused_window(const MapSrc& m, int H, int W, int 
 constexpr double CUBIC_ABS_SUM_SQ = 1.890625;      // max over t of (sum_k |cubic_k(t)|)^2, A = -0.75
 
 // planes: [n*nparts][H][W] (T = float or double); mask: [n*nparts][H][words]
-template <typename T, bool FUSED>
+template <typename T, bool FUSED, int WR = NMS_SRC_ROWS, int WC = NMS_SRC_COLS>
 __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, int W, int words,
                                           unsigned long long* __restrict__ mask, double thre, int mode_hand,
                                           const MapSrc& m, int nch, int plane, int by, int bx) {
@@ -363,9 +368,9 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
   // horizontal pass holds its v run in registers across a barrier) -> 31 KB,
   // so 4 blocks fit a CU and hide each other's load latency
   __shared__ double s_v[NMS_VR][NMS_VC];
-  __shared__ float s_hz[FUSED ? NMS_SRC_ROWS : 1][FUSED ? NMS_VC : 1];
+  __shared__ float s_hz[FUSED ? WR : 1][FUSED ? NMS_VC : 1];
   __shared__ int4 s_ti[FUSED ? NMS_IR : 1];
-  __shared__ float s_low[FUSED ? NMS_SRC_ROWS : 1][FUSED ? NMS_SRC_COLS : 1];
+  __shared__ float s_low[FUSED ? WR : 1][FUSED ? WC : 1];
   __shared__ float4 s_tb[FUSED ? NMS_IR : 1];
   __shared__ int s_live;
   __shared__ double s_cmax[NMS_VC];   // max |in| of every window column (word liveness)
@@ -400,9 +405,9 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
     const float* b = m.base + (size_t)f * m.fs + chan_off(m, c);
     int sr0, nsr, sc0, nsc;
     fused_window(m, H, W, y0, x0, &sr0, &nsr, &sc0, &nsc);
-    if (nsr > NMS_SRC_ROWS) __builtin_trap();   // the host fuses only scale 1/8, tiles of 42 rows
+    if (nsr > WR) __builtin_trap();   // the host picks a window that holds the tile's source rows
     // the low-res window is staged in LDS: one coalesced pass, reused by the resize
-    if (nsc > NMS_SRC_COLS) __builtin_trap();
+    if (nsc > WC) __builtin_trap();
     float amax = 0.f;
     for (int i = tid; i < nsr * nsc; i += 256) {
       const int r = i / nsc, cc = i - r * nsc;
@@ -540,7 +545,7 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
   }
 }
 
-template <typename T, bool FUSED>
+template <typename T, bool FUSED, int WR = NMS_SRC_ROWS, int WC = NMS_SRC_COLS>
 __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ planes, int H, int W, int words,
                                                         unsigned long long* __restrict__ mask, double thre,
                                                         int mode_hand, MapSrc m, int nch, const int* __restrict__ live,
@@ -553,7 +558,7 @@ __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ pla
     for (int k = blockIdx.x; k < cnt; k += gridDim.x) {
       const int t = live[k];
       const int bx = t % tiles_x, r = t / tiles_x, by = r % tiles_y, plane = r / tiles_y;
-      blur_tile<T, true>(planes, H, W, words, mask, thre, mode_hand, m, nch, plane, by, bx);
+      blur_tile<T, true, WR, WC>(planes, H, W, words, mask, thre, mode_hand, m, nch, plane, by, bx);
       __syncthreads();   // LDS reuse by the next tile
     }
   }
@@ -563,6 +568,7 @@ __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ pla
 // (one wave per tile at a time); live tiles are appended to `live` with one atomic
 // per block (order irrelevant: every tile owns its mask words).
 constexpr int TL_TILES = 16;   // 4 tiles per wave: enough blocks to hide the load latency
+template <int WR, int WC>
 __global__ void __launch_bounds__(256) tile_live_kernel(MapSrc m, int nch, int H, int W, int tiles_x, int tiles_y,
                                                         int n_tiles, double thre, int* __restrict__ live,
                                                         int* __restrict__ live_count) {
@@ -578,11 +584,11 @@ __global__ void __launch_bounds__(256) tile_live_kernel(MapSrc m, int nch, int H
       int sr0, nsr, sc0, nsc;
       fused_window(m, H, W, by * NMS_TY, bx * NMS_TX, &sr0, &nsr, &sc0, &nsc);
       float amax = 0.f;
-      if (nsr > NMS_SRC_ROWS || nsc > NMS_SRC_COLS) __builtin_trap();   // host fuses scale 1/8 only
-      if (lane < nsc) {   // nsc <= NMS_SRC_COLS < 64: one column per lane, all rows in flight
-        const float* col = b + (size_t)(sc0 + lane) * m.xs + (size_t)sr0 * m.ys;
+      if (nsr > WR || nsc > WC) __builtin_trap();   // the host picks a window that holds them
+      for (int cc = lane; cc < nsc; cc += 64) {   // one column per lane, all rows in flight
+        const float* col = b + (size_t)(sc0 + cc) * m.xs + (size_t)sr0 * m.ys;
 #pragma unroll
-        for (int rr = 0; rr < NMS_SRC_ROWS; ++rr)
+        for (int rr = 0; rr < WR; ++rr)
           if (rr < nsr) amax = fmaxf(amax, fabsf(col[(size_t)rr * m.ys]));
       }
       for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
@@ -1960,6 +1966,16 @@ static bool fused_blur_enabled() {
   return !(e && e[0] == '0');
 }
 
+// ISLPOSE_FUSED_WIDE=1: two-stage frames whose stage-2 scale needs the wide LDS window
+// (Mode R at 368 x 656) resize on the fly in blur_nms too (A/B; per call).  Off by default:
+// measured slower than materialising the planes (Mode R batch-32 post 1.54 -> 1.61 ms, batch
+// 1 0.19 -> 0.22 ms, profiles/r03/wide/): two 72 KB blocks per CU and a 28-row horizontal
+// pass per tile cost more than the 0.8 GB write and re-read.
+static bool fused_wide_enabled() {
+  const char* e = getenv("ISLPOSE_FUSED_WIDE");
+  return e && e[0] == '1';
+}
+
 static int post_fail(int code, const char* msg) {
   set_error(msg);
   return code;
@@ -2031,9 +2047,14 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   // second resize is a strong upsampling whose full-resolution planes cost more HBM
   // traffic than the on-the-fly resize; fused too when a blur tile's source window fits
   // the LDS window (~1/5.2 and below; at 368 x 656, scale 1/2, it does not)
-  const bool fuse2 = !multi && !(geom[0].valid_h == H && geom[0].valid_w == W) &&
-                     41.0 * geom[0].valid_h / H + 6.0 <= NMS_SRC_ROWS &&
-                     217.0 * geom[0].valid_w / W + 6.0 <= NMS_SRC_COLS;
+  // (the wide window takes stage-2 scales down to ~1/2: Mode R at 368 x 656)
+  auto window_fits = [&](int rows, int cols) {
+    return 41.0 * geom[0].valid_h / H + 6.0 <= rows && 217.0 * geom[0].valid_w / W + 6.0 <= cols;
+  };
+  const bool two = !multi && !(geom[0].valid_h == H && geom[0].valid_w == W);
+  const bool fuse2_small = two && window_fits(NMS_SRC_ROWS, NMS_SRC_COLS);
+  const bool fuse2 = two && (fuse2_small || (window_fits(NMS_WSRC_ROWS, NMS_WSRC_COLS) && fused_wide_enabled()));
+  const bool wide = fuse2 && !fuse2_small;
   const bool fused = !multi && ((geom[0].valid_h == H && geom[0].valid_w == W) || fuse2) && fused_blur_enabled();
   const size_t heat_bytes = fused ? 0 : (size_t)n * nparts * H * W * (multi ? 8 : 4);
   size_t mid_bytes = 0;
@@ -2131,12 +2152,22 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     const int n_tiles = (int)(gb.x * gb.y * gb.z);
     PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));
     PHIP(hipMemsetAsync(live_count, 0, sizeof(int), s));
-    hipLaunchKernelGGL(tile_live_kernel, dim3((n_tiles + TL_TILES - 1) / TL_TILES), dim3(256), 0, s, fused_src, nparts, H, W, (int)gb.x,
-                       (int)gb.y, n_tiles, 0.1, live, live_count);
-    PHIP(hipGetLastError());
-    hipLaunchKernelGGL((blur_nms_kernel<float, true>), dim3(std::min(n_tiles, 256 * 8)), dim3(256), 0, s,
-                       (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts, live, live_count,
-                       (int)gb.x, (int)gb.y);
+    const dim3 tl((n_tiles + TL_TILES - 1) / TL_TILES);
+    if (wide) {
+      hipLaunchKernelGGL((tile_live_kernel<NMS_WSRC_ROWS, NMS_WSRC_COLS>), tl, dim3(256), 0, s, fused_src, nparts, H, W,
+                         (int)gb.x, (int)gb.y, n_tiles, 0.1, live, live_count);
+      PHIP(hipGetLastError());
+      hipLaunchKernelGGL((blur_nms_kernel<float, true, NMS_WSRC_ROWS, NMS_WSRC_COLS>), dim3(std::min(n_tiles, 256 * 4)),
+                         dim3(256), 0, s, (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts, live,
+                         live_count, (int)gb.x, (int)gb.y);
+    } else {
+      hipLaunchKernelGGL((tile_live_kernel<NMS_SRC_ROWS, NMS_SRC_COLS>), tl, dim3(256), 0, s, fused_src, nparts, H, W,
+                         (int)gb.x, (int)gb.y, n_tiles, 0.1, live, live_count);
+      PHIP(hipGetLastError());
+      hipLaunchKernelGGL((blur_nms_kernel<float, true>), dim3(std::min(n_tiles, 256 * 8)), dim3(256), 0, s,
+                         (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts, live, live_count,
+                         (int)gb.x, (int)gb.y);
+    }
   } else
     hipLaunchKernelGGL((blur_nms_kernel<float, false>), gb, dim3(256), 0, s, (const float*)heat, H, W, words, mask,
                        0.1, 0, MapSrc{}, 0, nullptr, nullptr, 0, 0);

@@ -271,11 +271,14 @@ def test_fused_resize_blur_matches_unfused(est25, monkeypatch, H, W):
         assert np.array_equal(fused[i].subset, subset), i
 
 
-@pytest.mark.parametrize("H,W", [(1000, 1000), (1080, 1920)])
+@pytest.mark.parametrize("H,W", [(1000, 1000), (1080, 1920), (368, 656), (400, 520)])
 def test_fused_two_stage_post_matches_unfused(est25, monkeypatch, H, W):
-    """Mode R on large frames (scale 0.5: net 184 px tall, then a >5x second resize): the
-    second resize fused into blur_nms (no full-resolution planes) == the materialised
-    two-kernel path == the oracle, on noisy maps around the 0.1 threshold."""
+    """Mode R (scale 0.5: net 184 px tall, then the second resize: >5x on large frames, the
+    small LDS window; ~2x at 368 x 656 / 400 x 520, the wide window): the second resize fused
+    into blur_nms (no full-resolution planes) == the materialised two-kernel path == the
+    oracle, on noisy maps around the 0.1 threshold.  The wide window is opt-in
+    (ISLPOSE_FUSED_WIDE=1: measured slower than the materialised planes)."""
+    monkeypatch.setenv("ISLPOSE_FUSED_WIDE", "1")
     geoms = [g[1:] for g in scale_geometry(H, W, (0.5,))]
     nh, nw = geoms[0][0] // 8, geoms[0][1] // 8
     rng = np.random.RandomState(H + W)

@@ -1998,8 +1998,10 @@ static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mo
     while (ty > 1 && (ty - 1) * m.scy + 5.0 > (double)RS_MAXR) --ty;
   const long long ty_tiles = (oh + ty - 1) / ty;
   if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "resize: output too tall");
-  // 128-column blocks where they leave fewer idle lanes (ow = 328: 384 vs 512 lanes)
-  if ((ow + 127) / 128 * 128 < (ow + RS_TX - 1) / RS_TX * RS_TX)
+  // 128-column blocks unless 256 pads less (it never does): fewer idle lanes (ow = 328: 384 vs
+  // 512), and at equal padding (ow = 656) twice the resident blocks: Mode R batch-32 post
+  // 1.51 / 1.49 -> 1.47 / 1.47 ms; 32 or 16 rows per block lost (profiles/r03/rsty/)
+  if ((ow + 127) / 128 * 128 <= (ow + RS_TX - 1) / RS_TX * RS_TX)
     hipLaunchKernelGGL(resize_sep_kernel<128>, dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128), dim3(128), 0, s,
                        m, nch, oh, ow, ty, mode, div_f, out);
   else

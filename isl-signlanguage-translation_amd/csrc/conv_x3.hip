@@ -1376,10 +1376,14 @@ static int device_cus() {
 // batch 32) it loses 10-20 % (profiles/r03/halfco_ab/).  Same bits either way.
 // ISLPOSE_X3_HALFCO=0 off, =1 every 128-channel launch of the family (read per launch; A/B).
 static bool x3_halfco(const ConvLaunch& c) {
-  const char* e = getenv("ISLPOSE_X3_HALFCO");
   if (c.ks > 7 || c.fold) return false;
+#ifdef ISLPOSE_DEV
+  // development build only (A/B of profiles/r03/halfco_ab/): =0 off, =1 every 128-channel
+  // launch of the family (measured slower at one block per CU, so not in the product)
+  const char* e = getenv("ISLPOSE_X3_HALFCO");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
+#endif
   return c.ks <= 3 && c.ksplit > 1 && c.ws;
 }
 
@@ -1410,6 +1414,7 @@ static bool x3_deep(const ConvLaunch& c) {
 // -1.2 %, profiles/r03/pps2_ab/), so it is off by default.  ISLPOSE_X3_PPS2=1: on (A/B; read
 // per launch).
 static int x3_canonical_ranges(const ConvLaunch& c);
+#ifdef ISLPOSE_DEV
 static bool x3_pps2(const ConvLaunch& c) {
   // the fold A/B (ISLPOSE_X3_FOLD=1) runs its consumers on one-pair steps, so every layer of a
   // frame keeps one order at every batch size only with PPS2 off there
@@ -1423,6 +1428,9 @@ static bool x3_pps2(const ConvLaunch& c) {
   const int pps = (pairs + S - 1) / S;
   return pairs % 2 == 0 && pps % 2 == 0;
 }
+#else
+static bool x3_pps2(const ConvLaunch&) { return false; }   // rejected (profiles/r03/pps2_ab/): dev build only
+#endif
 
 static int x3_canonical_ranges(const ConvLaunch& c) {
   const int pairs = (c.cin_chunks + 1) / 2;
@@ -1539,11 +1547,15 @@ static bool x3_union(const ConvLaunch& c) {
 
 // The row union on v_mfma_f32_16x16x32_f16 (VAR 131072) for 128-channel tiles with an even
 // number of chunk pairs.  ISLPOSE_X3_M16=0|1 (read per launch: A/B in one process).
+#ifdef ISLPOSE_DEV
 static bool x3_m16(const ConvLaunch& c) {
   const char* e = getenv("ISLPOSE_X3_M16");
   const bool on = e && e[0] == '1';
   return on && c.ks == 3 && c.bco == 128 && ((c.cin_chunks + 1) / 2) % 2 == 0;
 }
+#else
+static bool x3_m16(const ConvLaunch&) { return false; }    // rejected (profiles/r03/m16_ab/): dev build only
+#endif
 
 // K-range plan of a launch on the 128-pixel family: S ranges, computed across S blocks
 // per tile (split-K, partials through the workspace) when the plain grid has fewer
@@ -1589,14 +1601,18 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
         }
       }
 #endif
+#ifdef ISLPOSE_DEV
       const bool m16 = c.bco == 128 && x3_m16(c);
+      if (m16) {
+        if (c.vin) return launch_t<KS, 2, 8, 2, 2, 512 | 32768 | 131072, 4>(c, s);
+        return launch_t<KS, 2, 8, 2, 2, 512 | 131072, 4>(c, s);
+      }
+#endif
       if (c.vin) {
-        if (m16) return launch_t<KS, 2, 8, 2, 2, 512 | 32768 | 131072, 4>(c, s);
         if (c.bco == 128) return launch_t<KS, 2, 8, 2, 2, 512 | 32768, 4>(c, s);
         set_error("conv_x3: pooled-input staging without a variant (x3_vin_ok)");
         return hipErrorInvalidValue;
       }
-      if (m16) return launch_t<KS, 2, 8, 2, 2, 512 | 131072, 4>(c, s);
       switch (c.bco) {
         case 128: return launch_t<KS, 2, 8, 2, 2, 512, 4>(c, s);
         case 96: return launch_t<KS, 1, 16, 3, 1, 512, 4>(c, s);
@@ -1650,6 +1666,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   static const int more = getenv("ISLPOSE_X3_S8") ? atoi(getenv("ISLPOSE_X3_S8")) : 1;
   if (more) {
     {
+#ifdef ISLPOSE_DEV
       if constexpr (KS <= 3) {
         if (c.fold) {   // consumers of folded split-K partials (x3_fold_ok)
           switch (c.bco) {
@@ -1666,6 +1683,12 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
           return hipErrorInvalidValue;
         }
       }
+#else
+      if (c.fold) {
+        set_error("conv_x3: the split-K fold is a development-build variant");
+        return hipErrorInvalidValue;
+      }
+#endif
       if constexpr (KS <= 3) {
         if (x3_deep(c)) {   // prefetch two K steps ahead
           switch (c.bco) {
@@ -1680,6 +1703,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
           }
         }
       }
+#ifdef ISLPOSE_DEV
       if constexpr (KS <= 3) {
         if (x3_pps2(c)) {   // two chunk pairs per K step: twice the MFMAs between barriers
           switch (c.bco) {
@@ -1694,6 +1718,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
           }
         }
       }
+#endif
       if (c.bco == 128 && x3_halfco(c)) {   // two blocks of 4 waves (64co x 32px) per 128-channel tile
         if (split) return launch_t<KS, 1, 4, 2, 1, 2048 | 256, 4>(c, s);
         if (ranged) return launch_t<KS, 1, 4, 2, 1, 1024 | 256, 4>(c, s);

@@ -1971,10 +1971,14 @@ static bool fused_blur_enabled() {
 // measured slower than materialising the planes (Mode R batch-32 post 1.54 -> 1.61 ms, batch
 // 1 0.19 -> 0.22 ms, profiles/r03/wide/): two 72 KB blocks per CU and a 28-row horizontal
 // pass per tile cost more than the 0.8 GB write and re-read.
+#ifdef ISLPOSE_DEV
 static bool fused_wide_enabled() {
   const char* e = getenv("ISLPOSE_FUSED_WIDE");
   return e && e[0] == '1';
 }
+#else
+static bool fused_wide_enabled() { return false; }   // rejected: development build only
+#endif
 
 static int post_fail(int code, const char* msg) {
   set_error(msg);
@@ -2156,12 +2160,14 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     PHIP(hipMemsetAsync(live_count, 0, sizeof(int), s));
     const dim3 tl((n_tiles + TL_TILES - 1) / TL_TILES);
     if (wide) {
+#ifdef ISLPOSE_DEV
       hipLaunchKernelGGL((tile_live_kernel<NMS_WSRC_ROWS, NMS_WSRC_COLS>), tl, dim3(256), 0, s, fused_src, nparts, H, W,
                          (int)gb.x, (int)gb.y, n_tiles, 0.1, live, live_count);
       PHIP(hipGetLastError());
       hipLaunchKernelGGL((blur_nms_kernel<float, true, NMS_WSRC_ROWS, NMS_WSRC_COLS>), dim3(std::min(n_tiles, 256 * 4)),
                          dim3(256), 0, s, (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts, live,
                          live_count, (int)gb.x, (int)gb.y);
+#endif
     } else {
       hipLaunchKernelGGL((tile_live_kernel<NMS_SRC_ROWS, NMS_SRC_COLS>), tl, dim3(256), 0, s, fused_src, nparts, H, W,
                          (int)gb.x, (int)gb.y, n_tiles, 0.1, live, live_count);

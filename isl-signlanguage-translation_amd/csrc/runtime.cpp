@@ -17,7 +17,6 @@
 #include <string>
 #include <vector>
 
-#include <unistd.h>   // environ (run_key)
 
 #include "internal.h"
 #include "islpose.h"
@@ -232,8 +231,10 @@ struct isl_net {
     struct Graph {
       hipGraphExec_t exec = nullptr;
       std::vector<int> op_variant;
+      unsigned long long last_use = 0;
     };
     std::map<unsigned long long, Graph> graphs;
+    unsigned long long graph_clock = 0;
     std::map<unsigned long long, int> graph_seen;
   };
   std::map<long long, Arena> plans;
@@ -690,8 +691,18 @@ static size_t arena_budget() {
 
 // Instantiated graphs hold the pointers and scalars of the launches they captured: any
 // reallocation of a buffer they name (arena, split-K workspace, weights re-uploaded with new
-// scales) drops them.  hipGraphExecDestroy lets queued replays finish.
+// scales) drops them.  A replay may still be queued on any stream (the caller's, not ours), so
+// the device drains before an exec is destroyed: drops are rare (weights, workspace growth,
+// arena eviction, the per-arena cap), the wait is cheap next to them.
+static void destroy_exec(hipGraphExec_t exec) {
+  (void)hipDeviceSynchronize();
+  (void)hipGraphExecDestroy(exec);
+}
+
 static void drop_graphs(isl_net::Arena& ar) {
+  bool any = false;
+  for (auto& kv : ar.graphs) any |= kv.second.exec != nullptr;
+  if (any) (void)hipDeviceSynchronize();
   for (auto& kv : ar.graphs)
     if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
   ar.graphs.clear();
@@ -833,8 +844,12 @@ static bool pool_into_next_conv(const isl_net* net, size_t k) {
 // per run).  Off by default: at batch 1 (Mode R) the consumers' staging re-reads S partials
 // per element and kernel row, and the frame ran 427 -> 315 frames/s (profiles/r03/fold_ab/)
 static bool fold_enabled() {
+#ifdef ISLPOSE_DEV
   const char* e = getenv("ISLPOSE_X3_FOLD");
   return e && e[0] == '1';
+#else
+  return false;   // rejected: development build only
+#endif
 }
 
 // The conv launch of op k before the per-run adjustments (pools, wide 1x1 tiles, fold)
@@ -1111,16 +1126,40 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
 // launches it on the caller's stream; later runs replay it.  The kernels, their order and
 // arguments are those of the eager run: the same bits.  Timed runs (isl_net_set_timing) and
 // the split-K fold (its plan uploads a table) stay eager.
+// The switches the launch selection of this build reads (its kernel choice per launch), in a
+// fixed order, each hashed as name=value; -- so the key depends on their values only, not on
+// the order of environ or on unrelated ISLPOSE_* variables.
+static const char* const kRunKeySwitches[] = {
+    "ISLPOSE_X3_DEEP",   "ISLPOSE_RGB_CONV", "ISLPOSE_FUSED_POOL", "ISLPOSE_POOL_INPUT", "ISLPOSE_CONV_STAGING",
+    "ISLPOSE_X3_TILES",  "ISLPOSE_X3_UNION", "ISLPOSE_X3_HALF64",  "ISLPOSE_X3_WIDE7",   "ISLPOSE_X3_ACROSS",
+    "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67",
+#ifdef ISLPOSE_DEV
+    "ISLPOSE_X3_HALFCO", "ISLPOSE_X3_PPS2",  "ISLPOSE_X3_M16",     "ISLPOSE_X3_WINO",    "ISLPOSE_X3_ABL",
+#endif
+};
+
 static unsigned long long run_key(const isl_net* net) {
   unsigned long long h = 1469598103934665603ull;
   auto mix = [&](unsigned long long v) { h = (h ^ v) * 1099511628211ull; };
   mix((unsigned long long)net->pn);
   mix((unsigned long long)net->split_k + 16 * (unsigned long long)net->algo);
-  for (char** e = environ; e && *e; ++e)
-    if (!strncmp(*e, "ISLPOSE_", 8))
-      for (const char* c = *e; *c; ++c) mix((unsigned char)*c);
+  for (const char* name : kRunKeySwitches) {
+    const char* v = getenv(name);
+    for (const char* c = name; *c; ++c) mix((unsigned char)*c);
+    mix('=');
+    if (v)
+      for (const char* c = v; *c; ++c) mix((unsigned char)*c);
+    else
+      mix(0x100);   // unset differs from set-but-empty
+    mix(';');
+  }
   return h;
 }
+
+// instantiated graphs kept per arena (least recently launched dropped beyond it): ragged hand
+// crop batches and A/B switches would otherwise add executables without bound
+constexpr size_t kGraphsPerArena = 8;
+constexpr size_t kGraphSeenCap = 64;
 
 static bool graph_enabled(const isl_net* net) {
   const char* e = getenv("ISLPOSE_NET_GRAPH");
@@ -1135,9 +1174,11 @@ static int run_ops(isl_net* net, hipStream_t s) {
   auto g = ar.graphs.find(key);
   if (g != ar.graphs.end()) {
     net->op_variant = g->second.op_variant;
+    g->second.last_use = ++ar.graph_clock;
     HIP_OK(hipGraphLaunch(g->second.exec, s));
     return ISL_OK;
   }
+  if (ar.graph_seen.size() >= kGraphSeenCap && !ar.graph_seen.count(key)) ar.graph_seen.clear();
   int& seen = ar.graph_seen[key];
   if (seen++ < 1) return run_ops_eager(net, s);
   if (!net->cap_stream) HIP_OK(hipStreamCreateWithFlags(&net->cap_stream, hipStreamNonBlocking));
@@ -1158,9 +1199,17 @@ static int run_ops(isl_net* net, hipStream_t s) {
     seen = -(1 << 30);
     return run_ops_eager(net, s);
   }
+  while (ar.graphs.size() >= kGraphsPerArena) {
+    auto lru = ar.graphs.begin();
+    for (auto j = ar.graphs.begin(); j != ar.graphs.end(); ++j)
+      if (j->second.last_use < lru->second.last_use) lru = j;
+    destroy_exec(lru->second.exec);
+    ar.graphs.erase(lru);
+  }
   isl_net::Arena::Graph& G = ar.graphs[key];
   G.exec = exec;
   G.op_variant = net->op_variant;
+  G.last_use = ++ar.graph_clock;
   HIP_OK(hipGraphLaunch(exec, s));
   return ISL_OK;
 }
@@ -1523,7 +1572,10 @@ int isl_net_check(isl_net* net, int clear) {
   if (!net->d_flag) return ISL_OK;
   HIP_OK(hipSetDevice(net->device));
   int f = 0;
-  HIP_OK(hipMemcpy(&f, net->d_flag, sizeof(int), hipMemcpyDeviceToHost));   // device-synchronising
+  // the convs ran on the caller's stream, which may be non-blocking (torch's): a null-stream
+  // copy alone would not wait for them
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(&f, net->d_flag, sizeof(int), hipMemcpyDeviceToHost));
   if (f && clear) {
     HIP_OK(hipMemset(net->d_flag, 0, sizeof(int)));
     ++net->range_trips_host;   // one trip per cleared flag (a check without clear counts nothing)
@@ -1548,7 +1600,10 @@ int isl_net_range_info(isl_net* net, int64_t* trips) {
   unsigned long long d = 0;
   if (net->d_trips) {
     HIP_OK(hipSetDevice(net->device));
-    HIP_OK(hipMemcpy(&d, net->d_trips, sizeof(d), hipMemcpyDeviceToHost));   // device-synchronising
+    // range_count_kernel runs on the caller's (non-blocking) stream, which a null-stream copy
+    // does not wait for: drain the device first
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(&d, net->d_trips, sizeof(d), hipMemcpyDeviceToHost));
   }
   *trips = (int64_t)(net->range_trips_host + (long long)d);
   return ISL_OK;

@@ -227,7 +227,9 @@ class BodyEstimator:
         batch's low-res maps into tensors of its own, the range check follows them on the
         current stream, and the post and the records' copy run on post_stream: the next
         launch's nets may start on the current stream at once, beside this post (the body
-        of a video's batch k+1 beside the post of batch k; bench.py's default step)."""
+        of a video's batch k+1 beside the post of batch k).  post_stream is opt-in: it
+        measured as a slowdown of the convs beside the fp64 blur; bench.py's
+        --post-overlap times the same overlap on its own step loop."""
         import torch
         n, H, W, _ = frames_t.shape
         geoms, pafs, heats = self.run_scales(frames_t, keep_maps=post_stream is not None)

@@ -42,8 +42,9 @@
 //   512   row union (3x3 on 512-pixel tiles): the three kernel rows of a chunk pair
 //         are staged once as one run, a third per ky step, by loader waves, while
 //         DMA waves stream the weights (role split, see the union loop);
-//   1024  canonical K ranges (in-block): the chunk pairs are summed in S ranges,
-//         each from zero, and the range sums added in order -- the same bits as 2048;
+//   1024  canonical K ranges (in-block): the chunk pairs are summed in S ranges, each from
+//         zero; the first h = ceil(S / 2) range sums are added in order, the others in order,
+//         then the two halves (x3_canonical_order) -- the same bits as 2048;
 //   2048  split-K across blocks: each block writes one range's sum, x3_splitk_reduce
 //         adds them in range order.  S depends on the layer shape only
 //         (x3_canonical_ranges), so a frame gives the same bits at any batch size
@@ -54,7 +55,18 @@
 //         compiled only with -DISLPOSE_DEV, never into libislpose.so).
 //   32768 pooled input (ConvLaunch::vin): the input is the pair-max buffer of the 2x2
 //         pool before this layer; staging takes the row-pair max (x3_vin_ok).
-//   131072 the row union on v_mfma_f32_16x16x32_f16 (products folded into K, x3_m16).
+//   131072 the row union on v_mfma_f32_16x16x32_f16 (products folded into K, x3_m16;
+//         development build only).
+//   32    two K groups per block (with 1024): waves [0, NW) sum the first half of the K ranges,
+//         waves [NW, 2 NW) the second half, each group on its own double buffers, one barrier
+//         per step for both; the halves meet in LDS at the end (small grids: one block per CU
+//         with twice the waves, so one group's step latency overlaps the other's MFMAs);
+//   16    the 1x1 pair Mconv6 -> Mconv7 in one launch (ConvLaunch::cout7): the block holds
+//         every Mconv6 output channel of its pixel tile in registers, turns the activated
+//         values into the split B operand of Mconv7 in place (the MFMA D layout of a 32-row
+//         tile is two K=16 B fragments once Mconv7's K is packed in that order, pack_x3_f7),
+//         each wave sums its 64 channels' Mconv7 products, and the waves' sums are added in
+//         wave order through LDS.  The Mconv6 output never goes to HBM.
 // conv_x3_rgb: the 3-channel first layers (conv1_1) with K packed as the 27 real
 // (ky, kx, c) values instead of 9 taps x 16 channels.
 #include <algorithm>
@@ -90,6 +102,13 @@ struct X3Args {
   int vin;                      // ConvLaunch::vin: in is the [n][chunk][2H][W][8] pair-max buffer of a pool
   const X3Fold* fold;           // VAR 8192: per input chunk, the split-K partials it is folded from
   int abl;                      // development (-DISLPOSE_DEV, ISLPOSE_X3_ABL): generic-loop ablations
+  // VAR 16 (the fused 1x1 pair): Mconv7's filters in the fused K order (pack_x3_f7), bias,
+  // PReLU slopes, activation, 2^-s and output channels; out / out_* describe Mconv7's output
+  const f16x8* wpk7;
+  const float* bias7;
+  const float* slope7;
+  float wscale7_inv;
+  int cout7, act7;
 };
 
 // u / d for 0 <= u < 2^20, d >= 1, through the fp32 reciprocal r = 1/d: (u + 0.5) / d sits
@@ -143,9 +162,13 @@ constexpr int x3_segmax(int bpx) { return bpx + 64; }
 constexpr int x3_segu_max() { return 856; }
 
 template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, int VAR, int OCC>
-__global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Args a) {
-  constexpr int NT = WAVES_M * WAVES_N * 64;
-  constexpr int NWAVES = WAVES_M * WAVES_N;
+__global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1), OCC) conv_x3_f16(X3Args a) {
+  // VAR 32: two K groups of WAVES_M x WAVES_N waves each (see the generic loop)
+  constexpr bool G2 = (VAR & 32) != 0;
+  constexpr int NG = G2 ? 2 : 1;
+  constexpr int NWAVES = WAVES_M * WAVES_N;      // waves per K group
+  constexpr int NTG = NWAVES * 64;               // threads per K group
+  constexpr int NT = NG * NTG;
   constexpr int BCO = WAVES_M * WM * 32;
   constexpr int BPX = WAVES_N * WN * 32;
   constexpr int P = KS / 2;
@@ -158,7 +181,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr int SEGP = SEGMAX + 1;               // + one dummy slot idle staging items write to
   constexpr int XSLAB = 2 * 2 * PPS * SEGP;      // 16-byte units: [hi|lo][chunk of the step][px]
   constexpr int BUF = WSLAB + XSLAB;
-  constexpr int IT = (2 * PPS * SEGMAX + NT - 1) / NT; // staging items (chunk, px) per thread
+  constexpr int IT = (2 * PPS * SEGMAX + NTG - 1) / NTG; // staging items (chunk, px) per thread of a group
   static_assert(WSLAB % 64 == 0, "weight slab is whole 1 KiB DMA pieces");
   static_assert(BPX <= SEGMAX, "segment must hold a tile");
   constexpr bool UNION = (VAR & 512) != 0;
@@ -172,9 +195,15 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   constexpr bool SIB = (VAR & 65536) != 0;
   constexpr int SEGUP = x3_segu_max() + 1;       // + dummy slot
   constexpr int XSLABU = 2 * 2 * SEGUP;          // [hi|lo][h][px]
-  constexpr int SMEM = UNION ? 2 * WSLAB + 2 * XSLABU : SIB ? 2 * WSLAB + XSLAB
-                     : (VAR & 128) ? 3 * WSLAB + 2 * XSLAB : 2 * BUF;
+  constexpr int SMEM0 = UNION ? 2 * WSLAB + 2 * XSLABU : SIB ? 2 * WSLAB + XSLAB
+                      : (VAR & 128) ? 3 * WSLAB + 2 * XSLAB : NG * 2 * BUF;
   static_assert(!(SIB && UNION), "one input buffer: generic loop only");
+  // VAR 16: Mconv6 -> Mconv7 fused (the epilogue below); its LDS: the epilogue parameters and
+  // the waves' Mconv7 sums of one pass (WAVES_N pixel tiles), [WAVES_M][WAVES_N * 32][F7_ROWS]
+  constexpr bool FUSE67 = (VAR & 16) != 0;
+  constexpr int F7_ROWS = 68;                    // 64 rows + 4 (staggers the banks of the pixel rows)
+  constexpr int F7_SMEM = FUSE67 ? ((2 * BCO + 128) * 4 + WAVES_M * WAVES_N * 32 * F7_ROWS * 4 + 15) / 16 : 0;
+  constexpr int SMEM = SMEM0 > F7_SMEM ? SMEM0 : F7_SMEM;
   static_assert(SMEM * 16 <= 160 * 1024, "LDS");
   constexpr bool RANGED = (VAR & 1024) != 0;
   constexpr bool SPLIT = (VAR & 2048) != 0;
@@ -197,6 +226,9 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   static_assert(!(FOLD && (VIN || UNION || M16 || KS > 3 || PPS > 1)), "fold: the generic loop of 1x1 / 3x3 layers");
   static_assert(!(UNION && (RANGED || SPLIT)), "K ranges run on the generic loop");
   static_assert(PPS == 1 || !(UNION || M16 || HALFCO || DEEP || FOLD || VIN), "two pairs per step: generic loop");
+  static_assert(!G2 || (RANGED && !SPLIT && !UNION && !M16 && !SIB && !DEEP && !FOLD && !VIN && !HALFCO && PPS == 1 &&
+                        !FUSE67 && !STAMP),
+                "two K groups: in-block K ranges on the plain generic loop");
   __shared__ f16x8 smem[SMEM];
 
   // XCD-aware tile order (conv.hip): co-tiles of a pixel tile, then neighbouring
@@ -229,9 +261,11 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   const float* in_f = a.in + (size_t)n * a.in_fs;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wave_m = wave % WAVES_M, wave_n = wave / WAVES_M;
+  const int grp = G2 ? __builtin_amdgcn_readfirstlane(wave / NWAVES) : 0;   // K group (VAR 32)
+  const int wave_g = wave - grp * NWAVES, tid_g = tid - grp * NTG;           // within the group
+  const int wave_m = wave_g % WAVES_M, wave_n = wave_g / WAVES_M;
   const int h = lane >> 5, l32 = lane & 31;
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave_g);
 
   int rel[WN];
 #pragma unroll
@@ -599,10 +633,10 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
   } else {
     // Generic loop: one step = (pair, ky); weights by LDS-DMA one step ahead, the
     // input row run register-staged one step ahead.
-    int ih[IT], ipx[IT];                 // staging items: tid + i*NT -> (chunk of the step, pixel)
+    int ih[IT], ipx[IT];                 // staging items: tid_g + i*NTG -> (chunk of the step, pixel)
 #pragma unroll
     for (int i = 0; i < IT; ++i) {
-      const int it = tid + i * NT;
+      const int it = tid_g + i * NTG;
       ih[i] = min(it / seg, 2 * PPS - 1);
       ipx[i] = it - ih[i] * seg;
       if (it >= 2 * PPS * seg) ipx[i] = -1;   // idle
@@ -640,13 +674,23 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
                 q0[k] = *(const f32x4*)pk;
                 q1[k] = *(const f32x4*)(pk + 4);
               }
-              f32x4 s0 = q0[0], s1 = q1[0];
+              // x3_canonical_order: the two halves of the ranges, each in order, then added
+              const int hh = (f.S + 1) / 2;
+              f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0, u0 = s0, u1 = s0;
 #pragma unroll
-              for (int k = 1; k < 8; ++k)
-                if (k < f.S) {
+              for (int k = 0; k < 8; ++k) {
+                if (k < hh) {
                   s0 += q0[k];
                   s1 += q1[k];
+                } else if (k < f.S) {
+                  u0 += q0[k];
+                  u1 += q1[k];
                 }
+              }
+              if (f.S > hh) {
+                s0 += u0;
+                s1 += u1;
+              }
               const f32x4 b0 = *(const f32x4*)f.bias, b1 = *(const f32x4*)(f.bias + 4);
               f32x4 v0, v1;
 #pragma unroll
@@ -690,9 +734,11 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
         }
       }
     };
-    auto wbuf = [&](int buf) __attribute__((always_inline)) { return smem + buf * (SIB || DEEP ? WSLAB : BUF); };
+    // VAR 32: each K group on its own pair of buffers
+    f16x8* const gsm = smem + grp * 2 * BUF;
+    auto wbuf = [&](int buf) __attribute__((always_inline)) { return gsm + buf * (SIB || DEEP ? WSLAB : BUF); };
     auto xbuf = [&](int buf) __attribute__((always_inline)) {
-      return SIB ? smem + 2 * WSLAB : DEEP ? smem + 3 * WSLAB + buf * XSLAB : smem + buf * BUF + WSLAB;
+      return SIB ? gsm + 2 * WSLAB : DEEP ? gsm + 3 * WSLAB + buf * XSLAB : gsm + buf * BUF + WSLAB;
     };
     auto store_x = [&](int buf) __attribute__((always_inline)) {
       f16x8* s = xbuf(buf);
@@ -742,31 +788,60 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
 #pragma unroll
       for (int kx = 0; kx < KS; ++kx) tap(sw, sx, SEGP, kx);
     };
-    // K ranges: [t0, t1) of this block (SPLIT: one range), range length R steps
-    int t0 = 0, t1 = T, R = T;
+    // K ranges: [t0, t1) of this block (SPLIT: one range; G2: this group's half), range
+    // length R steps, the first range of the second half at step th
+    int t0 = 0, t1 = T, R = T, th = T;
     if constexpr (SPLIT || RANGED) {
       // PPS == 2: the host checks that every range has an even number of pairs
       const int pps = (a.pairs + a.ksplit - 1) / a.ksplit;
       R = pps / PPS * KS;
+      th = min(T, (a.ksplit + 1) / 2 * R);
       if constexpr (SPLIT) {
         t0 = ks_i * R;
         t1 = min(a.pairs, (ks_i + 1) * pps) / PPS * KS;
       }
+      if constexpr (G2) {
+        t0 = grp ? th : 0;
+        t1 = grp ? T : th;
+      }
     }
+    // x3_canonical_order: each half's range sums (each from zero) added in order onto +0, then
+    // the halves added; tot holds the first half (G2: this group's half), toth the second
     f32x16 tot[RANGED ? WM : 1][RANGED ? WN : 1];
+    f32x16 toth[RANGED && !G2 ? WM : 1][RANGED && !G2 ? WN : 1];
+    if constexpr (RANGED) {
+#pragma unroll
+      for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+        for (int wn = 0; wn < WN; ++wn)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            tot[wm][wn][r] = 0.f;
+            if constexpr (!G2) toth[wm][wn][r] = 0.f;
+          }
+    }
     auto range_end = [&](int t) __attribute__((always_inline)) {
       if constexpr (RANGED) {
-        // end of a range: its sum (from zero) joins the total, ranges in order
         if (t + 1 == t1 || (t + 1) % R == 0) {
+          if (!G2 && t >= th) {                        // (uniform) a range of the second half
+            if constexpr (!G2) {
+#pragma unroll
+              for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+                for (int wn = 0; wn < WN; ++wn) toth[wm][wn] += acc[wm][wn];
+            }
+          } else {
+#pragma unroll
+            for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+              for (int wn = 0; wn < WN; ++wn) tot[wm][wn] += acc[wm][wn];
+          }
 #pragma unroll
           for (int wm = 0; wm < WM; ++wm)
 #pragma unroll
-            for (int wn = 0; wn < WN; ++wn) {
-              if (t + 1 == R) tot[wm][wn] = acc[wm][wn];
-              else tot[wm][wn] += acc[wm][wn];
+            for (int wn = 0; wn < WN; ++wn)
 #pragma unroll
               for (int r = 0; r < 16; ++r) acc[wm][wn][r] = 0.f;
-            }
         }
       }
     };
@@ -893,24 +968,56 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
       store_x(0);
     }
     __syncthreads();
-    for (int t = t0; t < t1; ++t) {
-      const int buf = (t - t0) & 1;
-      if (t + 1 < t1) {
+    // G2: both groups meet at every barrier; the first group has at least as many steps (its
+    // half holds the larger share of the ranges), the second idles through the surplus
+    const int nsteps = G2 ? th : t1 - t0;
+    for (int i = 0; i < nsteps; ++i) {
+      const int t = t0 + i;
+      const bool on = !G2 || t < t1;                // (uniform per group)
+      const int buf = i & 1;
+      if (on && t + 1 < t1) {
         if (!(abl & 4)) issue_w(t + 1, buf ^ 1);
         if (!(abl & 2)) load_x(t + 1);
       }
-      if (!(abl & 1)) compute(buf);
-      range_end(t);
+      if (on) {
+        if (!(abl & 1)) compute(buf);
+        range_end(t);
+      }
       if constexpr (SIB) __syncthreads();         // every wave is done with the one input buffer
-      if (t + 1 < t1 && !(abl & 2)) store_x(buf ^ 1);
+      if (on && t + 1 < t1 && !(abl & 2)) store_x(buf ^ 1);
       if (!(abl & 8)) __syncthreads();
     }
     }
-    if constexpr (RANGED) {
+    if constexpr (G2) {
+      // the second group's half through LDS (the loop ended on a barrier), added to the first
+      // group's in the first group's waves: lo + hi
+      float* xch = (float*)smem;
+      constexpr int NV = WM * WN * 16;
+      if (grp) {
+#pragma unroll
+        for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+          for (int wn = 0; wn < WN; ++wn)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) xch[((size_t)wave_g * NV + (wm * WN + wn) * 16 + r) * 64 + lane] = tot[wm][wn][r];
+      }
+      __syncthreads();
+      if (!grp) {
+#pragma unroll
+        for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+          for (int wn = 0; wn < WN; ++wn)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              acc[wm][wn][r] = tot[wm][wn][r] + xch[((size_t)wave_g * NV + (wm * WN + wn) * 16 + r) * 64 + lane];
+      }
+      __syncthreads();                              // the epilogue reuses the LDS
+    } else if constexpr (RANGED) {
+      const bool two = a.ksplit > (a.ksplit + 1) / 2;   // a second half exists (S >= 2)
 #pragma unroll
       for (int wm = 0; wm < WM; ++wm)
 #pragma unroll
-        for (int wn = 0; wn < WN; ++wn) acc[wm][wn] = tot[wm][wn];
+        for (int wn = 0; wn < WN; ++wn) acc[wm][wn] = two ? tot[wm][wn] + toth[wm][wn] : tot[wm][wn];
     }
     if constexpr (FOLD) {
       if (fold_bad) atomicOr(a.range_flag, 1);
@@ -943,6 +1050,125 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     }
     return;
   }
+  if constexpr (FUSE67) {
+    // Mconv6 -> Mconv7 (model.py:108-109, 125-126: two 1x1 convs, Mconv6 + PReLU, Mconv7).
+    // This block holds all BCO Mconv6 channels of its BPX pixels: wave (wave_m, wave_n) the
+    // channels [64 wave_m, 64 wave_m + 64) of pixel tiles wave_n * WN + wn.  One pass per wn
+    // (the pixel tiles wave_n * WN + wn of every wave_n): Mconv6's epilogue and split, each
+    // wave's Mconv7 sums into LDS, then the waves' sums added in wave order and stored.
+    static_assert(KS == 1 && WM == 2 && WN == 2 && !SPLIT && !RANGED && !UNION && !DEEP && !VIN && !HALFCO,
+                  "fused 1x1 pair: generic loop, 64co x 64px waves");
+    constexpr int RPX = WAVES_N * 32;            // pixels of one pass
+    float* eb = (float*)smem;                    // [BCO] bias6, [BCO] slope6, [64] bias7, [64] slope7
+    float* red = eb + 2 * BCO + 128;             // [WAVES_M][RPX][F7_ROWS]
+    for (int i = tid; i < BCO; i += NT) {        // the K loop ended on a barrier: LDS is free
+      eb[i] = a.bias[i];
+      eb[BCO + i] = a.act == ACT_PRELU ? a.slope[i] : 0.f;
+    }
+    for (int i = tid; i < 64; i += NT) {
+      eb[2 * BCO + i] = i < a.cout7 ? a.bias7[i] : 0.f;
+      eb[2 * BCO + 64 + i] = i < a.cout7 && a.act7 == ACT_PRELU ? a.slope7[i] : 0.f;
+    }
+    __syncthreads();
+    bool bad = false;
+    const int nt7 = (a.cout7 + 31) / 32;         // Mconv7 row tiles (1 or 2)
+    const int nch = (a.cout7 + 7) / 8;           // its 8-channel output chunks
+    constexpr int KB = BCO / 16;                 // Mconv7 K blocks (16 Mconv6 channels each)
+    const float* bias7 = eb + 2 * BCO;
+    const float* slope7 = eb + 2 * BCO + 64;
+    const int Wo = a.W + 2 * a.out_pad;
+    float* out_f = a.out + (size_t)n * a.out_fs;
+#pragma unroll
+    for (int wn = 0; wn < WN; ++wn) {
+      // Mconv6's epilogue (x 2^-s, bias, activation, range check) and the split: register r
+      // of a 32x32 D tile is row (r & 3) + 8 (r >> 2) + 4 h, so registers 8 kq .. 8 kq + 7 of
+      // lane half h are the K = 16 B fragment of rows {16 kq + 4 h + 8 (j >> 2) + (j & 3)};
+      // Mconv7's filters are packed in that K order (pack_x3_f7): no value leaves its lane
+      const bool live = m0 + (wave_n * WN + wn) * 32 + l32 <= mlast;
+      f16x8 Bh[WM][2], Bl[WM][2];
+#pragma unroll
+      for (int wm = 0; wm < WM; ++wm) {
+        f32x16 v;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int col = (wave_m * WM + wm) * 32 + 4 * h + 8 * q;
+          const f32x4 b = *(const f32x4*)(eb + col);
+          const f32x4 sl = *(const f32x4*)(eb + BCO + col);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float x = acc[wm][wn][4 * q + e] * a.wscale_inv + b[e];
+            if (a.act == ACT_RELU) x = x > 0.f ? x : 0.f;
+            else if (a.act == ACT_PRELU) x = x >= 0.f ? x : x * sl[e];
+            bad |= live && !(__builtin_fabsf(x) < 65504.f);
+            v[4 * q + e] = x;
+          }
+        }
+#pragma unroll
+        for (int kq = 0; kq < 2; ++kq)
+          x3_split8(f32x4{v[8 * kq], v[8 * kq + 1], v[8 * kq + 2], v[8 * kq + 3]},
+                    f32x4{v[8 * kq + 4], v[8 * kq + 5], v[8 * kq + 6], v[8 * kq + 7]}, Bh[wm][kq], Bl[wm][kq]);
+      }
+      // this wave's 64-channel share of every Mconv7 row tile: its K blocks in order, 3 split
+      // products each, from zero
+      for (int t = 0; t < nt7; ++t) {
+        f32x16 d;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) d[r] = 0.f;
+#pragma unroll
+        for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+          for (int kq = 0; kq < 2; ++kq) {
+            const int kb = (wave_m * WM + wm) * 2 + kq;
+            const f16x8* wp = a.wpk7 + ((size_t)(t * KB + kb) * 2) * 64 + lane;
+            const f16x8 Ah = wp[0], Al = wp[64];
+            d = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ah, Bh[wm][kq], d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ah, Bl[wm][kq], d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_32x32x16_f16(Al, Bh[wm][kq], d, 0, 0, 0);
+          }
+        float* rp = red + ((size_t)wave_m * RPX + wave_n * 32 + l32) * F7_ROWS + 32 * t + 4 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) *(f32x4*)(rp + 8 * q) = f32x4{d[4 * q], d[4 * q + 1], d[4 * q + 2], d[4 * q + 3]};
+      }
+      __syncthreads();
+      // the waves' sums added in wave order, x 2^-s, bias, activation, range check; one thread
+      // per (8-channel output chunk, pixel): 32-byte stores, neighbouring pixels together
+      for (int task = tid; task < nch * RPX; task += NT) {
+        const int c8 = task / RPX, px = task - c8 * RPX;
+        const int m = m0 + ((px >> 5) * WN + wn) * 32 + (px & 31);
+        if (m > mlast) continue;
+        const float* rq = red + (size_t)px * F7_ROWS + 8 * c8;
+        f32x4 s0 = *(const f32x4*)rq, s1 = *(const f32x4*)(rq + 4);
+#pragma unroll
+        for (int w = 1; w < WAVES_M; ++w) {
+          s0 += *(const f32x4*)(rq + (size_t)w * RPX * F7_ROWS);
+          s1 += *(const f32x4*)(rq + (size_t)w * RPX * F7_ROWS + 4);
+        }
+        const int co = 8 * c8;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = (e < 4 ? s0[e] : s1[e - 4]) * a.wscale7_inv + bias7[co + e];
+          if (a.act7 == ACT_RELU) x = x > 0.f ? x : 0.f;
+          else if (a.act7 == ACT_PRELU) x = x >= 0.f ? x : x * slope7[co + e];
+          bad |= co + e < a.cout7 && !(__builtin_fabsf(x) < 65504.f);
+          o[e] = x;
+        }
+        const int y = m / a.W, x = m - y * a.W;
+        float* oc = out_f + (size_t)(co >> 3) * a.out_chs + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8;
+        if (co + 7 < a.cout7) {
+          *(f32x4*)oc = f32x4{o[0], o[1], o[2], o[3]};
+          *(f32x4*)(oc + 4) = f32x4{o[4], o[5], o[6], o[7]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (co + e < a.cout7) oc[e] = o[e];
+        }
+      }
+      __syncthreads();                           // red is rewritten by the next pass
+    }
+    if (bad) atomicOr(a.range_flag, 1);
+    return;
+  }
   // epilogue: x 2^-s, bias + activation, range check, masked float4 stores.  Bias and
   // PReLU slopes come from LDS (staged once), so no global load -- and no vmcnt(0)
   // behind the stores issued so far -- sits between the output stores.
@@ -962,6 +1188,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64, OCC) conv_x3_f16(X3Arg
     ebias[BCO + i] = !abl_bias && a.act == ACT_PRELU ? a.slope[co_t * BCO + i] : 0.f;
   }
   __syncthreads();
+  if (G2 && grp) return;                        // the first K group stores the sums
 #pragma unroll
   for (int wn = 0; wn < WN; ++wn) {
     const int m = m0 + (wave_n * WN + wn) * 32 + l32;
@@ -1191,15 +1418,23 @@ double conv_x3_rgb_mfma_flops(const ConvLaunch& c) {
 // wave's loads and stores are contiguous.  The ranges' loads are all issued before the first
 // add (up to 8 in flight; the batch-1 frames' reduces had waited on one range at a time:
 // 5.0 us per launch at 23x41).
+// x3_canonical_order: ranges [0, h) summed in order, ranges [h, S) in order, then the two
+// halves, h = ceil(S / 2) -- the order of the in-block ranges (one or two K groups)
 template <int S>
 __device__ __forceinline__ f32x4 x3_sum_ranges(const float* p, size_t stride) {
   f32x4 part[S];
 #pragma unroll
   for (int k = 0; k < S; ++k) part[k] = __builtin_nontemporal_load((const f32x4*)(p + k * stride));
-  f32x4 sum = part[0];
+  constexpr int H = (S + 1) / 2;
+  f32x4 lo = f32x4{0.f, 0.f, 0.f, 0.f}, hi = lo;   // onto +0, as the in-block sums
 #pragma unroll
-  for (int k = 1; k < S; ++k) sum += part[k];
-  return sum;
+  for (int k = 0; k < H; ++k) lo += part[k];
+  if constexpr (S > H) {
+#pragma unroll
+    for (int k = H; k < S; ++k) hi += part[k];
+    return lo + hi;
+  }
+  return lo;
 }
 
 __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
@@ -1228,9 +1463,14 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
     case 6: sum = x3_sum_ranges<6>(p, split_stride); break;
     case 7: sum = x3_sum_ranges<7>(p, split_stride); break;
     case 8: sum = x3_sum_ranges<8>(p, split_stride); break;
-    default:
-      sum = *(const f32x4*)p;
-      for (int k = 1; k < a.ksplit; ++k) sum += *(const f32x4*)(p + k * split_stride);
+    default: {
+      const int hh = (a.ksplit + 1) / 2;
+      f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
+      sum = hi;
+      for (int k = 0; k < hh; ++k) sum += *(const f32x4*)(p + k * split_stride);
+      for (int k = hh; k < a.ksplit; ++k) hi += *(const f32x4*)(p + k * split_stride);
+      if (a.ksplit > hh) sum += hi;
+    }
   }
   f32x4 v;
 #pragma unroll
@@ -1262,7 +1502,9 @@ template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, int VAR, int OCC>
 static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   constexpr int BCO = WAVES_M * WM * 32;
   constexpr int BPX = WAVES_N * WN * 32;
-  t_last_variant = x3_variant_code(VAR, KS, BPX, BCO);
+  // (the fused pair's 512-channel tile does not fit the 4-bit tile field: it records BCO / 2,
+  // decode_variant doubles it back for VAR 16)
+  t_last_variant = x3_variant_code(VAR, KS, BPX, (VAR & 16) ? BCO / 2 : BCO);
   constexpr int P = KS / 2;
   constexpr int SEGCAP = x3_segmax(BPX);
   constexpr bool SPLIT = (VAR & 2048) != 0, RANGED = (VAR & 1024) != 0;
@@ -1289,6 +1531,22 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   }
   a.vin = c.vin;
   a.fold = c.fold;
+  if ((VAR & 16) != 0) {
+    if (c.cout7 <= 0 || c.cout7 > 64 || !c.wx3f7 || !c.bias7 || (c.act7 == ACT_PRELU && !c.slope7) || c.cout != BCO ||
+        c.hpool || c.vin || c.fold || c.fold_out || c.ksplit > 1) {
+      set_error("conv_x3: fused 1x1 pair needs Mconv7 filters, <= 64 outputs and one tile of every Mconv6 channel");
+      return hipErrorInvalidValue;
+    }
+    a.wpk7 = (const f16x8*)c.wx3f7;
+    a.bias7 = c.bias7;
+    a.slope7 = c.slope7;
+    a.wscale7_inv = c.wscale7_inv;
+    a.cout7 = c.cout7;
+    a.act7 = c.act7;
+  } else if (c.cout7 > 0) {
+    set_error("conv_x3: fused-pair launch on a plain variant");
+    return hipErrorInvalidValue;
+  }
 #ifdef ISLPOSE_DEV
   a.abl = getenv("ISLPOSE_X3_ABL") ? atoi(getenv("ISLPOSE_X3_ABL")) : 0;
 #else
@@ -1329,7 +1587,7 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
   hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN, VAR, OCC>), dim3(a.nblocks),
-                     dim3(WAVES_M * WAVES_N * 64), 0, s, a);
+                     dim3(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1)), 0, s, a);
   if constexpr (SPLIT) {
     // fold_out: every consumer sums the partials in its staging (X3Fold), no reduce launch
     if (!c.fold_out) {
@@ -1385,6 +1643,18 @@ static bool x3_halfco(const ConvLaunch& c) {
   if (e && e[0] == '1') return true;
 #endif
   return c.ks <= 3 && c.ksplit > 1 && c.ws;
+}
+
+// Small grids (the 128-pixel family) with two K groups per block (VAR 32, 16 waves: the first
+// and second half of the canonical K ranges side by side, one block per CU): every 128-channel
+// 1x1 / 3x3 launch whose K ranges run in one block (Mode R's 23x41 stage layers and conv4_x at
+// batch > 1).  The one-group form keeps both halves' sums and the range's in registers (153
+// VGPRs: one 8-wave block per CU) where two groups hold one each (122: 16 waves per CU).
+// ISLPOSE_X3_G2=0: the one-group loops (A/B; read per launch).
+static bool x3_g2(const ConvLaunch& c) {
+  if (c.ks > 3 || c.bco != 128 || c.fold || c.vin || c.ksplit < 2 || c.ws) return false;
+  const char* e = getenv("ISLPOSE_X3_G2");
+  return !(e && e[0] == '0');
 }
 
 // Small grids (the 128-pixel family) with the inputs and weights prefetched two K steps
@@ -1690,6 +1960,9 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
       }
 #endif
       if constexpr (KS <= 3) {
+        if (x3_g2(c)) return launch_t<KS, 2, 4, 2, 1, 1024 | 32, 1>(c, s);   // two K groups of 8 waves
+      }
+      if constexpr (KS <= 3) {
         if (x3_deep(c)) {   // prefetch two K steps ahead
           switch (c.bco) {
             case 128:
@@ -1721,8 +1994,10 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
 #endif
       if (c.bco == 128 && x3_halfco(c)) {   // two blocks of 4 waves (64co x 32px) per 128-channel tile
         if (split) return launch_t<KS, 1, 4, 2, 1, 2048 | 256, 4>(c, s);
+#ifdef ISLPOSE_DEV
         if (ranged) return launch_t<KS, 1, 4, 2, 1, 1024 | 256, 4>(c, s);
         return launch_t<KS, 1, 4, 2, 1, 256, 4>(c, s);
+#endif
       }
       switch (c.bco) {
         case 128:   // 8 waves of 64co x 32px
@@ -1791,7 +2066,39 @@ size_t x3_splitk_ws_floats(const ConvLaunch& c) {
   return r.across_blocks ? (size_t)r.S * c.n * ((c.cout + 7) / 8) * 8 * c.H * c.W : 0;
 }
 
+bool x3_fused67_fits(int cout6, int cout7) {
+  return (cout6 == 128 || cout6 == 256 || cout6 == 512) && cout7 > 0 && cout7 <= 64;
+}
+
+// The fused 1x1 pair, one tile of every Mconv6 channel: 16 waves of 64co x 64px, 8 x 2
+// (512 channels, 128 pixels), 4 x 4 (256, 256) or 2 x 8 (128, 512).  No K ranges: the pair
+// always runs fused, at every batch size, so a frame's bits do not depend on its batch.
+static hipError_t launch_x3_fused67(ConvLaunch c, hipStream_t s) {
+  if (c.ks != 1 || !x3_fused67_fits(c.cout, c.cout7)) {
+    set_error("conv_x3: fused 1x1 pair outside its shapes");
+    return hipErrorInvalidValue;
+  }
+  c.ksplit = 1;
+  c.ws = nullptr;
+  c.bco = c.cout;
+  switch (c.cout) {
+    case 512: return launch_t<1, 8, 2, 2, 2, 16, 4>(c, s);
+    case 256: return launch_t<1, 4, 4, 2, 2, 16, 4>(c, s);
+    case 128: return launch_t<1, 2, 8, 2, 2, 16, 4>(c, s);
+  }
+  set_error("conv_x3: fused 1x1 pair outside its shapes");
+  return hipErrorInvalidValue;
+}
+
+double conv_x3_fused67_mfma_flops(const ConvLaunch& c) {
+  const int bpx = c.cout == 512 ? 128 : c.cout == 256 ? 256 : 512;
+  const double px = std::ceil((double)c.H * c.W / tile_pixels(c, bpx, x3_segmax(bpx))) * bpx * c.n;
+  const double k6 = ((c.cin_chunks + 1) / 2) * 16.0;
+  return 3.0 * 2.0 * px * ((double)c.cout * k6 + 32.0 * ((c.cout7 + 31) / 32) * c.cout);
+}
+
 hipError_t launch_conv_x3(const ConvLaunch& c0, hipStream_t s) {
+  if (c0.cout7 > 0) return launch_x3_fused67(c0, s);
   ConvLaunch c = c0;
   const X3Ranges r = x3_ranges(c);
   c.ksplit = r.S;

@@ -74,6 +74,15 @@ struct ConvLaunch {
   // by folding consumers, so its x3_splitk_reduce launch is skipped (a producer).
   const X3Fold* fold = nullptr;
   int fold_out = 0;
+  // The fused 1x1 pair (conv_x3 VAR 16; Mconv6 -> Mconv7 of a stage, model.py:108-109):
+  // cout7 > 0 makes this launch the pair.  The fields above describe Mconv6 (wx3 packed for a
+  // tile of all its cout channels) with `out` / out_* describing Mconv7's output; these
+  // describe Mconv7 (wx3f7 = pack_x3_f7, K in the order of Mconv6's accumulator registers).
+  const void* wx3f7 = nullptr;
+  const float* bias7 = nullptr;
+  const float* slope7 = nullptr;
+  float wscale7_inv = 1.f;
+  int cout7 = 0, act7 = 0;
 };
 
 // Pixels per tile of the flattened-raster conv kernels: BPX, or fewer when the
@@ -124,6 +133,11 @@ constexpr int x3_variant_code(int var, int ks, int bpx, int bco) {
   return (var & 0xfffff) | ((bpx / 32) << 20) | ((bco / 32) << 25) | ((ks / 2) << 29);
 }
 int x3_last_variant();
+// whether launch_conv_x3 has a fused-pair variant for a 1x1 layer of cout6 outputs followed by
+// a 1x1 layer of cout7 outputs reading all of them (VAR 16)
+bool x3_fused67_fits(int cout6, int cout7);
+// MFMA FLOPs a fused-pair launch executes (both layers, tile padding included)
+double conv_x3_fused67_mfma_flops(const ConvLaunch& c);
 // floats of split-K workspace launch_conv_x3 would use for c (0 = no split)
 size_t x3_splitk_ws_floats(const ConvLaunch& c);
 // K ranges launch_conv_x3 would use for c: S, and whether they run across blocks (split-K

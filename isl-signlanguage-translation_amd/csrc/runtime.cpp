@@ -65,6 +65,12 @@ struct ConvLayer {
   float x3_inv = 1.f;            // 2^-s of the split weights
   void* d_wux3 = nullptr;        // split-fp16 Winograd filters (wino_x3.hip), 3x3 only
   float wx3_inv = 1.f;
+  // the fused 1x1 pair (conv_x3 VAR 16): fuse6 marks the first layer (Mconv6), packed once
+  // more for one tile of all its channels (d_wx3f, when bco < cout); fuse7 the second, packed
+  // in the fused K order (d_wx3f7, pack_x3_f7)
+  bool fuse6 = false, fuse7 = false;
+  void* d_wx3f = nullptr;
+  void* d_wx3f7 = nullptr;
 };
 
 static ConvLayer mk(const std::string& name, int cin, int cout, int k, int act, const std::string& prelu = "") {
@@ -179,6 +185,7 @@ struct Op {
   int layer;
   int in, in_coff, out, out_coff, C;
   int hbuf = -1;  // maxpool: the pair-max buffer its producing conv may write instead of `in`
+  bool fuse67 = false;   // conv: this op and the next run as one fused 1x1 pair (plan_fuse67)
 };
 
 struct OutRef {
@@ -558,6 +565,74 @@ static std::vector<_Float16> pack_x3_rgb(const ConvLayer& c) {
   return out;
 }
 
+// Mconv7 of a fused 1x1 pair (conv_x3 VAR 16): the K order of Mconv6's accumulator
+// registers.  K block kb = 2 g + q covers Mconv6 channels [32 g, 32 g + 32) half q; its slot j
+// of lane half h is register 8 q + j of that 32-row D tile, i.e. channel
+// 32 g + 16 q + 8 (j >> 2) + 4 h + (j & 3).  Layout [row tile t][kb][hi|lo][h][32][8], the same
+// 2^s as pack_x3 (max|w| * 2^s in [2^13, 2^14)).
+static std::vector<_Float16> pack_x3_f7(const ConvLayer& c, float* inv_scale) {
+  float mx = 0.f;
+  for (float v : c.w) mx = std::max(mx, std::fabs(v));
+  int e = 0;
+  if (mx > 0.f) {
+    std::frexp(mx, &e);
+    e = 14 - e;
+  }
+  const float scale = std::ldexp(1.f, e);
+  *inv_scale = std::ldexp(1.f, -e);
+  const int nt = (c.cout + 31) / 32, kbs = c.cin / 16;
+  std::vector<_Float16> out((size_t)nt * kbs * 2 * 2 * 32 * 8, (_Float16)0.f);
+  for (int t = 0; t < nt; ++t)
+    for (int kb = 0; kb < kbs; ++kb)
+      for (int h = 0; h < 2; ++h)
+        for (int row = 0; row < 32; ++row)
+          for (int j = 0; j < 8; ++j) {
+            const int co = 32 * t + row;
+            if (co >= c.cout) continue;
+            const int ch = 32 * (kb >> 1) + 16 * (kb & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+            const float w = c.w[(size_t)co * c.cin + ch] * scale;
+            const _Float16 hi = (_Float16)w;
+            const size_t base = ((size_t)(t * kbs + kb) * 2) * 64;
+            out[(base + h * 32 + row) * 8 + j] = hi;
+            out[(base + 64 + h * 32 + row) * 8 + j] = (_Float16)(w - (float)hi);
+          }
+  return out;
+}
+
+// Fusable 1x1 pairs (conv_x3 VAR 16): op k and op k + 1 both 1x1 convs, op k + 1 reading the
+// whole output of op k (offset 0, identity channel map) from a buffer nothing else reads and
+// that is no net output, shapes with a fused variant (x3_fused67_fits).  body_25's six
+// Mconv6 -> Mconv7 pairs and the hand's conv6_1/6_2 and Mconv6/7 pairs; COCO's pairs are not
+// adjacent (both branches read the stage input before either Mconv7 overwrites it).
+static void plan_fuse67(isl_net* net) {
+  for (size_t k = 0; k + 1 < net->ops.size(); ++k) {
+    Op& a = net->ops[k];
+    const Op& b = net->ops[k + 1];
+    if (a.type != 0 || b.type != 0) continue;
+    ConvLayer& la = net->layers[a.layer];
+    ConvLayer& lb = net->layers[b.layer];
+    if (la.k != 1 || lb.k != 1 || b.in != a.out || b.in_coff != 0 || a.out_coff != 0) continue;
+    if (lb.cin != la.cout || lb.cin_phys != la.cout || lb.cmap.size() != 1 || lb.cmap[0].logical != 0 ||
+        lb.cmap[0].phys != 0 || !x3_fused67_fits(la.cout, lb.cout))
+      continue;
+    if (net->out0.buf == a.out || (net->n_out > 1 && net->out1.buf == a.out)) continue;
+    bool other = false;
+    for (size_t j = 0; j < net->ops.size(); ++j)
+      if (j != k + 1 && net->ops[j].in == a.out) other = true;
+    if (other) continue;
+    a.fuse67 = true;
+    la.fuse6 = true;
+    lb.fuse7 = true;
+  }
+}
+
+// ISLPOSE_X3_FUSE67=0: the pairs as two launches through the Mconv6 output buffer (A/B; read
+// per run)
+static bool fuse67_enabled() {
+  const char* e = getenv("ISLPOSE_X3_FUSE67");
+  return !(e && e[0] == '0');
+}
+
 #ifdef ISLPOSE_DEV
 // Split-fp16 Winograd filters for wino_x3.hip: U = G g G^T (double) per (co,
 // physical ci), scaled by a per-layer 2^s (max|U| * 2^s in [2^13, 2^14)), split
@@ -639,6 +714,19 @@ static int upload_params(isl_net* net) {
       std::vector<_Float16> rp = pack_x3_rgb(c);
       if (!c.d_wrgb) HIP_OK(hipMalloc(&c.d_wrgb, rp.size() * sizeof(_Float16)));
       HIP_OK(hipMemcpy(c.d_wrgb, rp.data(), rp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
+    if (c.fuse6 && c.bco != c.cout) {   // one tile of all channels for the fused pair
+      float inv = 1.f;
+      std::vector<_Float16> xp = pack_x3(c, c.cout, &inv);
+      if (!c.d_wx3f) HIP_OK(hipMalloc(&c.d_wx3f, xp.size() * sizeof(_Float16)));
+      HIP_OK(hipMemcpy(c.d_wx3f, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
+    if (c.fuse7) {
+      float inv = 1.f;
+      std::vector<_Float16> xp = pack_x3_f7(c, &inv);
+      if (inv != c.x3_inv) return fail(ISL_E_STATE, "fused pair: Mconv7 scale mismatch");
+      if (!c.d_wx3f7) HIP_OK(hipMalloc(&c.d_wx3f7, xp.size() * sizeof(_Float16)));
+      HIP_OK(hipMemcpy(c.d_wx3f7, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
     if (c.x3_wide) {
       float inv = 1.f;
@@ -1007,10 +1095,38 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
   bool fused = false;   // the previous conv wrote the pair-max buffer of this pool
   int vin_buf = -1;     // this conv stages from that buffer (the pool op was skipped)
   const bool fuse_pools = fused_pool_enabled(), pool_input = fuse_pools && pool_input_enabled();
+  const bool fuse67 = net->algo == ISL_ALGO_X3 && fuse67_enabled();
   for (size_t k = 0; k < net->ops.size(); ++k) {
     const Op& op = net->ops[k];
     const Act& in = net->act[op.in];
     const Act& out = net->act[op.out];
+    if (fuse67 && op.fuse67 && vin_buf < 0) {
+      // Mconv6 -> Mconv7 in one launch (conv_x3 VAR 16): op k's input, op k + 1's output
+      const Op& op7 = net->ops[k + 1];
+      const ConvLayer& c6 = net->layers[op.layer];
+      const ConvLayer& c7 = net->layers[op7.layer];
+      const Act& o7 = net->act[op7.out];
+      ConvLaunch L = basic_launch(net, op);
+      L.out = o7.base; L.out_pad = o7.pad; L.out_cs = o7.cs; L.out_coff = op7.out_coff;
+      L.wx3 = c6.d_wx3f ? c6.d_wx3f : c6.d_wx3;
+      L.wx3f7 = c7.d_wx3f7; L.bias7 = c7.d_b; L.slope7 = c7.d_s; L.wscale7_inv = c7.x3_inv;
+      L.cout7 = c7.cout; L.act7 = c7.act;
+      HIP_OK(launch_conv_x3(L, s));
+      net->op_variant[k] = x3_last_variant();
+      net->op_variant[k + 1] = -2;   // ran inside op k
+      if (tr) {
+        // the pair's FLOPs and time on op k; op k + 1 an empty interval (not a launch)
+        tr->kind.push_back(3);
+        tr->flops.push_back(2.0 * in.H * in.W * in.n * ((double)c6.cout * c6.cin + (double)c7.cout * c7.cin));
+        tr->mfma_flops.push_back(conv_x3_fused67_mfma_flops(L));
+        HIP_OK(hipEventRecord(tr->ev[k + 1], s));
+        tr->kind.push_back(0); tr->flops.push_back(0.0); tr->mfma_flops.push_back(0.0);
+        HIP_OK(hipEventRecord(tr->ev[k + 2], s));
+      }
+      ++k;
+      continue;
+    }
+
     if (op.type == 1) {
       // deferred: the next conv either stages from the pair-max buffer or runs vpool2 first
       if (fused && pool_input && pool_into_next_conv(net, k)) { vin_buf = (int)k; net->op_variant[k] = -1; }
@@ -1132,7 +1248,7 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
 static const char* const kRunKeySwitches[] = {
     "ISLPOSE_X3_DEEP",   "ISLPOSE_RGB_CONV", "ISLPOSE_FUSED_POOL", "ISLPOSE_POOL_INPUT", "ISLPOSE_CONV_STAGING",
     "ISLPOSE_X3_TILES",  "ISLPOSE_X3_UNION", "ISLPOSE_X3_HALF64",  "ISLPOSE_X3_WIDE7",   "ISLPOSE_X3_ACROSS",
-    "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67",
+    "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67", "ISLPOSE_X3_G2",
 #ifdef ISLPOSE_DEV
     "ISLPOSE_X3_HALFCO", "ISLPOSE_X3_PPS2",  "ISLPOSE_X3_M16",     "ISLPOSE_X3_WINO",    "ISLPOSE_X3_ABL",
 #endif
@@ -1306,6 +1422,7 @@ int isl_net_create(int kind, int device, isl_net** out) {
   if (kind == ISL_BODY25) build_body25(net);
   else if (kind == ISL_COCO) build_coco(net);
   else build_hand(net);
+  plan_fuse67(net);
   *out = net;
   return ISL_OK;
 }
@@ -1322,6 +1439,8 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_wx3w) (void)hipFree(c.d_wx3w);
     if (c.d_wrgb) (void)hipFree(c.d_wrgb);
     if (c.d_wux3) (void)hipFree(c.d_wux3);
+    if (c.d_wx3f) (void)hipFree(c.d_wx3f);
+    if (c.d_wx3f7) (void)hipFree(c.d_wx3f7);
   }
   if (net->d_flag) (void)hipFree(net->d_flag);
   if (net->d_trips) (void)hipFree(net->d_trips);

@@ -182,9 +182,13 @@ def decode_variant(code: int) -> dict:
     """isl_net_op_info's variant code -> dict(var=VAR bits, bpx, bco, ks, rgb, pool_fused)."""
     if code == -1:
         return {"pool_fused": True}
+    if code == -2:
+        return {"fused_into_prev": True}     # the second layer of a fused 1x1 pair (VAR 16)
     if code <= 0:
         return {}
-    return {"var": code & 0xfffff, "bpx": ((code >> 20) & 31) * 32, "bco": ((code >> 25) & 15) * 32,
+    f67 = bool(code & 16)   # the fused pair records its all-channel tile halved (4-bit field)
+    return {"var": code & 0xfffff, "bpx": ((code >> 20) & 31) * 32,
+            "bco": ((code >> 25) & 15) * 32 * (2 if f67 else 1), "fused67": f67, "g2": bool(code & 32),
             "ks": 2 * ((code >> 29) & 3) + 1, "rgb": bool(code & (1 << 18)),
             "union": bool(code & 512), "ranged": bool(code & 1024), "split": bool(code & 2048),
             "pairs2": bool(code & 4096), "vin": bool(code & 32768), "sib": bool(code & 65536),

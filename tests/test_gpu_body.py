@@ -390,8 +390,8 @@ def test_timed_config_forward_vs_oracle(net25, w25):
     368x656; reference src/model.py:171-207) checked against the oracle on frames 0, 17 and
     31, with the kernel variants the bench times asserted through isl_net_op_info: the
     46x82 stage 3x3 layers on the 512-pixel row union, conv2_1 / conv3_1 / conv4_1 staging
-    their pooled input (the pools folded away), Mconv6 on 256-channel tiles with two chunk
-    pairs per step, conv1_1 on its 27-term kernel."""
+    their pooled input (the pools folded away), every Mconv6 -> Mconv7 pair fused into
+    one launch (VAR 16), conv1_1 on its 27-term kernel."""
     n, h, w = 32, 368, 656
     x = _inputs(n, h, w, seed=2024)
     paf, heat = net25.forward(torch.from_numpy(x).cuda())
@@ -405,7 +405,8 @@ def test_timed_config_forward_vs_oracle(net25, w25):
         assert var[k].get("vin"), (k, var[k])
     assert var["conv4_1"].get("union"), var["conv4_1"]
     m6 = [k for k in var if k.startswith("Mconv6")]
-    assert len(m6) == 6 and all(var[k].get("pairs2") and var[k]["bco"] == 256 for k in m6), m6
+    assert len(m6) == 6 and all(var[k].get("fused67") and var[k]["bco"] in (256, 512) for k in m6), m6
+    assert all(var[k].get("fused_into_prev") for k in var if k.startswith("Mconv7"))
     assert var["conv1_1"].get("rgb")
     assert sum(1 for _, v in net25.op_variants() if v == -1) == 3      # all three pools folded
     fn = cpu_ref.make_net_fn("body25", w25)
@@ -531,3 +532,28 @@ def test_graph_drop_waits_for_queued_replays(w25):
     rp, rh = eager.forward(x)
     torch.cuda.synchronize()
     assert torch.equal(o0, rp) and torch.equal(o1, rh)
+
+
+@pytest.mark.parametrize("n", [20, 32])
+def test_x3_g2_two_k_groups_bit_identical(net25, w25, n, monkeypatch):
+    """Two K groups per block (VAR 32: waves 0-7 sum the first half of a layer's canonical K
+    ranges, waves 8-15 the second, the halves meet in LDS) == one group walking every range
+    (ISLPOSE_X3_G2=0: three accumulator sets) bit for bit -- both add each half's range sums
+    in order and then the halves (x3_canonical_order), as x3_splitk_reduce does for the
+    ranges split across blocks.  The 23x41 stage layers take the variant (isl_net_op_info);
+    frame 0 matches the oracle."""
+    x = _inputs(n, 184, 328, seed=900 + n)
+    xt = torch.from_numpy(x).cuda()
+    monkeypatch.delenv("ISLPOSE_X3_G2", raising=False)
+    paf1, heat1 = net25.forward(xt)
+    torch.cuda.synchronize()
+    var = [rt.decode_variant(v) for _, v in net25.op_variants()]
+    assert sum(1 for v in var if v.get("g2")) >= 60, sum(1 for v in var if v.get("g2"))
+    assert all(v.get("ranged") and v["bco"] == 128 for v in var if v.get("g2"))
+    monkeypatch.setenv("ISLPOSE_X3_G2", "0")
+    paf0, heat0 = net25.forward(xt)
+    torch.cuda.synchronize()
+    assert not any(v.get("g2") for v in (rt.decode_variant(c) for _, c in net25.op_variants()))
+    assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
+    rp, rh = cpu_ref.make_net_fn("body25", w25)(x[:1])
+    assert _rel(paf1[:1].cpu().numpy(), rp) < TOL and _rel(heat1[:1].cpu().numpy(), rh) < TOL

@@ -1,0 +1,140 @@
+"""The fused 1x1 pair (conv_x3 VAR 16): Mconv6 -> Mconv7 of every body_25 stage
+(/root/reference/src/model.py:108-109, 125-126, make_layers_Mconv :48-64) and the hand's
+conv6_1/6_2 and Mconv6/7 pairs (:360-392) in one launch, the Mconv6 output never written.
+Checked against the oracle at the tolerance of the north star, against the two-launch path
+(ISLPOSE_X3_FUSE67=0) at fp32 round-off, and for batch-invariant bits.  GPU only."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref
+from islpose import synth
+from islpose import runtime as rt
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4   # north_star: heatmap/PAF tensors within 1e-4 relative (max|d| / max|ref|) in fp32
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def _inputs(n, h, w, seed):
+    f = synth.synth_frames(n, h, w, seed=seed)
+    return np.ascontiguousarray(np.transpose(f.astype(np.float32), (0, 3, 1, 2)) / 256 - 0.5)
+
+
+@pytest.fixture(scope="module")
+def w25():
+    return synth.synth_weights(0)
+
+
+@pytest.fixture(scope="module")
+def net25(w25):
+    n = rt.Net(rt.ISL_BODY25)
+    n.load_weights(w25)
+    return n
+
+
+def _assert_fused(net, n_pairs):
+    var = net.op_variants()
+    fused = [(k, rt.decode_variant(v)) for k, (_, v) in enumerate(var) if rt.decode_variant(v).get("fused67")]
+    assert len(fused) == n_pairs, [var[k][0] for k, _ in fused]
+    for k, d in fused:
+        assert d["ks"] == 1 and d["bco"] in (128, 256, 512), (var[k], d)
+        assert var[k + 1][1] == -2, var[k + 1]          # the second layer ran inside the first
+    return [var[k][0] for k, _ in fused]
+
+
+@pytest.mark.parametrize("n,h,w", [(1, 184, 328), (2, 92, 164), (3, 64, 200)])
+def test_body25_fused_pair_vs_oracle(net25, w25, monkeypatch, n, h, w):
+    """Mode R's net size at batch 1 and two awkward sizes: all six Mconv6 -> Mconv7 pairs fused
+    (asserted through isl_net_op_info), the maps within the bar of the oracle and within
+    fp32 round-off of the two-launch path."""
+    x = _inputs(n, h, w, seed=7 * h + w + n)
+    xt = torch.from_numpy(x).cuda()
+    monkeypatch.delenv("ISLPOSE_X3_FUSE67", raising=False)
+    paf, heat = net25.forward(xt)
+    torch.cuda.synchronize()
+    names = _assert_fused(net25, 6)
+    assert all(nm.startswith("Mconv6") for nm in names), names
+    monkeypatch.setenv("ISLPOSE_X3_FUSE67", "0")
+    paf0, heat0 = net25.forward(xt)
+    torch.cuda.synchronize()
+    assert not any(rt.decode_variant(v).get("fused67") for _, v in net25.op_variants())
+    assert _rel(paf.cpu().numpy(), paf0.cpu().numpy()) < 1e-5
+    assert _rel(heat.cpu().numpy(), heat0.cpu().numpy()) < 1e-5
+    rp, rh = cpu_ref.make_net_fn("body25", w25)(x)
+    assert _rel(paf.cpu().numpy(), rp) < TOL and _rel(heat.cpu().numpy(), rh) < TOL
+
+
+def test_body25_fused_pair_timed_config(net25, w25):
+    """The bench's configuration (32 frames of 368x656, net input 368x656): the six pairs on
+    the fused variant (512- and 256-channel tiles), frames 0 and 31 against the oracle."""
+    n, h, w = 32, 368, 656
+    x = _inputs(n, h, w, seed=31337)
+    paf, heat = net25.forward(torch.from_numpy(x).cuda())
+    torch.cuda.synchronize()
+    _assert_fused(net25, 6)
+    bcos = sorted(rt.decode_variant(v)["bco"] for _, v in net25.op_variants()
+                  if rt.decode_variant(v).get("fused67"))
+    assert bcos == [256, 256, 512, 512, 512, 512], bcos
+    fn = cpu_ref.make_net_fn("body25", w25)
+    for f in (0, 31):
+        rp, rh = fn(x[f:f + 1])
+        assert _rel(paf[f:f + 1].cpu().numpy(), rp) < TOL and _rel(heat[f:f + 1].cpu().numpy(), rh) < TOL, f
+
+
+def test_fused_pair_batch_invariant(net25):
+    """The pair always runs fused (no K ranges), so a Mode R frame gives the same bits alone
+    and inside a batch of 12."""
+    x = torch.from_numpy(_inputs(12, 184, 328, seed=404)).cuda()
+    pb, hb = net25.forward(x)
+    for i in (0, 11):
+        p1, h1 = net25.forward(x[i:i + 1].contiguous())
+        assert torch.equal(p1, pb[i:i + 1]) and torch.equal(h1, hb[i:i + 1]), i
+
+
+@pytest.mark.parametrize("n,side", [(1, 184), (5, 368)])
+def test_hand_fused_pairs_vs_oracle(monkeypatch, n, side):
+    """The hand net: conv6_1_CPM -> conv6_2_CPM (128 -> 512 -> 22) and the five Mconv6 ->
+    Mconv7 pairs (128 -> 128 -> 22) fused; maps vs the oracle and the two-launch path."""
+    wh = synth.synth_weights(2)
+    net = rt.Net(rt.ISL_HAND)
+    net.load_weights(wh)
+    x = _inputs(n, side, side, seed=side + n)
+    xt = torch.from_numpy(x).cuda()
+    monkeypatch.delenv("ISLPOSE_X3_FUSE67", raising=False)
+    hm = net.forward(xt)
+    torch.cuda.synchronize()
+    names = _assert_fused(net, 6)
+    assert "conv6_1_CPM" in names, names
+    monkeypatch.setenv("ISLPOSE_X3_FUSE67", "0")
+    h0 = net.forward(xt)
+    torch.cuda.synchronize()
+    assert _rel(hm.cpu().numpy(), h0.cpu().numpy()) < 1e-5
+    rh = cpu_ref.make_net_fn("hand", wh)(x)
+    rh = rh[0] if isinstance(rh, tuple) else rh
+    assert _rel(hm.cpu().numpy(), rh) < TOL
+
+
+def test_fused_pair_range_guard(w25):
+    """An Mconv6 output beyond the split range (|x| >= 65504 cannot be split into the fp16
+    operand of Mconv7) raises the range flag inside the fused launch; Net.forward then
+    recomputes on the fp32 kernels and still matches the oracle."""
+    w = dict(w25)
+    for k in list(w):
+        if k.startswith("Mconv6_stage0_L2") and k.endswith(".bias"):
+            w[k] = w[k] + np.float32(1e5)
+    net = rt.Net(rt.ISL_BODY25)
+    net.load_weights(w)
+    x = _inputs(1, 64, 96, seed=5)
+    xt = torch.from_numpy(x).cuda()
+    o0 = torch.empty((1, 52, 8, 12), device="cuda")
+    o1 = torch.empty((1, 26, 8, 12), device="cuda")
+    rt.check(rt.lib().isl_net_forward(net.h, rt.ptr(xt), 1, 64, 96, rt.ptr(o0), rt.ptr(o1), rt.stream_handle()))
+    assert not net.range_ok()
+    paf, heat = net.forward(xt)
+    rp, rh = cpu_ref.make_net_fn("body25", w)(x)
+    assert _rel(paf.cpu().numpy(), rp) < TOL and _rel(heat.cpu().numpy(), rh) < TOL

@@ -161,3 +161,72 @@ def test_arena_bounded_over_crop_counts():
     ref.net.load_weights(synth.synth_weights(2))
     ref.estimate_crops(frames, [(i % 2, 10 + 7 * i, 5 + 3 * i, 60) for i in range(max(counts))])
     assert used == ref.net.arena_info()[0]
+
+
+def _x3_7x7_bpx(n, side):
+    """conv_x3.hip x3_7x7_bpx for the hand's 7x7 stage layers (128 outputs, input ring 3) on
+    a side x side level-3 grid at batch n: canonical K ranges (<= 1024 pixels) keep 128-pixel
+    tiles, else the tile with the fewest rounds of one block per CU, a round of 256- / 384-
+    pixel blocks costing 1.74 / 2.58 rounds of 128 (ties keep the smaller tile)."""
+    if side * side <= 1024:
+        return 128
+
+    def tile_pixels(bpx):
+        for t in range(bpx, 1, -1):
+            if t - 1 + 2 * 3 * ((side + t - 2) // side) + 2 * 3 + 1 <= bpx + 64:
+                return t
+        return 1
+    best, best_t = 128, None
+    for bpx, cost in ((128, 1.0), (256, 1.74), (384, 2.58)):
+        blocks = n * -(-side * side // tile_pixels(bpx))
+        tt = -(-blocks // 256) * cost
+        if best_t is None or tt < best_t:
+            best, best_t = bpx, tt
+    return best
+
+
+def test_c3_crop_batch_vs_oracle():
+    """configs[2] (C3) at its own batch: 16 frames of 368x656 with 2 hand crops each (120-200
+    px, as tools/bench_configs.py c3), 32 crops per scale through the batched hand net at all
+    four scales (reference src/hand.py:25-56 per crop).  Crops 0, 15 and 31: maps within 1e-4 of
+    the oracle's net on the oracle's own crop input, peaks bit-exact with the oracle's post on
+    those maps; the 7x7 tile size every scale ran (isl_net_op_info) is the grid-quantisation
+    choice for 32 crops."""
+    from islpose import runtime as rt
+    B, H, W = 16, 368, 656
+    frames = synth.synth_frames(B, H, W, seed=5)
+    rng = np.random.RandomState(0)
+    boxes = []
+    for f in range(B):
+        for _ in range(2):
+            w = int(rng.randint(120, 201))
+            boxes.append((f, int(rng.randint(0, W - w)), int(rng.randint(0, H - w)), w))
+    wh = synth.synth_weights(2)
+    net = rt.Net(rt.ISL_HAND)
+    net.load_weights(wh)
+    t = torch.from_numpy(frames).cuda()
+    heats = []
+    for s in HAND_SCALES:
+        one = HandEstimator(net=net, scale_search=(s,))
+        heats += one.run_crops(t, boxes)
+        torch.cuda.synchronize()
+        side = int(round(s * 368)) // 8
+        want = _x3_7x7_bpx(len(boxes), side)
+        var = [rt.decode_variant(v) for name, v in net.op_variants() if name.startswith("Mconv") and "Mconv6" not in name
+               and "Mconv7" not in name]
+        assert len(var) == 25 and all(d["ks"] == 7 and d["bpx"] == want for d in var), (s, want, var[:2])
+    peaks = HandEstimator(net=net).post_crops(boxes, heats)
+    fn = cpu_ref.make_net_fn("hand", wh)
+    for i in (0, 15, 31):
+        f, x, y, w = boxes[i]
+        crop = np.ascontiguousarray(frames[f, y:y + w, x:x + w])
+        for si, s in enumerate(HAND_SCALES):
+            im, _, _ = cpu_ref.net_input(crop, s * 368 / w)
+            ref = fn(im)
+            ref = ref[0] if isinstance(ref, tuple) else ref
+            got = heats[si][i:i + 1].cpu().numpy()
+            assert got.shape == ref.shape, (i, s)
+            d = float(np.max(np.abs(got - ref)) / max(np.max(np.abs(ref)), 1e-30))
+            assert d < 1e-4, (i, s, d)
+        maps = iter([h[i].cpu().numpy() for h in heats])
+        assert np.array_equal(peaks[i], cpu_ref.hand_call(crop, lambda im: next(maps)[None])), i

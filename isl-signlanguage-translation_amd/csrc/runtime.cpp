@@ -600,8 +600,8 @@ static std::vector<_Float16> pack_x3_f7(const ConvLayer& c, float* inv_scale) {
 }
 
 // Fusable 1x1 pairs (conv_x3 VAR 16): op k and op k + 1 both 1x1 convs, op k + 1 reading the
-// whole output of op k (offset 0, identity channel map) from a buffer nothing else reads and
-// that is no net output, shapes with a fused variant (x3_fused67_fits).  body_25's six
+// whole output of op k (offset 0, identity channel map) from a buffer no other op reads before
+// it is written again and that is no net output, shapes with a fused variant (x3_fused67_fits).  body_25's six
 // Mconv6 -> Mconv7 pairs and the hand's conv6_1/6_2 and Mconv6/7 pairs; COCO's pairs are not
 // adjacent (both branches read the stage input before either Mconv7 overwrites it).
 static void plan_fuse67(isl_net* net) {
@@ -616,9 +616,13 @@ static void plan_fuse67(isl_net* net) {
         lb.cmap[0].phys != 0 || !x3_fused67_fits(la.cout, lb.cout))
       continue;
     if (net->out0.buf == a.out || (net->n_out > 1 && net->out1.buf == a.out)) continue;
+    // the value op k writes is read by op k + 1 only: no later op reads the buffer before the
+    // next op that writes it (every stage's Mconv6 reuses one buffer)
     bool other = false;
-    for (size_t j = 0; j < net->ops.size(); ++j)
-      if (j != k + 1 && net->ops[j].in == a.out) other = true;
+    for (size_t j = k + 2; j < net->ops.size(); ++j) {
+      if (net->ops[j].in == a.out) { other = true; break; }
+      if (net->ops[j].out == a.out) break;
+    }
     if (other) continue;
     a.fuse67 = true;
     la.fuse6 = true;

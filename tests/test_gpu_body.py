@@ -441,6 +441,7 @@ def test_x3_deep_small_grids_bit_identical(net25, n, monkeypatch):
     the waits are counted, raw barriers) run the same MFMA sequence as the default loop:
     bit-identical maps, with the stage layers on the variant (isl_net_op_info)."""
     x = torch.from_numpy(_inputs(n, 184, 328, seed=600 + n)).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_G2", "0")     # two K groups take precedence over the deep loop
     monkeypatch.setenv("ISLPOSE_X3_DEEP", "0")
     paf0, heat0 = net25.forward(x)
     torch.cuda.synchronize()
@@ -536,8 +537,8 @@ def test_graph_drop_waits_for_queued_replays(w25):
 
 @pytest.mark.parametrize("n", [20, 32])
 def test_x3_g2_two_k_groups_bit_identical(net25, w25, n, monkeypatch):
-    """Two K groups per block (VAR 32: waves 0-7 sum the first half of a layer's canonical K
-    ranges, waves 8-15 the second, the halves meet in LDS) == one group walking every range
+    """Two K groups per block (VAR 32: the first group of waves sums the first half of a layer's
+    canonical K ranges, the second group the second half, the halves meet in LDS) == one group walking every range
     (ISLPOSE_X3_G2=0: three accumulator sets) bit for bit -- both add each half's range sums
     in order and then the halves (x3_canonical_order), as x3_splitk_reduce does for the
     ranges split across blocks.  The 23x41 stage layers take the variant (isl_net_op_info);
@@ -548,8 +549,8 @@ def test_x3_g2_two_k_groups_bit_identical(net25, w25, n, monkeypatch):
     paf1, heat1 = net25.forward(xt)
     torch.cuda.synchronize()
     var = [rt.decode_variant(v) for _, v in net25.op_variants()]
-    assert sum(1 for v in var if v.get("g2")) >= 60, sum(1 for v in var if v.get("g2"))
-    assert all(v.get("ranged") and v["bco"] == 128 for v in var if v.get("g2"))
+    assert sum(1 for v in var if v.get("g2")) >= 90, sum(1 for v in var if v.get("g2"))
+    assert all(v.get("ranged") and v["bco"] in (96, 128) for v in var if v.get("g2"))
     monkeypatch.setenv("ISLPOSE_X3_G2", "0")
     paf0, heat0 = net25.forward(xt)
     torch.cuda.synchronize()

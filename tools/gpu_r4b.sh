@@ -17,6 +17,17 @@ timeout -k 10 200 python -u tools/op_table.py --batch 1 --h 184 --w 328 --runs 2
 head -12 $O/ops_R_b32_*.txt $O/ops_N_b32*.txt $O/ops_R_b1.txt
 timeout -k 10 400 python -u bench.py --no-cpu > $O/bench.json 2> $O/bench.err
 rb=$?
+[ $rb -eq 0 ] && ISLPOSE_X3_ACROSS=0 timeout -k 10 200 python -u bench.py --scale 0.5 --batch 1 --steps 50 --warmup 5 --no-cpu --e2e-steps 0 --no-mode-r > $O/b1_across0.json 2>> $O/bench.err
+rb=$?
+[ $rb -eq 0 ] && timeout -k 10 200 python -u bench.py --scale 0.5 --batch 1 --steps 50 --warmup 5 --no-cpu --e2e-steps 0 --no-mode-r > $O/b1_default.json 2>> $O/bench.err
+rb=$?
+[ $rb -eq 0 ] && ISLPOSE_X3_FUSE67=0 timeout -k 10 200 python -u bench.py --scale 0.5 --batch 1 --steps 50 --warmup 5 --no-cpu --e2e-steps 0 --no-mode-r > $O/b1_fuse0.json 2>> $O/bench.err
+rb=$?
+python3 -c "
+import json
+for f in ('b1_across0','b1_default','b1_fuse0'):
+    d=json.load(open('$O/'+f+'.json')); print(f, d['value'], d['roofline']['frac'])
+"
 python3 -c "
 import json
 d=json.load(open('$O/bench.json'))

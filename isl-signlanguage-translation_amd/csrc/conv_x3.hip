@@ -1136,13 +1136,19 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
         const int c8 = task / RPX, px = task - c8 * RPX;
         const int m = m0 + ((px >> 5) * WN + wn) * 32 + (px & 31);
         if (m > mlast) continue;
+        // x3_canonical_order over the waves' shares (the K ranges of the two-launch Mconv7,
+        // pack_x3_f7): each half from +0 in wave order, then the halves
         const float* rq = red + (size_t)px * F7_ROWS + 8 * c8;
-        f32x4 s0 = *(const f32x4*)rq, s1 = *(const f32x4*)(rq + 4);
+        constexpr int HW7 = (WAVES_M + 1) / 2;
+        f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0, u0 = s0, u1 = s0;
 #pragma unroll
-        for (int w = 1; w < WAVES_M; ++w) {
-          s0 += *(const f32x4*)(rq + (size_t)w * RPX * F7_ROWS);
-          s1 += *(const f32x4*)(rq + (size_t)w * RPX * F7_ROWS + 4);
+        for (int w = 0; w < WAVES_M; ++w) {
+          const f32x4 p0 = *(const f32x4*)(rq + (size_t)w * RPX * F7_ROWS);
+          const f32x4 p1 = *(const f32x4*)(rq + (size_t)w * RPX * F7_ROWS + 4);
+          if (w < HW7) { s0 += p0; s1 += p1; }
+          else { u0 += p0; u1 += p1; }
         }
+        if constexpr (WAVES_M > HW7) { s0 += u0; s1 += u1; }
         const int co = 8 * c8;
         float o[8];
 #pragma unroll
@@ -1703,9 +1709,12 @@ static bool x3_pps2(const ConvLaunch&) { return false; }   // rejected (profiles
 #endif
 
 static int x3_canonical_ranges(const ConvLaunch& c) {
-  const int pairs = (c.cin_chunks + 1) / 2;
-  if (!c.allow_split || c.H * c.W > 1024 || pairs < 4) return 1;
-  int S = std::min(8, pairs / 2);
+  // 3x3 / 7x7 layers: ranges of >= 2 chunk pairs; 1x1 layers: >= 4 pairs (64 channels), so
+  // that a range of an Mconv7 is one wave's share of the fused pair (VAR 16) and the two
+  // executions of the pair give the same bits
+  const int pairs = (c.cin_chunks + 1) / 2, per = c.ks == 1 ? 4 : 2;
+  if (!c.allow_split || c.H * c.W > 1024 || pairs < 2 * per) return 1;
+  int S = std::min(8, pairs / per);
   while (S > 1 && (S - 1) * ((pairs + S - 1) / S) >= pairs) --S;
   return S;
 }
@@ -2091,6 +2100,17 @@ static hipError_t launch_x3_fused67(ConvLaunch c, hipStream_t s) {
   }
   set_error("conv_x3: fused 1x1 pair outside its shapes");
   return hipErrorInvalidValue;
+}
+
+// The pair runs fused where its grid has at least half a block per CU; smaller grids (batch-1
+// Mode R: 8 pixel tiles) take the two launches (Mconv6 then Mconv7 with its K ranges split
+// across blocks), whose bits are the fused kernel's (the runtime's permuted Mconv6 output order,
+// pack_x3 with the Mconv7 channel map; x3_canonical_order over the waves).
+bool x3_fused67_grid(const ConvLaunch& c) {
+  const int bpx = c.cout == 512 ? 128 : c.cout == 256 ? 256 : 512;
+  const long long blocks = (long long)c.n * ((c.H * c.W + tile_pixels(c, bpx, x3_segmax(bpx)) - 1) /
+                                             tile_pixels(c, bpx, x3_segmax(bpx)));
+  return 2 * blocks >= device_cus();
 }
 
 double conv_x3_fused67_mfma_flops(const ConvLaunch& c) {

@@ -136,6 +136,8 @@ int x3_last_variant();
 // whether launch_conv_x3 has a fused-pair variant for a 1x1 layer of cout6 outputs followed by
 // a 1x1 layer of cout7 outputs reading all of them (VAR 16)
 bool x3_fused67_fits(int cout6, int cout7);
+// whether a fusable pair's launch has the grid for the fused kernel (else two launches)
+bool x3_fused67_grid(const ConvLaunch& c);
 // MFMA FLOPs a fused-pair launch executes (both layers, tile padding included)
 double conv_x3_fused67_mfma_flops(const ConvLaunch& c);
 // floats of split-K workspace launch_conv_x3 would use for c (0 = no split)

@@ -71,6 +71,11 @@ struct ConvLayer {
   bool fuse6 = false, fuse7 = false;
   void* d_wx3f = nullptr;
   void* d_wx3f7 = nullptr;
+  // ... and for the pair's two-launch form on small grids: Mconv6 writes its channels in the
+  // fused K order (rows, bias and slopes permuted: d_wx3p, d_bp, d_sp), Mconv7 reads them
+  // through that channel map (d_wx3p)
+  void* d_wx3p = nullptr;
+  float *d_bp = nullptr, *d_sp = nullptr;
 };
 
 static ConvLayer mk(const std::string& name, int cin, int cout, int k, int act, const std::string& prelu = "") {
@@ -630,11 +635,40 @@ static void plan_fuse67(isl_net* net) {
   }
 }
 
-// ISLPOSE_X3_FUSE67=0: the pairs as two launches through the Mconv6 output buffer (A/B; read
-// per run)
-static bool fuse67_enabled() {
+// Mconv6 output channel order of a fusable pair's two-launch form: physical channel
+// 16 p + 8 h + j (chunk h of pair p, element j) holds the channel that sits in slot j of lane
+// half h of the fused kernel's K block p (pack_x3_f7): 32 g + 16 q + 8 (j >> 2) + 4 h + (j & 3),
+// p = 2 g + q.  Mconv7 then stages exactly the fused kernel's B fragments.
+static int f7_logical(int phys) {
+  const int p = phys >> 4, h = (phys >> 3) & 1, j = phys & 7, g = p >> 1, q = p & 1;
+  return 32 * g + 16 * q + 8 * (j >> 2) + 4 * h + (j & 3);
+}
+
+// The permuted copies of a fusable pair's layers (two-launch form): Mconv6 with its output
+// rows (weights, bias, slopes) in f7_logical order, Mconv7 with the matching channel map
+static ConvLayer f7_permuted(const ConvLayer& c) {
+  ConvLayer p = c;
+  if (c.fuse6) {
+    const size_t per = (size_t)c.cin * c.k * c.k;
+    for (int ph = 0; ph < c.cout; ++ph) {
+      const int lg = f7_logical(ph);
+      std::copy(c.w.begin() + lg * per, c.w.begin() + (lg + 1) * per, p.w.begin() + ph * per);
+      p.b[ph] = c.b[lg];
+      if (c.act == ACT_PRELU) p.s[ph] = c.s[lg];
+    }
+  } else {
+    p.cmap.clear();
+    for (int ph = 0; ph < c.cin; ++ph) p.cmap.push_back({f7_logical(ph), ph, 1});
+  }
+  return p;
+}
+
+// ISLPOSE_X3_FUSE67: 0 the pairs as two plain launches (natural channel order; A/B), 2 always
+// fused, 3 always the permuted two launches (tests), default by grid (x3_fused67_grid); read
+// per run
+static int fuse67_mode() {
   const char* e = getenv("ISLPOSE_X3_FUSE67");
-  return !(e && e[0] == '0');
+  return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 1;
 }
 
 #ifdef ISLPOSE_DEV
@@ -731,6 +765,23 @@ static int upload_params(isl_net* net) {
       if (inv != c.x3_inv) return fail(ISL_E_STATE, "fused pair: Mconv7 scale mismatch");
       if (!c.d_wx3f7) HIP_OK(hipMalloc(&c.d_wx3f7, xp.size() * sizeof(_Float16)));
       HIP_OK(hipMemcpy(c.d_wx3f7, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
+    if (c.fuse6 || c.fuse7) {   // the pair's permuted two-launch form
+      const ConvLayer pc = f7_permuted(c);
+      float inv = 1.f;
+      std::vector<_Float16> xp = pack_x3(pc, c.bco, &inv);
+      if (inv != c.x3_inv) return fail(ISL_E_STATE, "fused pair: permuted scale mismatch");
+      if (!c.d_wx3p) HIP_OK(hipMalloc(&c.d_wx3p, xp.size() * sizeof(_Float16)));
+      HIP_OK(hipMemcpy(c.d_wx3p, xp.data(), xp.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+      if (c.fuse6) {
+        std::vector<float> b2(bp.size(), 0.f), s2(sp.size(), 0.f);
+        std::copy(pc.b.begin(), pc.b.end(), b2.begin());
+        if (c.act == ACT_PRELU) std::copy(pc.s.begin(), pc.s.end(), s2.begin());
+        if (!c.d_bp) HIP_OK(hipMalloc(&c.d_bp, b2.size() * sizeof(float)));
+        if (!c.d_sp) HIP_OK(hipMalloc(&c.d_sp, s2.size() * sizeof(float)));
+        HIP_OK(hipMemcpy(c.d_bp, b2.data(), b2.size() * sizeof(float), hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(c.d_sp, s2.data(), s2.size() * sizeof(float), hipMemcpyHostToDevice));
+      }
     }
     if (c.x3_wide) {
       float inv = 1.f;
@@ -1099,12 +1150,18 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
   bool fused = false;   // the previous conv wrote the pair-max buffer of this pool
   int vin_buf = -1;     // this conv stages from that buffer (the pool op was skipped)
   const bool fuse_pools = fused_pool_enabled(), pool_input = fuse_pools && pool_input_enabled();
-  const bool fuse67 = net->algo == ISL_ALGO_X3 && fuse67_enabled();
+  const int f67 = net->algo == ISL_ALGO_X3 ? fuse67_mode() : 0;
+  size_t perm_op = (size_t)-1;   // the pair (perm_op, perm_op + 1) runs as its permuted two launches
   for (size_t k = 0; k < net->ops.size(); ++k) {
     const Op& op = net->ops[k];
     const Act& in = net->act[op.in];
     const Act& out = net->act[op.out];
-    if (fuse67 && op.fuse67 && vin_buf < 0) {
+    // the two launches only where Mconv7 has K ranges (canonical: its ranges are the fused
+    // kernel's wave shares, so both forms give the same bits); larger planes always fuse
+    if (f67 && op.fuse67 && vin_buf < 0 && (f67 == 3 || (f67 == 1 && !x3_fused67_grid(basic_launch(net, op)))) &&
+        x3_split_ranges(basic_launch(net, net->ops[k + 1]), nullptr) > 1)
+      perm_op = k;
+    if (f67 && op.fuse67 && vin_buf < 0 && perm_op != k) {
       // Mconv6 -> Mconv7 in one launch (conv_x3 VAR 16): op k's input, op k + 1's output
       const Op& op7 = net->ops[k + 1];
       const ConvLayer& c6 = net->layers[op.layer];
@@ -1177,7 +1234,15 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
         }
         vin_buf = -1;
       }
-      if (c.x3_wide) {   // 256-channel tiles, two pairs per step, where the grid is big enough
+      const bool perm = k == perm_op || (perm_op != (size_t)-1 && k == perm_op + 1);
+      if (perm && k == perm_op) {
+        // Mconv6 of the pair's two launches: output channels in the fused K order, its K
+        // summed in one sequence as the fused kernel does (no ranges)
+        L.wx3 = c.d_wx3p; L.bias = c.d_bp; L.slope = c.d_sp;
+        L.allow_split = 0;
+      } else if (perm) {
+        L.wx3 = c.d_wx3p;   // Mconv7 reading them through that channel map
+      } else if (c.x3_wide) {   // 256-channel tiles, two pairs per step, where the grid is big enough
         ConvLaunch Lw = L;
         Lw.bco = 256;
         if (x3_wide1(Lw)) { L.bco = 256; L.wx3 = c.d_wx3w; }
@@ -1445,6 +1510,9 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_wux3) (void)hipFree(c.d_wux3);
     if (c.d_wx3f) (void)hipFree(c.d_wx3f);
     if (c.d_wx3f7) (void)hipFree(c.d_wx3f7);
+    if (c.d_wx3p) (void)hipFree(c.d_wx3p);
+    if (c.d_bp) (void)hipFree(c.d_bp);
+    if (c.d_sp) (void)hipFree(c.d_sp);
   }
   if (net->d_flag) (void)hipFree(net->d_flag);
   if (net->d_trips) (void)hipFree(net->d_trips);

@@ -50,15 +50,29 @@ def _assert_fused(net, n_pairs):
 @pytest.mark.parametrize("n,h,w", [(1, 184, 328), (2, 92, 164), (3, 64, 200)])
 def test_body25_fused_pair_vs_oracle(net25, w25, monkeypatch, n, h, w):
     """Mode R's net size at batch 1 and two awkward sizes: all six Mconv6 -> Mconv7 pairs fused
-    (asserted through isl_net_op_info), the maps within the bar of the oracle and within
-    fp32 round-off of the two-launch path."""
+    (forced, ISLPOSE_X3_FUSE67=2, and asserted through isl_net_op_info), the maps within the bar
+    of the oracle; bit-identical to the pair's permuted two-launch form (=3: these stage planes
+    have canonical K ranges) that small grids run by default; within fp32 round-off of the
+    plain two launches (=0)."""
     x = _inputs(n, h, w, seed=7 * h + w + n)
     xt = torch.from_numpy(x).cuda()
-    monkeypatch.delenv("ISLPOSE_X3_FUSE67", raising=False)
+    monkeypatch.setenv("ISLPOSE_X3_FUSE67", "2")
     paf, heat = net25.forward(xt)
     torch.cuda.synchronize()
     names = _assert_fused(net25, 6)
     assert all(nm.startswith("Mconv6") for nm in names), names
+    monkeypatch.setenv("ISLPOSE_X3_FUSE67", "3")
+    pp, hp = net25.forward(xt)
+    torch.cuda.synchronize()
+    var = net25.op_variants()
+    assert not any(rt.decode_variant(v).get("fused67") for _, v in var)
+    m7 = [rt.decode_variant(v) for name, v in var if name.startswith("Mconv7")]
+    assert len(m7) == 6 and all(d.get("split") or d.get("ranged") for d in m7), m7
+    assert torch.equal(pp, paf) and torch.equal(hp, heat)
+    monkeypatch.delenv("ISLPOSE_X3_FUSE67")
+    pd, hd = net25.forward(xt)
+    torch.cuda.synchronize()
+    assert torch.equal(pd, paf) and torch.equal(hd, heat)
     monkeypatch.setenv("ISLPOSE_X3_FUSE67", "0")
     paf0, heat0 = net25.forward(xt)
     torch.cuda.synchronize()
@@ -87,11 +101,12 @@ def test_body25_fused_pair_timed_config(net25, w25):
 
 
 def test_fused_pair_batch_invariant(net25):
-    """The pair always runs fused (no K ranges), so a Mode R frame gives the same bits alone
-    and inside a batch of 12."""
-    x = torch.from_numpy(_inputs(12, 184, 328, seed=404)).cuda()
+    """A Mode R frame gives the same bits alone (the pairs as their permuted two launches)
+    and inside a batch of 16 (fused)."""
+    x = torch.from_numpy(_inputs(16, 184, 328, seed=404)).cuda()
     pb, hb = net25.forward(x)
-    for i in (0, 11):
+    assert sum(1 for _, v in net25.op_variants() if rt.decode_variant(v).get("fused67")) == 6
+    for i in (0, 15):
         p1, h1 = net25.forward(x[i:i + 1].contiguous())
         assert torch.equal(p1, pb[i:i + 1]) and torch.equal(h1, hb[i:i + 1]), i
 
@@ -99,17 +114,23 @@ def test_fused_pair_batch_invariant(net25):
 @pytest.mark.parametrize("n,side", [(1, 184), (5, 368)])
 def test_hand_fused_pairs_vs_oracle(monkeypatch, n, side):
     """The hand net: conv6_1_CPM -> conv6_2_CPM (128 -> 512 -> 22) and the five Mconv6 ->
-    Mconv7 pairs (128 -> 128 -> 22) fused; maps vs the oracle and the two-launch path."""
+    Mconv7 pairs (128 -> 128 -> 22) fused (forced); maps vs the oracle and the two-launch
+    paths (the permuted one bit-identical where the planes have canonical K ranges: 23x23)."""
     wh = synth.synth_weights(2)
     net = rt.Net(rt.ISL_HAND)
     net.load_weights(wh)
     x = _inputs(n, side, side, seed=side + n)
     xt = torch.from_numpy(x).cuda()
-    monkeypatch.delenv("ISLPOSE_X3_FUSE67", raising=False)
+    monkeypatch.setenv("ISLPOSE_X3_FUSE67", "2")
     hm = net.forward(xt)
     torch.cuda.synchronize()
     names = _assert_fused(net, 6)
     assert "conv6_1_CPM" in names, names
+    if side == 184:
+        monkeypatch.setenv("ISLPOSE_X3_FUSE67", "3")
+        hp = net.forward(xt)
+        torch.cuda.synchronize()
+        assert torch.equal(hp, hm)
     monkeypatch.setenv("ISLPOSE_X3_FUSE67", "0")
     h0 = net.forward(xt)
     torch.cuda.synchronize()
@@ -119,10 +140,11 @@ def test_hand_fused_pairs_vs_oracle(monkeypatch, n, side):
     assert _rel(hm.cpu().numpy(), rh) < TOL
 
 
-def test_fused_pair_range_guard(w25):
+def test_fused_pair_range_guard(w25, monkeypatch):
     """An Mconv6 output beyond the split range (|x| >= 65504 cannot be split into the fp16
     operand of Mconv7) raises the range flag inside the fused launch; Net.forward then
     recomputes on the fp32 kernels and still matches the oracle."""
+    monkeypatch.setenv("ISLPOSE_X3_FUSE67", "2")
     w = dict(w25)
     for k in list(w):
         if k.startswith("Mconv6_stage0_L2") and k.endswith(".bias"):
@@ -138,3 +160,20 @@ def test_fused_pair_range_guard(w25):
     paf, heat = net.forward(xt)
     rp, rh = cpu_ref.make_net_fn("body25", w)(x)
     assert _rel(paf.cpu().numpy(), rp) < TOL and _rel(heat.cpu().numpy(), rh) < TOL
+
+
+@pytest.mark.parametrize("n", [1, 8, 32])
+def test_fused_pair_default_form_by_grid(net25, monkeypatch, n):
+    """Default choice (x3_fused67_grid): Mode R frames fuse the pairs from half a block per CU
+    up (batch 32), smaller batches run the permuted two launches; both forms give the same
+    bits (so a frame's maps do not depend on its batch)."""
+    x = torch.from_numpy(_inputs(n, 184, 328, seed=77 + n)).cuda()
+    monkeypatch.delenv("ISLPOSE_X3_FUSE67", raising=False)
+    pd, hd = net25.forward(x)
+    torch.cuda.synchronize()
+    fused = sum(1 for _, v in net25.op_variants() if rt.decode_variant(v).get("fused67"))
+    assert fused == (6 if n >= 32 else 0), fused
+    monkeypatch.setenv("ISLPOSE_X3_FUSE67", "3" if n >= 32 else "2")
+    po, ho = net25.forward(x)
+    torch.cuda.synchronize()
+    assert torch.equal(po, pd) and torch.equal(ho, hd)

@@ -2,8 +2,8 @@
 # (G2 on / off, fused on / off), then the bench line.
 T=${1:-r4b}; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_body.py -x -v --timeout 300 --timeout-method thread \
-  -k "fused or timed_config or canonical or halfco or graph or g2 or splitk or deep" > $O/gputest.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_body.py tests/test_gpu_hand.py -x -v --timeout 300 --timeout-method thread \
+  -k "fused or timed_config or canonical or halfco or graph or g2 or splitk or deep or c3" > $O/gputest.log 2>&1
 rc=$?
 tail -5 $O/gputest.log
 if [ $rc -ne 0 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi

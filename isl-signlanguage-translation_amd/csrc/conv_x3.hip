@@ -1651,14 +1651,17 @@ static bool x3_halfco(const ConvLaunch& c) {
   return c.ks <= 3 && c.ksplit > 1 && c.ws;
 }
 
-// Small grids (the 128-pixel family) with two K groups per block (VAR 32, 16 / 12 waves: the
-// first and second half of the canonical K ranges side by side, one block per CU): every 128-
-// and 96-channel 1x1 / 3x3 launch whose K ranges run in one block (Mode R's 23x41 stage layers and conv4_x at
-// batch > 1).  The one-group form keeps both halves' sums and the range's in registers (153
-// VGPRs: one 8-wave block per CU) where two groups hold one each (122: 16 waves per CU).
+// Small grids (the 128-pixel family) with two K groups per block (VAR 32, 16 waves: the first
+// and second half of the canonical K ranges side by side, one block per CU): every 128-channel
+// 1x1 / 3x3 launch whose K ranges run in one block (Mode R's 23x41 stage layers and conv4_x at
+// batch >= 32; 5-6 % faster than the one-group loops there, profiles/r04/r4b/).  The 96-channel
+// form (two groups of 6 waves of 32co x 64px) measured 7 % slower than the deep-prefetch loop on
+// the c96 stage layers and is not built.  The one-group form keeps both halves' sums and the
+// range's in registers (153 VGPRs: one 8-wave block per CU) where two groups hold one each (122:
+// 16 waves per CU).
 // ISLPOSE_X3_G2=0: the one-group loops (A/B; read per launch).
 static bool x3_g2(const ConvLaunch& c) {
-  if (c.ks > 3 || (c.bco != 128 && c.bco != 96) || c.fold || c.vin || c.ksplit < 2 || c.ws) return false;
+  if (c.ks > 3 || c.bco != 128 || c.fold || c.vin || c.ksplit < 2 || c.ws) return false;
   const char* e = getenv("ISLPOSE_X3_G2");
   return !(e && e[0] == '0');
 }
@@ -1969,10 +1972,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
       }
 #endif
       if constexpr (KS <= 3) {
-        if (x3_g2(c)) {   // two K groups: 8 waves of 64co x 32px / 6 waves of 32co x 64px each
-          if (c.bco == 128) return launch_t<KS, 2, 4, 2, 1, 1024 | 32, 1>(c, s);
-          return launch_t<KS, 3, 2, 1, 2, 1024 | 32, 1>(c, s);
-        }
+        if (x3_g2(c)) return launch_t<KS, 2, 4, 2, 1, 1024 | 32, 1>(c, s);   // two K groups of 8 waves
       }
       if constexpr (KS <= 3) {
         if (x3_deep(c)) {   // prefetch two K steps ahead

@@ -549,8 +549,8 @@ def test_x3_g2_two_k_groups_bit_identical(net25, w25, n, monkeypatch):
     paf1, heat1 = net25.forward(xt)
     torch.cuda.synchronize()
     var = [rt.decode_variant(v) for _, v in net25.op_variants()]
-    assert sum(1 for v in var if v.get("g2")) >= 90, sum(1 for v in var if v.get("g2"))
-    assert all(v.get("ranged") and v["bco"] in (96, 128) for v in var if v.get("g2"))
+    assert sum(1 for v in var if v.get("g2")) >= 60, sum(1 for v in var if v.get("g2"))
+    assert all(v.get("ranged") and v["bco"] == 128 for v in var if v.get("g2"))
     monkeypatch.setenv("ISLPOSE_X3_G2", "0")
     paf0, heat0 = net25.forward(xt)
     torch.cuda.synchronize()

@@ -2093,16 +2093,8 @@ static hipError_t launch_x3_fused67(ConvLaunch c, hipStream_t s) {
   c.ksplit = 1;
   c.ws = nullptr;
   c.bco = c.cout;
-  // ISLPOSE_X3_F67PPS=1: two chunk pairs per K step with one input buffer (VAR 4096 | 65536:
-  // twice the MFMAs per step against the weight slab's L2 round trip; A/B, read per launch)
-  const char* e = getenv("ISLPOSE_X3_F67PPS");
-  if (e && e[0] == '1' && ((c.cin_chunks + 1) / 2) % 2 == 0) {
-    switch (c.cout) {
-      case 512: return launch_t<1, 8, 2, 2, 2, 16 | 4096 | 65536, 4>(c, s);
-      case 256: return launch_t<1, 4, 4, 2, 2, 16 | 4096 | 65536, 4>(c, s);
-      case 128: return launch_t<1, 2, 8, 2, 2, 16 | 4096 | 65536, 4>(c, s);
-    }
-  }
+  // (two chunk pairs per K step with one input buffer, VAR 4096 | 65536, measured level with
+  // this loop in Mode N and Mode R, profiles/r04/r4c/ops_*_pps1.txt: not built)
   switch (c.cout) {
     case 512: return launch_t<1, 8, 2, 2, 2, 16, 4>(c, s);
     case 256: return launch_t<1, 4, 4, 2, 2, 16, 4>(c, s);

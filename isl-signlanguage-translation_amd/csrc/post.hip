@@ -125,12 +125,22 @@ constexpr int RS_TY = 64, RS_TX = 256, RS_MAXR = 40;   // 64 rows: amortise the 
 // depend on the row only; per thread they were most of the vertical pass's VALU work), and
 // the block is TX = 128 or 256 columns wide, whichever wastes fewer idle lanes on the
 // output width (launch_resize): the same values, bit for bit.
-template <int TX>
+// WIN: the tile's source window (rows [r_lo, r_lo + nr) x columns [c_lo, c_lo + nc), nc <=
+// RS_WINC) is first staged in LDS with every load in flight at once, and the horizontal pass
+// reads it there (upsampling tiles: the gathers were one L2 round trip per 8 source rows).
+// VU: vertical outputs per unrolled step.  The arithmetic is the same either way.
+constexpr int RS_WINC = 80;
+// BM (mode 1, 64-row tiles of 128 columns): also the max |value| of every 16-row band x
+// 64-column word of the output plane into bandmax[plane][oh / 16][ow / 64] (the blur's tile
+// liveness, blur_tile: a tile whose window's bands stay below the threshold loads nothing)
+constexpr int BM_ROWS = 16;
+template <int TX, int VU = 1, bool WIN = false, int HU = 8, bool BM = false>
 __global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int oh, int ow, int ty_rows, int mode,
-                                                         float inv_div_f, void* out) {
+                                                         float inv_div_f, void* out, float* bandmax = nullptr) {
   __shared__ float s_h[RS_MAXR][TX];
   __shared__ int4 s_yi[RS_TY];
   __shared__ float4 s_be[RS_TY];
+  __shared__ float s_win[WIN ? RS_MAXR : 1][WIN ? RS_WINC : 1];
   const int plane = blockIdx.x, f = plane / nch, c = plane - f * nch;
   const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * TX + threadIdx.x;
   const int ny = min(ty_rows, oh - y0);
@@ -153,7 +163,31 @@ __global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int o
     }
   }
   if (nr > RS_MAXR) __builtin_trap();   // the host sizes ty_rows so that this cannot happen
-  if (x < ow) {
+  if constexpr (WIN) {
+    // (host: non-identity maps whose tile windows fit RS_WINC columns)
+    const int x0 = blockIdx.z * TX, x1 = min(x0 + TX, ow) - 1;
+    int lo[4], hi[4];
+    float dmy[4];
+    taps(x0, m.scx, m.sw, lo, dmy);
+    taps(x1, m.scx, m.sw, hi, dmy);
+    const int c_lo = lo[0], nc = hi[3] - c_lo + 1;
+    if (nc > RS_WINC) __builtin_trap();
+    for (int i = threadIdx.x; i < nr * nc; i += TX) {
+      const int r = i / nc, cc = i - r * nc;
+      s_win[r][cc] = b[(size_t)(r_lo + r) * m.ys + (size_t)(c_lo + cc) * m.xs];
+    }
+    __syncthreads();
+    if (x < ow) {
+      int xi[4];
+      float a[4];
+      taps(x, m.scx, m.sw, xi, a);
+      const int i0 = xi[0] - c_lo, i1 = xi[1] - c_lo, i2 = xi[2] - c_lo, i3 = xi[3] - c_lo;
+      for (int r = 0; r < nr; ++r) {
+        const float* row = s_win[r];
+        s_h[r][threadIdx.x] = ((row[i0] * a[0] + row[i1] * a[1]) + row[i2] * a[2]) + row[i3] * a[3];
+      }
+    }
+  } else if (x < ow) {
     if (m.identity) {
       for (int r = 0; r < nr; ++r) s_h[r][threadIdx.x] = b[(size_t)(r_lo + r) * m.ys + (size_t)x * m.xs];
     } else {
@@ -163,7 +197,7 @@ __global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int o
       const long long o0 = xi[0] * m.xs, o1 = xi[1] * m.xs, o2 = xi[2] * m.xs, o3 = xi[3] * m.xs;
       // 8 rows' loads in flight at a time: the row loop is otherwise one L2 round trip per row
       // (Mode R post 1.60 -> 1.48 ms against a rolled loop, profiles/r03/resize_ab/)
-#pragma unroll 8
+#pragma unroll HU
       for (int r = 0; r < nr; ++r) {
         const float* row = b + (size_t)(r_lo + r) * m.ys;
         s_h[r][threadIdx.x] = ((row[o0] * a[0] + row[o1] * a[1]) + row[o2] * a[2]) + row[o3] * a[3];
@@ -171,33 +205,48 @@ __global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int o
     }
   }
   __syncthreads();
-  if (x >= ow) return;
+  if (!BM && x >= ow) return;   // (BM: every lane takes part in the band maxima's shuffles)
   const int rowlen = m.dw * m.cn, body = rowlen - rowlen % 4;
   const bool simd = x * m.cn + c < body;
+  float bmx = 0.f;
+#pragma unroll VU
   for (int t = 0; t < ny; ++t) {
     const int y = y0 + t;
-    float v;
-    if (m.identity) {
-      v = s_h[t][threadIdx.x];
-    } else {
-      const int4 yi = s_yi[t];
-      const float4 be = s_be[t];
-      const float h0 = s_h[yi.x][threadIdx.x], h1 = s_h[yi.y][threadIdx.x];
-      const float h2 = s_h[yi.z][threadIdx.x], h3 = s_h[yi.w][threadIdx.x];
-      v = simd ? h0 * be.x + (h1 * be.y + (h2 * be.z + h3 * be.w))   // VResizeCubicVec_32f body
-               : ((h0 * be.x + h1 * be.y) + h2 * be.z) + h3 * be.w;   // scalar tail
+    float v = 0.f;
+    if (!BM || x < ow) {
+      if (m.identity) {
+        v = s_h[t][threadIdx.x];
+      } else {
+        const int4 yi = s_yi[t];
+        const float4 be = s_be[t];
+        const float h0 = s_h[yi.x][threadIdx.x], h1 = s_h[yi.y][threadIdx.x];
+        const float h2 = s_h[yi.z][threadIdx.x], h3 = s_h[yi.w][threadIdx.x];
+        v = simd ? h0 * be.x + (h1 * be.y + (h2 * be.z + h3 * be.w))   // VResizeCubicVec_32f body
+                 : ((h0 * be.x + h1 * be.y) + h2 * be.z) + h3 * be.w;   // scalar tail
+      }
+      const size_t i = ((size_t)plane * oh + y) * ow + x;
+      if (BM || mode == 1) {
+        ((float*)out)[i] = v;
+      } else {
+        // mode | 8: the first scale -- the accumulator is the reference's np.zeros, so it
+        // starts from +0.0 here instead of a memset pass (same bits, 0.0 + x included)
+        double* o = (double*)out + i;
+        const double o0 = (mode & 8) ? 0.0 : *o;
+        const float q = v / inv_div_f;   // heatmap / len(multiplier), float32
+        if ((mode & 7) == 2) *o = o0 + (o0 + (double)q);   // body.py:80, the doubling quirk
+        else *o = o0 + (double)q;                          // hand.py:56
+      }
     }
-    const size_t i = ((size_t)plane * oh + y) * ow + x;
-    if (mode == 1) {
-      ((float*)out)[i] = v;
-    } else {
-      // mode | 8: the first scale -- the accumulator is the reference's np.zeros, so it
-      // starts from +0.0 here instead of a memset pass (same bits, 0.0 + x included)
-      double* o = (double*)out + i;
-      const double o0 = (mode & 8) ? 0.0 : *o;
-      const float q = v / inv_div_f;   // heatmap / len(multiplier), float32
-      if ((mode & 7) == 2) *o = o0 + (o0 + (double)q);   // body.py:80, the doubling quirk
-      else *o = o0 + (double)q;                          // hand.py:56
+    if constexpr (BM) {
+      bmx = fmaxf(bmx, fabsf(v));   // (0 past the plane's width)
+      if (t % BM_ROWS == BM_ROWS - 1 || t == ny - 1) {   // a band ends (uniform): max over the wave's 64 columns
+        float w = bmx;
+        for (int o = 32; o > 0; o >>= 1) w = fmaxf(w, __shfl_xor(w, o));
+        const int words = (ow + 63) / 64, bands = (oh + BM_ROWS - 1) / BM_ROWS;
+        if ((threadIdx.x & 63) == 0 && blockIdx.z * TX + (threadIdx.x & ~63) < ow)
+          bandmax[((size_t)plane * bands + y / BM_ROWS) * words + (blockIdx.z * TX + threadIdx.x) / 64] = w;
+        bmx = 0.f;
+      }
     }
   }
 }
@@ -363,7 +412,8 @@ constexpr double CUBIC_ABS_SUM_SQ = 1.890625;      // max over t of (sum_k |cubi
 template <typename T, bool FUSED, int WR = NMS_SRC_ROWS, int WC = NMS_SRC_COLS>
 __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, int W, int words,
                                           unsigned long long* __restrict__ mask, double thre, int mode_hand,
-                                          const MapSrc& m, int nch, int plane, int by, int bx) {
+                                          const MapSrc& m, int nch, int plane, int by, int bx,
+                                          const float* __restrict__ bandmax) {
   // one LDS tile: v (axis-0 result), then g written in place over it (the
   // horizontal pass holds its v run in registers across a barrier) -> 31 KB,
   // so 4 blocks fit a CU and hide each other's load latency
@@ -381,6 +431,36 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
   const int lane = tid & 63, wave = tid >> 6;
   if (tid == 0) s_live = 0;
   __syncthreads();
+  if constexpr (!FUSED) {
+    // Early out before any plane load (bandmax: the resize's max |value| per 16-row band x
+    // 64-column word, resize_sep_kernel BM): the window's rows and columns, reflected, lie in
+    // those bands and words, so the same exact bound as below holds with their maximum
+    if (bandmax) {
+      if (tid < 64) {
+        int rlo, rhi, clo, chi;
+        reflect_range(y0 - 1 - NMS_R, y0 - 2 - NMS_R + NMS_IR, H, &rlo, &rhi);
+        reflect_range(x0 - 1 - NMS_R, x0 - 2 - NMS_R + NMS_VC, W, &clo, &chi);
+        const int b0 = rlo / BM_ROWS, nb = rhi / BM_ROWS - b0 + 1, w0 = clo / 64, nw = chi / 64 - w0 + 1;
+        const int bands = (H + BM_ROWS - 1) / BM_ROWS;
+        float mx = nb * nw > 64 ? 1e30f : 0.f;    // (tiny planes: no early out)
+        if (tid < nb * nw)
+          mx = fmaxf(mx, bandmax[((size_t)plane * bands + b0 + tid / nw) * words + w0 + tid % nw]);
+        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+        if (tid == 0 && (double)mx >= thre * (1.0 - 1e-9)) s_live = 1;
+      }
+      __syncthreads();
+      if (!s_live) {
+        for (int it = wave; it < NMS_TY * 3; it += 4) {
+          const int y = y0 + it / 3, wi = bx * 3 + it % 3;
+          if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = 0ull;
+        }
+        return;
+      }
+      __syncthreads();   // everyone has read s_live before the exact bound below resets it
+      if (tid == 0) s_live = 0;
+      __syncthreads();
+    }
+  }
   // axis 0 (NI_Correlate1D, symmetric): o = c*w0; for j = 12..1: o += (a[-j] + a[+j]) * w[j]
   double in[NMS_IR];
   if constexpr (!FUSED) {
@@ -549,16 +629,17 @@ template <typename T, bool FUSED, int WR = NMS_SRC_ROWS, int WC = NMS_SRC_COLS>
 __global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ planes, int H, int W, int words,
                                                         unsigned long long* __restrict__ mask, double thre,
                                                         int mode_hand, MapSrc m, int nch, const int* __restrict__ live,
-                                                        const int* __restrict__ live_count, int tiles_x, int tiles_y) {
+                                                        const int* __restrict__ live_count, int tiles_x, int tiles_y,
+                                                        const float* __restrict__ bandmax = nullptr) {
   if constexpr (!FUSED) {
-    blur_tile<T, false>(planes, H, W, words, mask, thre, mode_hand, m, nch, blockIdx.z, blockIdx.y, blockIdx.x);
+    blur_tile<T, false>(planes, H, W, words, mask, thre, mode_hand, m, nch, blockIdx.z, blockIdx.y, blockIdx.x, bandmax);
   } else {
     // grid-stride over the live tiles found by tile_live_kernel (mask pre-zeroed)
     const int cnt = *live_count;
     for (int k = blockIdx.x; k < cnt; k += gridDim.x) {
       const int t = live[k];
       const int bx = t % tiles_x, r = t / tiles_x, by = r % tiles_y, plane = r / tiles_y;
-      blur_tile<T, true, WR, WC>(planes, H, W, words, mask, thre, mode_hand, m, nch, plane, by, bx);
+      blur_tile<T, true, WR, WC>(planes, H, W, words, mask, thre, mode_hand, m, nch, plane, by, bx, nullptr);
       __syncthreads();   // LDS reuse by the next tile
     }
   }
@@ -1995,17 +2076,39 @@ static int post_fail(int code, const char* msg) {
   } while (0)
 
 // planar resize of n*nch planes (see resize_sep_kernel); rows per tile sized to the LDS window
+// bandmax (mode 1): also write the band maxima of the output planes (resize_sep_kernel BM) when
+// the tiles align with the bands; *bm_done says whether they were written
 static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mode, float div_f, void* out,
-                         hipStream_t s) {
+                         hipStream_t s, float* bandmax = nullptr, bool* bm_done = nullptr) {
   int ty = RS_TY;
   if (!m.identity)
     while (ty > 1 && (ty - 1) * m.scy + 5.0 > (double)RS_MAXR) --ty;
   const long long ty_tiles = (oh + ty - 1) / ty;
   if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "resize: output too tall");
+  if (bm_done) *bm_done = false;
+  if (bandmax && mode == 1 && ty % BM_ROWS == 0) {
+    hipLaunchKernelGGL((resize_sep_kernel<128, 1, false, 8, true>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128),
+                       dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out, bandmax);
+    PHIP(hipGetLastError());
+    if (bm_done) *bm_done = true;
+    return ISL_OK;
+  }
   // 128-column blocks unless 256 pads less (it never does): fewer idle lanes (ow = 328: 384 vs
   // 512), and at equal padding (ow = 656) twice the resident blocks: Mode R batch-32 post
   // 1.51 / 1.49 -> 1.47 / 1.47 ms; 32 or 16 rows per block lost (profiles/r03/rsty/)
-  if ((ow + 127) / 128 * 128 <= (ow + RS_TX - 1) / RS_TX * RS_TX)
+  const char* e = getenv("ISLPOSE_RESIZE");   // A/B: "<vertical unroll 1|4><window 0|1|2: 16 rows in flight>"
+  const int vu = e && e[0] == '4' ? 4 : 1;
+  const bool win = e && e[0] && e[1] == '1' && !m.identity && m.scx <= 0.55 &&
+                   (int)(128 * m.scx) + 6 <= RS_WINC;
+  const bool hu = e && e[0] && e[1] == '2';
+  if (vu == 4 || win || hu) {
+    dim3 g(n * nch, (unsigned)ty_tiles, (ow + 127) / 128);
+    if (hu && vu == 4) hipLaunchKernelGGL((resize_sep_kernel<128, 4, false, 16>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
+    else if (hu) hipLaunchKernelGGL((resize_sep_kernel<128, 1, false, 16>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
+    else if (vu == 4 && win) hipLaunchKernelGGL((resize_sep_kernel<128, 4, true>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
+    else if (win) hipLaunchKernelGGL((resize_sep_kernel<128, 1, true>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
+    else hipLaunchKernelGGL((resize_sep_kernel<128, 4, false>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
+  } else if ((ow + 127) / 128 * 128 <= (ow + RS_TX - 1) / RS_TX * RS_TX)
     hipLaunchKernelGGL(resize_sep_kernel<128>, dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128), dim3(128), 0, s,
                        m, nch, oh, ow, ty, mode, div_f, out);
   else
@@ -2074,9 +2177,14 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   const size_t used_bytes = (size_t)n * nlimbs * 2 * caps->max_peaks;
   const size_t n_tiles_all = (size_t)((W + NMS_TX - 1) / NMS_TX) * ((H + NMS_TY - 1) / NMS_TY) * n * nparts;
   const size_t live_bytes = fused ? (n_tiles_all + 1) * sizeof(int) : 0;
+  // single scale, materialised planes: the band maxima of the final resize (blur early out)
+  // (ISLPOSE_BLUR_BANDS=0: without, A/B; read per call)
+  const char* bme = getenv("ISLPOSE_BLUR_BANDS");
+  const bool bands_on = !(bme && bme[0] == '0');
+  const size_t bm_bytes = (!fused && !multi && bands_on) ? (size_t)n * nparts * ((H + BM_ROWS - 1) / BM_ROWS) * words * 4 : 0;
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t total = up(heat_bytes) + up(mid_bytes) + up(mask_bytes) + up(pair_bytes) + up(used_bytes) +
-                       up(live_bytes);
+                       up(live_bytes) + up(bm_bytes);
   char* base = (char*)net_scratch(net, total);
   if (!base) return ISL_E_HIP;
   char* heat = base;
@@ -2086,6 +2194,8 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   unsigned char* used = (unsigned char*)(pairs + up(pair_bytes));
   int* live_count = (int*)(used + up(used_bytes));
   int* live = live_count + 1;
+  float* bandmax = bm_bytes ? (float*)((char*)live_count + up(live_bytes)) : nullptr;
+  bool bm_done = false;
 
   hipLaunchKernelGGL(init_records_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (char*)d_result, lay, n, nlimbs);
   PHIP(hipGetLastError());
@@ -2132,7 +2242,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     }
     if (fused) fused_src = fh;   // no full-resolution heat: blur_nms resizes on the fly
     else if (multi) fin.m[si] = fh;   // every scale's final resize, one fp64 pass below
-    else if ((rc = launch_resize(fh, n, nparts, H, W, 1, div_f, heat, s))) return rc;
+    else if ((rc = launch_resize(fh, n, nparts, H, W, 1, div_f, heat, s, bandmax, &bm_done))) return rc;
     ga.paf[si] = fp;
   }
   if (multi) {
@@ -2178,7 +2288,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     }
   } else
     hipLaunchKernelGGL((blur_nms_kernel<float, false>), gb, dim3(256), 0, s, (const float*)heat, H, W, words, mask,
-                       0.1, 0, MapSrc{}, 0, nullptr, nullptr, 0, 0);
+                       0.1, 0, MapSrc{}, 0, nullptr, nullptr, 0, 0, bm_done ? (const float*)bandmax : nullptr);
   PHIP(hipGetLastError());
   if (multi)
     hipLaunchKernelGGL((compact_kernel<double, false>), dim3(nparts, n), dim3(256), 0, s, mask, (const double*)heat,

@@ -125,22 +125,18 @@ constexpr int RS_TY = 64, RS_TX = 256, RS_MAXR = 40;   // 64 rows: amortise the 
 // depend on the row only; per thread they were most of the vertical pass's VALU work), and
 // the block is TX = 128 or 256 columns wide, whichever wastes fewer idle lanes on the
 // output width (launch_resize): the same values, bit for bit.
-// WIN: the tile's source window (rows [r_lo, r_lo + nr) x columns [c_lo, c_lo + nc), nc <=
-// RS_WINC) is first staged in LDS with every load in flight at once, and the horizontal pass
-// reads it there (upsampling tiles: the gathers were one L2 round trip per 8 source rows).
-// VU: vertical outputs per unrolled step.  The arithmetic is the same either way.
-constexpr int RS_WINC = 80;
+// VU: vertical outputs per unrolled step; HU: source rows' loads in flight.  The arithmetic is
+// the same either way.
 // BM (mode 1, 64-row tiles of 128 columns): also the max |value| of every 16-row band x
 // 64-column word of the output plane into bandmax[plane][oh / 16][ow / 64] (the blur's tile
 // liveness, blur_tile: a tile whose window's bands stay below the threshold loads nothing)
 constexpr int BM_ROWS = 16;
-template <int TX, int VU = 1, bool WIN = false, int HU = 8, bool BM = false>
+template <int TX, int VU = 1, int HU = 8, bool BM = false>
 __global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int oh, int ow, int ty_rows, int mode,
                                                          float inv_div_f, void* out, float* bandmax = nullptr) {
   __shared__ float s_h[RS_MAXR][TX];
   __shared__ int4 s_yi[RS_TY];
   __shared__ float4 s_be[RS_TY];
-  __shared__ float s_win[WIN ? RS_MAXR : 1][WIN ? RS_WINC : 1];
   const int plane = blockIdx.x, f = plane / nch, c = plane - f * nch;
   const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * TX + threadIdx.x;
   const int ny = min(ty_rows, oh - y0);
@@ -163,31 +159,7 @@ __global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int o
     }
   }
   if (nr > RS_MAXR) __builtin_trap();   // the host sizes ty_rows so that this cannot happen
-  if constexpr (WIN) {
-    // (host: non-identity maps whose tile windows fit RS_WINC columns)
-    const int x0 = blockIdx.z * TX, x1 = min(x0 + TX, ow) - 1;
-    int lo[4], hi[4];
-    float dmy[4];
-    taps(x0, m.scx, m.sw, lo, dmy);
-    taps(x1, m.scx, m.sw, hi, dmy);
-    const int c_lo = lo[0], nc = hi[3] - c_lo + 1;
-    if (nc > RS_WINC) __builtin_trap();
-    for (int i = threadIdx.x; i < nr * nc; i += TX) {
-      const int r = i / nc, cc = i - r * nc;
-      s_win[r][cc] = b[(size_t)(r_lo + r) * m.ys + (size_t)(c_lo + cc) * m.xs];
-    }
-    __syncthreads();
-    if (x < ow) {
-      int xi[4];
-      float a[4];
-      taps(x, m.scx, m.sw, xi, a);
-      const int i0 = xi[0] - c_lo, i1 = xi[1] - c_lo, i2 = xi[2] - c_lo, i3 = xi[3] - c_lo;
-      for (int r = 0; r < nr; ++r) {
-        const float* row = s_win[r];
-        s_h[r][threadIdx.x] = ((row[i0] * a[0] + row[i1] * a[1]) + row[i2] * a[2]) + row[i3] * a[3];
-      }
-    }
-  } else if (x < ow) {
+  if (x < ow) {
     if (m.identity) {
       for (int r = 0; r < nr; ++r) s_h[r][threadIdx.x] = b[(size_t)(r_lo + r) * m.ys + (size_t)x * m.xs];
     } else {
@@ -437,16 +409,30 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
     // those bands and words, so the same exact bound as below holds with their maximum
     if (bandmax) {
       if (tid < 64) {
+        // the tile's window and each of its three mask words' input columns (window columns
+        // 64w .. 64w+89), reflected, against the table's bands x words
         int rlo, rhi, clo, chi;
         reflect_range(y0 - 1 - NMS_R, y0 - 2 - NMS_R + NMS_IR, H, &rlo, &rhi);
         reflect_range(x0 - 1 - NMS_R, x0 - 2 - NMS_R + NMS_VC, W, &clo, &chi);
         const int b0 = rlo / BM_ROWS, nb = rhi / BM_ROWS - b0 + 1, w0 = clo / 64, nw = chi / 64 - w0 + 1;
         const int bands = (H + BM_ROWS - 1) / BM_ROWS;
-        float mx = nb * nw > 64 ? 1e30f : 0.f;    // (tiny planes: no early out)
-        if (tid < nb * nw)
-          mx = fmaxf(mx, bandmax[((size_t)plane * bands + b0 + tid / nw) * words + w0 + tid % nw]);
+        const bool all = nb * nw > 64;             // (tiny planes: no early out)
+        float v = 0.f;
+        int tw = -1;
+        if (tid < nb * nw) {
+          tw = w0 + tid % nw;
+          v = bandmax[((size_t)plane * bands + b0 + tid / nw) * words + tw];
+        }
+        float mx = all ? 1e30f : v;
         for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
         if (tid == 0 && (double)mx >= thre * (1.0 - 1e-9)) s_live = 1;
+        for (int wd = 0; wd < 3; ++wd) {
+          int wlo, whi;
+          reflect_range(x0 - 1 - NMS_R + 64 * wd, x0 - 1 - NMS_R + min(64 * wd + 89, NMS_VC - 1), W, &wlo, &whi);
+          float m = all ? 1e30f : (tw >= wlo / 64 && tw <= whi / 64 ? v : 0.f);
+          for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+          if (tid == 0) s_wlive[wd] = (double)m >= thre * (1.0 - 1e-9);
+        }
       }
       __syncthreads();
       if (!s_live) {
@@ -465,7 +451,15 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
   double in[NMS_IR];
   if constexpr (!FUSED) {
     const T* src = planes + (size_t)plane * H * W;
-    if (tid < NMS_VC) {
+    // (bandmax: columns only dead words read are not loaded -- their values are below the
+    // threshold, so zeros give the same liveness)
+    const bool ld = !bandmax || (s_wlive[0] && tid <= 89) || (s_wlive[1] && tid >= 64 && tid <= 153) ||
+                    (s_wlive[2] && tid >= 128);
+    if (tid < NMS_VC && !ld) {
+#pragma unroll
+      for (int r = 0; r < NMS_IR; ++r) in[r] = 0.0;
+      s_cmax[tid] = 0.0;
+    } else if (tid < NMS_VC) {
       const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
       double amax = 0.0;
 #pragma unroll
@@ -2087,7 +2081,7 @@ static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mo
   if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "resize: output too tall");
   if (bm_done) *bm_done = false;
   if (bandmax && mode == 1 && ty % BM_ROWS == 0) {
-    hipLaunchKernelGGL((resize_sep_kernel<128, 1, false, 8, true>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128),
+    hipLaunchKernelGGL((resize_sep_kernel<128, 4, 8, true>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128),
                        dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out, bandmax);
     PHIP(hipGetLastError());
     if (bm_done) *bm_done = true;
@@ -2096,23 +2090,14 @@ static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mo
   // 128-column blocks unless 256 pads less (it never does): fewer idle lanes (ow = 328: 384 vs
   // 512), and at equal padding (ow = 656) twice the resident blocks: Mode R batch-32 post
   // 1.51 / 1.49 -> 1.47 / 1.47 ms; 32 or 16 rows per block lost (profiles/r03/rsty/)
-  const char* e = getenv("ISLPOSE_RESIZE");   // A/B: "<vertical unroll 1|4><window 0|1|2: 16 rows in flight>"
-  const int vu = e && e[0] == '4' ? 4 : 1;
-  const bool win = e && e[0] && e[1] == '1' && !m.identity && m.scx <= 0.55 &&
-                   (int)(128 * m.scx) + 6 <= RS_WINC;
-  const bool hu = e && e[0] && e[1] == '2';
-  if (vu == 4 || win || hu) {
-    dim3 g(n * nch, (unsigned)ty_tiles, (ow + 127) / 128);
-    if (hu && vu == 4) hipLaunchKernelGGL((resize_sep_kernel<128, 4, false, 16>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
-    else if (hu) hipLaunchKernelGGL((resize_sep_kernel<128, 1, false, 16>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
-    else if (vu == 4 && win) hipLaunchKernelGGL((resize_sep_kernel<128, 4, true>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
-    else if (win) hipLaunchKernelGGL((resize_sep_kernel<128, 1, true>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
-    else hipLaunchKernelGGL((resize_sep_kernel<128, 4, false>), g, dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
-  } else if ((ow + 127) / 128 * 128 <= (ow + RS_TX - 1) / RS_TX * RS_TX)
-    hipLaunchKernelGGL(resize_sep_kernel<128>, dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128), dim3(128), 0, s,
+  // vertical pass unrolled by 4: Mode R batch-32 post -2.5 %, batch 1 -1.8 %; staging the
+  // source window in LDS lost 20 %, 16 source rows in flight instead of 8 gained nothing
+  // (tools/resize_ab.py, profiles/r04/r4d/resize_ab.json)
+  if ((ow + 127) / 128 * 128 <= (ow + RS_TX - 1) / RS_TX * RS_TX)
+    hipLaunchKernelGGL((resize_sep_kernel<128, 4>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128), dim3(128), 0, s,
                        m, nch, oh, ow, ty, mode, div_f, out);
   else
-    hipLaunchKernelGGL(resize_sep_kernel<RS_TX>, dim3(n * nch, (unsigned)ty_tiles, (ow + RS_TX - 1) / RS_TX),
+    hipLaunchKernelGGL((resize_sep_kernel<RS_TX, 4>), dim3(n * nch, (unsigned)ty_tiles, (ow + RS_TX - 1) / RS_TX),
                        dim3(RS_TX), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
   PHIP(hipGetLastError());
   return ISL_OK;

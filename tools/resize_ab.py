@@ -1,5 +1,5 @@
-"""A/B of the cubic resize variants (ISLPOSE_RESIZE=<vertical unroll 1|4><staged window 0|1>)
-on the Mode R post (scale 0.5: the two-stage resizes), batch 32 and batch 1, designed maps:
+"""A/B of the blur's band-maxima early out (ISLPOSE_BLUR_BANDS=0|1; round 4 also used it for the
+resize variants, profiles/r04/r4d/resize_ab.json) on the Mode R post (scale 0.5: the two-stage resizes), batch 32 and batch 1, designed maps:
 HIP-event time per post call, and the records equal across variants (dev tool)."""
 import json
 import os
@@ -27,8 +27,7 @@ def main():
         heat = torch.from_numpy(np.stack([b for _, b in des])).cuda()
         ref = None
         for rounds in range(2):
-            for v in ("10", "40", "12", "42", "B0"):
-                os.environ["ISLPOSE_RESIZE"] = v if v[0] != "B" else "10"
+            for v in ("B1", "B0"):
                 os.environ["ISLPOSE_BLUR_BANDS"] = "0" if v == "B0" else "1"
                 res = est.post_maps(H, W, geoms, [paf], [heat])
                 if ref is None:

@@ -409,8 +409,8 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
     // those bands and words, so the same exact bound as below holds with their maximum
     if (bandmax) {
       if (tid < 64) {
-        // the tile's window and each of its three mask words' input columns (window columns
-        // 64w .. 64w+89), reflected, against the table's bands x words
+        // the tile's window, reflected, against the table's bands x words (a word-level
+        // version that skipped the loads of dead words' columns measured level, r04/r4f)
         int rlo, rhi, clo, chi;
         reflect_range(y0 - 1 - NMS_R, y0 - 2 - NMS_R + NMS_IR, H, &rlo, &rhi);
         reflect_range(x0 - 1 - NMS_R, x0 - 2 - NMS_R + NMS_VC, W, &clo, &chi);
@@ -418,21 +418,10 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
         const int bands = (H + BM_ROWS - 1) / BM_ROWS;
         const bool all = nb * nw > 64;             // (tiny planes: no early out)
         float v = 0.f;
-        int tw = -1;
-        if (tid < nb * nw) {
-          tw = w0 + tid % nw;
-          v = bandmax[((size_t)plane * bands + b0 + tid / nw) * words + tw];
-        }
+        if (tid < nb * nw) v = bandmax[((size_t)plane * bands + b0 + tid / nw) * words + w0 + tid % nw];
         float mx = all ? 1e30f : v;
         for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
         if (tid == 0 && (double)mx >= thre * (1.0 - 1e-9)) s_live = 1;
-        for (int wd = 0; wd < 3; ++wd) {
-          int wlo, whi;
-          reflect_range(x0 - 1 - NMS_R + 64 * wd, x0 - 1 - NMS_R + min(64 * wd + 89, NMS_VC - 1), W, &wlo, &whi);
-          float m = all ? 1e30f : (tw >= wlo / 64 && tw <= whi / 64 ? v : 0.f);
-          for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-          if (tid == 0) s_wlive[wd] = (double)m >= thre * (1.0 - 1e-9);
-        }
       }
       __syncthreads();
       if (!s_live) {
@@ -451,15 +440,7 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
   double in[NMS_IR];
   if constexpr (!FUSED) {
     const T* src = planes + (size_t)plane * H * W;
-    // (bandmax: columns only dead words read are not loaded -- their values are below the
-    // threshold, so zeros give the same liveness)
-    const bool ld = !bandmax || (s_wlive[0] && tid <= 89) || (s_wlive[1] && tid >= 64 && tid <= 153) ||
-                    (s_wlive[2] && tid >= 128);
-    if (tid < NMS_VC && !ld) {
-#pragma unroll
-      for (int r = 0; r < NMS_IR; ++r) in[r] = 0.0;
-      s_cmax[tid] = 0.0;
-    } else if (tid < NMS_VC) {
+    if (tid < NMS_VC) {
       const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
       double amax = 0.0;
 #pragma unroll

@@ -26,9 +26,9 @@ def main():
         paf = torch.from_numpy(np.stack([a for a, _ in des])).cuda()
         heat = torch.from_numpy(np.stack([b for _, b in des])).cuda()
         ref = None
-        for rounds in range(2):
+        for rounds in range(4):
             for v in ("B1", "B0"):
-                os.environ["ISLPOSE_BLUR_BANDS"] = "0" if v == "B0" else "1"
+                os.environ["ISLPOSE_BLUR_BANDS"] = v[1]
                 res = est.post_maps(H, W, geoms, [paf], [heat])
                 if ref is None:
                     ref = res

@@ -28,6 +28,10 @@ build_dev/%.o: $(CSRC)/% $(CSRC)/internal.h include/islpose.h
 	@mkdir -p build_dev
 	$(HIPCC) $(HIPFLAGS) -DISLPOSE_DEV -x hip -c $< -o $@
 
+# development library (ISLPOSE_LIB=tools/libislpose_dev.so: tools/tile_prof.py)
+tools/libislpose_dev.so: $(DEV_OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -Wl,-z,defs -o $@ $^
+
 clean:
 	rm -rf build build_dev $(OUT)
 

@@ -380,19 +380,166 @@ __device__ __forceinline__ void fused_window(const MapSrc& m, int H, int W, int 
 // covered by the 1.9 / 1.890625 margin; then |g| <= max|resized| * (1 + 1e-13).
 constexpr double CUBIC_ABS_SUM_SQ = 1.890625;      // max over t of (sum_k |cubic_k(t)|)^2, A = -0.75
 
+// The fp32 filter (default): the two passes in packed fp32 with fused multiply-adds
+// (v_pk_fma_f32: two outputs per instruction, 25 instructions per output pair against 37
+// fp64 per output), a column pair per thread in the vertical pass, a row pair per thread in
+// the horizontal one.  Bound: each tap of the scipy recurrence goes through at most 14
+// roundings (weight, pair sum, 12 accumulations) and the weights are positive with sum 1,
+// so with M = max |in| over the tile's window |v32 - v| <= 14.01 u M and |g32 - g| <= 28.1 u M
+// (u = 2^-24; the fp64 passes and the fp32 rounding of fp64 planes add < 1.1 u M).  With
+// eps = 2^-18 M (64 u M) a pixel whose every comparison clears the margin (g vs thre by eps,
+// g vs a neighbour by 2 eps) has the fp64 decision; a tile with any pixel inside a margin
+// (a peak at the threshold, two near-equal neighbours at a peak: rare) is appended to a list
+// that a second launch re-runs on the exact fp64 passes (blur_tile_exact), which rewrite all
+// of the tile's words.  The mask bits are the fp64 ones either way.  The filter's tile keeps
+// no fp64 planes and no staged window: 19 KB of LDS (37 KB fused) against 33 / 52 KB.
+typedef float f2v __attribute__((ext_vector_type(2)));
+constexpr double kGaussC[13] = {
+    0x1.105a329f98197p-3, 0x1.01a25f86eb137p-3, 0x1.b42a57d56c0bep-4, 0x1.4a614d1afd337p-4,
+    0x1.bfde9c12bec92p-5, 0x1.0fa58939b528fp-5, 0x1.26defcaeb0202p-6, 0x1.1e6bccad344bap-7,
+    0x1.f1e9915139406p-9, 0x1.8345966f69518p-10, 0x1.0d8a5ad43c165p-11, 0x1.4fbe39149e277p-13,
+    0x1.763a210dfb306p-15};
+constexpr float kGaussF[13] = {(float)kGaussC[0],  (float)kGaussC[1],  (float)kGaussC[2],  (float)kGaussC[3],
+                               (float)kGaussC[4],  (float)kGaussC[5],  (float)kGaussC[6],  (float)kGaussC[7],
+                               (float)kGaussC[8],  (float)kGaussC[9],  (float)kGaussC[10], (float)kGaussC[11],
+                               (float)kGaussC[12]};
+constexpr double BLUR_EPS_REL = 0x1p-18;
+constexpr int NMS_CP = NMS_VC / 2;                  // column pairs of the filter's vertical pass (109)
+constexpr int NMS_VH = NMS_VR / 2;                  // v rows per thread (two waves' worth per half)
+constexpr int NMS_HSEG = 7, NMS_HRUNS = 28;         // filter horizontal pass: 9 row pairs x 28 runs of 7
+static_assert(NMS_VC % 2 == 0 && NMS_VR % 2 == 0 && NMS_CP <= 128 && NMS_HSEG * NMS_HRUNS >= NMS_GC &&
+                  NMS_VR / 2 * NMS_HRUNS <= 256,
+              "filter tiling");
+
+// Development build only: per-tile phase stamps of the blur (tools/tile_prof.py) -- 10 u64
+// per tile: wall clock at start / end, shader clock at start, after the prologue (band or
+// low-res bound, the fused horizontal resize), after the window, after the vertical pass,
+// after the horizontal pass, after the NMS, the fallback flag (the filter appended the
+// tile), at the exact re-run's end (0 where a phase never ran)
+#ifdef ISLPOSE_DEV
+__device__ unsigned long long* g_tile_prof = nullptr;
+#define TPROF(k, v)                                                                               \
+  do {                                                                                            \
+    if (g_tile_prof && tid == 0) {                                                                \
+      const long long tix =                                                                       \
+          ((long long)plane * ((H + NMS_TY - 1) / NMS_TY) + by) * ((W + NMS_TX - 1) / NMS_TX) + bx; \
+      g_tile_prof[tix * 10 + (k)] = (v);                                                          \
+    }                                                                                             \
+  } while (0)
+#else
+#define TPROF(k, v) \
+  do {              \
+  } while (0)
+#endif
+
+// The band-maxima early out shared by both tile functions (bandmax: resize_sep_kernel's max
+// |value| per 16-row band x 64-column word): the window's rows and columns, reflected, lie in
+// those bands and words, so the exact blur bound below holds with their maximum.  Wave 0
+// decides; true = the tile is dead.
+__device__ __forceinline__ bool band_dead(const float* __restrict__ bandmax, int plane, int H, int W, int words, int y0,
+                                          int x0, double thre, int* s_flag) {
+  const int tid = threadIdx.x;
+  if (tid == 0) *s_flag = 0;
+  __syncthreads();
+  if (tid < 64) {
+    int rlo, rhi, clo, chi;
+    reflect_range(y0 - 1 - NMS_R, y0 - 2 - NMS_R + NMS_IR, H, &rlo, &rhi);
+    reflect_range(x0 - 1 - NMS_R, x0 - 2 - NMS_R + NMS_VC, W, &clo, &chi);
+    const int b0 = rlo / BM_ROWS, nb = rhi / BM_ROWS - b0 + 1, w0 = clo / 64, nw = chi / 64 - w0 + 1;
+    const int bands = (H + BM_ROWS - 1) / BM_ROWS;
+    const bool all = nb * nw > 64;             // (tiny planes: no early out)
+    float v = 0.f;
+    if (tid < nb * nw) v = bandmax[((size_t)plane * bands + b0 + tid / nw) * words + w0 + tid % nw];
+    float mx = all ? 1e30f : v;
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    if (tid == 0 && (double)mx >= thre * (1.0 - 1e-9)) *s_flag = 1;
+  }
+  __syncthreads();
+  const bool dead = !*s_flag;
+  __syncthreads();   // everyone has read the flag before it is reused
+  return dead;
+}
+
+// The fused single-scale prologue: the low-res window into LDS, the exact low-res bound
+// (false: the tile is dead), then the horizontal cubic pass of every window column and the
+// vertical taps of the window's rows (resize_sep_kernel's order).
+template <int WR, int WC>
+__device__ __forceinline__ bool fused_prologue(const MapSrc& m, int nch, int plane, int H, int W, int y0, int x0,
+                                               double thre, float (*s_low)[WC], float (*s_hz)[NMS_VC], int4* s_ti,
+                                               float4* s_tb, int* s_flag) {
+  const int tid = threadIdx.x;
+  const int f = plane / nch, c = plane - f * nch;
+  const float* b = m.base + (size_t)f * m.fs + chan_off(m, c);
+  int sr0, nsr, sc0, nsc;
+  fused_window(m, H, W, y0, x0, &sr0, &nsr, &sc0, &nsc);
+  if (nsr > WR) __builtin_trap();   // the host picks a window that holds the tile's source rows
+  // the low-res window is staged in LDS: one coalesced pass, reused by the resize
+  if (nsc > WC) __builtin_trap();
+  if (tid == 0) *s_flag = 0;
+  __syncthreads();
+  float amax = 0.f;
+  for (int i = tid; i < nsr * nsc; i += 256) {
+    const int r = i / nsc, cc = i - r * nsc;
+    const float v = b[(size_t)(sr0 + r) * m.ys + (size_t)(sc0 + cc) * m.xs];
+    s_low[r][cc] = v;
+    amax = fmaxf(amax, fabsf(v));
+  }
+  if ((double)amax * 1.9 >= thre * (1.0 - 1e-9)) *s_flag = 1;
+  __syncthreads();
+  const bool live_lr = *s_flag != 0;
+  __syncthreads();   // everyone has read the flag before it is reused
+  if (!live_lr) return false;
+  if (tid < NMS_VC) {
+    // horizontal cubic pass for the window column (OpenCV HResizeCubic order)
+    const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
+    int xi[4];
+    float a[4];
+    taps(xx, m.scx, m.sw, xi, a);
+    const int i0 = xi[0] - sc0, i1 = xi[1] - sc0, i2 = xi[2] - sc0, i3 = xi[3] - sc0;
+    for (int r = 0; r < nsr; ++r) {
+      const float* row = s_low[r];
+      s_hz[r][tid] = ((row[i0] * a[0] + row[i1] * a[1]) + row[i2] * a[2]) + row[i3] * a[3];
+    }
+  } else {
+    // vertical taps of the window's 42 rows, once per block (the 38 idle lanes)
+    for (int r = tid - NMS_VC; r < NMS_IR; r += 256 - NMS_VC) {
+      int yi[4];
+      float be[4];
+      taps(reflect_idx(y0 - 1 - NMS_R + r, H), m.scy, m.sh, yi, be);
+      s_ti[r] = make_int4(yi[0] - sr0, yi[1] - sr0, yi[2] - sr0, yi[3] - sr0);
+      s_tb[r] = make_float4(be[0], be[1], be[2], be[3]);
+    }
+  }
+  __syncthreads();
+  return true;
+}
+
+// window value of the fused path: resize_sep_kernel's vertical combine (VResizeCubicVec_32f
+// body / scalar tail) of window row r, column t (plane column xx)
+__device__ __forceinline__ float fused_value(const MapSrc& m, int c, float (*s_hz)[NMS_VC], const int4* s_ti,
+                                             const float4* s_tb, int r, int t, int xx) {
+  const int4 yi = s_ti[r];
+  const float4 be = s_tb[r];
+  const float h0 = s_hz[yi.x][t], h1 = s_hz[yi.y][t], h2 = s_hz[yi.z][t], h3 = s_hz[yi.w][t];
+  const int rowlen = m.dw * m.cn;
+  return xx * m.cn + c < rowlen - rowlen % 4 ? h0 * be.x + (h1 * be.y + (h2 * be.z + h3 * be.w))
+                                             : ((h0 * be.x + h1 * be.y) + h2 * be.z) + h3 * be.w;
+}
+
+// the exact fp64 passes (scipy's order) of one tile
 // planes: [n*nparts][H][W] (T = float or double); mask: [n*nparts][H][words]
 template <typename T, bool FUSED, int WR = NMS_SRC_ROWS, int WC = NMS_SRC_COLS>
-__device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, int W, int words,
-                                          unsigned long long* __restrict__ mask, double thre, int mode_hand,
-                                          const MapSrc& m, int nch, int plane, int by, int bx,
-                                          const float* __restrict__ bandmax) {
+__device__ __forceinline__ void blur_tile_exact(const T* __restrict__ planes, int H, int W, int words,
+                                                unsigned long long* __restrict__ mask, double thre, int mode_hand,
+                                                const MapSrc& m, int nch, int plane, int by, int bx,
+                                                const float* __restrict__ bandmax) {
   // one LDS tile: v (axis-0 result), then g written in place over it (the
   // horizontal pass holds its v run in registers across a barrier) -> 31 KB,
   // so 4 blocks fit a CU and hide each other's load latency
   __shared__ double s_v[NMS_VR][NMS_VC];
-  __shared__ float s_hz[FUSED ? WR : 1][FUSED ? NMS_VC : 1];
+  __shared__ float s_hz[FUSED ? WR : 1][NMS_VC];
   __shared__ int4 s_ti[FUSED ? NMS_IR : 1];
-  __shared__ float s_low[FUSED ? WR : 1][FUSED ? WC : 1];
+  __shared__ float s_low[FUSED ? WR : 1][WC];
   __shared__ float4 s_tb[FUSED ? NMS_IR : 1];
   __shared__ int s_live;
   __shared__ double s_cmax[NMS_VC];   // max |in| of every window column (word liveness)
@@ -401,129 +548,47 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
   const int y0 = by * NMS_TY, x0 = bx * NMS_TX;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_live = 0;
-  __syncthreads();
-  if constexpr (!FUSED) {
-    // Early out before any plane load (bandmax: the resize's max |value| per 16-row band x
-    // 64-column word, resize_sep_kernel BM): the window's rows and columns, reflected, lie in
-    // those bands and words, so the same exact bound as below holds with their maximum
-    if (bandmax) {
-      if (tid < 64) {
-        // the tile's window, reflected, against the table's bands x words (a word-level
-        // version that skipped the loads of dead words' columns measured level, r04/r4f)
-        int rlo, rhi, clo, chi;
-        reflect_range(y0 - 1 - NMS_R, y0 - 2 - NMS_R + NMS_IR, H, &rlo, &rhi);
-        reflect_range(x0 - 1 - NMS_R, x0 - 2 - NMS_R + NMS_VC, W, &clo, &chi);
-        const int b0 = rlo / BM_ROWS, nb = rhi / BM_ROWS - b0 + 1, w0 = clo / 64, nw = chi / 64 - w0 + 1;
-        const int bands = (H + BM_ROWS - 1) / BM_ROWS;
-        const bool all = nb * nw > 64;             // (tiny planes: no early out)
-        float v = 0.f;
-        if (tid < nb * nw) v = bandmax[((size_t)plane * bands + b0 + tid / nw) * words + w0 + tid % nw];
-        float mx = all ? 1e30f : v;
-        for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-        if (tid == 0 && (double)mx >= thre * (1.0 - 1e-9)) s_live = 1;
-      }
-      __syncthreads();
-      if (!s_live) {
-        for (int it = wave; it < NMS_TY * 3; it += 4) {
-          const int y = y0 + it / 3, wi = bx * 3 + it % 3;
-          if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = 0ull;
-        }
-        return;
-      }
-      __syncthreads();   // everyone has read s_live before the exact bound below resets it
-      if (tid == 0) s_live = 0;
-      __syncthreads();
-    }
-  }
-  // axis 0 (NI_Correlate1D, symmetric): o = c*w0; for j = 12..1: o += (a[-j] + a[+j]) * w[j]
-  double in[NMS_IR];
-  if constexpr (!FUSED) {
-    const T* src = planes + (size_t)plane * H * W;
-    if (tid < NMS_VC) {
-      const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
-      double amax = 0.0;
-#pragma unroll
-      for (int r = 0; r < NMS_IR; ++r) {
-        in[r] = (double)src[(size_t)reflect_idx(y0 - 1 - NMS_R + r, H) * W + xx];
-        amax = fmax(amax, fabs(in[r]));
-      }
-      s_cmax[tid] = amax;
-      // Early out, exact: every g of the tile is a positive-weight average (weights sum
-      // to 1) of these inputs, so |g| <= max|in| * (1 + 1e-13) in fp64.  When that stays
-      // below the threshold no pixel can pass `g > thre` and the tile's mask is zero.
-      if (amax >= thre * (1.0 - 1e-9)) s_live = 1;
-    }
-    __syncthreads();
-  } else {
-    const int f = plane / nch, c = plane - f * nch;
-    const float* b = m.base + (size_t)f * m.fs + chan_off(m, c);
-    int sr0, nsr, sc0, nsc;
-    fused_window(m, H, W, y0, x0, &sr0, &nsr, &sc0, &nsc);
-    if (nsr > WR) __builtin_trap();   // the host picks a window that holds the tile's source rows
-    // the low-res window is staged in LDS: one coalesced pass, reused by the resize
-    if (nsc > WC) __builtin_trap();
-    float amax = 0.f;
-    for (int i = tid; i < nsr * nsc; i += 256) {
-      const int r = i / nsc, cc = i - r * nsc;
-      const float v = b[(size_t)(sr0 + r) * m.ys + (size_t)(sc0 + cc) * m.xs];
-      s_low[r][cc] = v;
-      amax = fmaxf(amax, fabsf(v));
-    }
-    if ((double)amax * 1.9 >= thre * (1.0 - 1e-9)) s_live = 1;
-    __syncthreads();
-    const bool s_live_lr = s_live != 0;
-    __syncthreads();   // everyone has read s_live before it is reused for the second bound
-    if (s_live_lr) {
-      if (tid < NMS_VC) {
-        // horizontal cubic pass for the window column (OpenCV HResizeCubic order)
-        const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
-        int xi[4];
-        float a[4];
-        taps(xx, m.scx, m.sw, xi, a);
-        const int i0 = xi[0] - sc0, i1 = xi[1] - sc0, i2 = xi[2] - sc0, i3 = xi[3] - sc0;
-        for (int r = 0; r < nsr; ++r) {
-          const float* row = s_low[r];
-          s_hz[r][tid] = ((row[i0] * a[0] + row[i1] * a[1]) + row[i2] * a[2]) + row[i3] * a[3];
-        }
-      } else {
-        // vertical taps of the window's 42 rows, once per block (the 38 idle lanes)
-        for (int r = tid - NMS_VC; r < NMS_IR; r += 256 - NMS_VC) {
-          int yi[4];
-          float be[4];
-          taps(reflect_idx(y0 - 1 - NMS_R + r, H), m.scy, m.sh, yi, be);
-          s_ti[r] = make_int4(yi[0] - sr0, yi[1] - sr0, yi[2] - sr0, yi[3] - sr0);
-          s_tb[r] = make_float4(be[0], be[1], be[2], be[3]);
-        }
-      }
-      if (tid == 0) s_live = 0;
-    }
-    __syncthreads();
-    if (s_live_lr && tid < NMS_VC) {
-      const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
-      const int rowlen = m.dw * m.cn;
-      const bool simd = xx * m.cn + c < rowlen - rowlen % 4;
-      double vmax = 0.0;
-#pragma unroll
-      for (int r = 0; r < NMS_IR; ++r) {
-        const int4 yi = s_ti[r];
-        const float4 be = s_tb[r];
-        const float h0 = s_hz[yi.x][tid], h1 = s_hz[yi.y][tid], h2 = s_hz[yi.z][tid], h3 = s_hz[yi.w][tid];
-        const float v = simd ? h0 * be.x + (h1 * be.y + (h2 * be.z + h3 * be.w))   // VResizeCubicVec_32f
-                             : ((h0 * be.x + h1 * be.y) + h2 * be.z) + h3 * be.w;
-        in[r] = (double)v;
-        vmax = fmax(vmax, fabs(in[r]));
-      }
-      s_cmax[tid] = vmax;
-      if (vmax >= thre * (1.0 - 1e-9)) s_live = 1;   // the exact blur bound, as unfused
-    }
-    __syncthreads();
-  }
-  if (!s_live) {
+  auto zero_masks = [&]() {
     for (int it = wave; it < NMS_TY * 3; it += 4) {
       const int y = y0 + it / 3, wi = bx * 3 + it % 3;
       if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = 0ull;
     }
+  };
+  if constexpr (!FUSED) {
+    if (bandmax && band_dead(bandmax, plane, H, W, words, y0, x0, thre, &s_live)) {
+      zero_masks();
+      return;
+    }
+  } else {
+    if (!fused_prologue<WR, WC>(m, nch, plane, H, W, y0, x0, thre, s_low, s_hz, s_ti, s_tb, &s_live)) {
+      zero_masks();
+      return;
+    }
+  }
+  if (tid == 0) s_live = 0;
+  __syncthreads();
+  // axis 0 (NI_Correlate1D, symmetric): o = c*w0; for j = 12..1: o += (a[-j] + a[+j]) * w[j]
+  double in[NMS_IR];
+  if (tid < NMS_VC) {
+    const int xx = reflect_idx(x0 - 1 - NMS_R + tid, W);
+    double amax = 0.0;
+#pragma unroll
+    for (int r = 0; r < NMS_IR; ++r) {
+      if constexpr (!FUSED)
+        in[r] = (double)planes[(size_t)plane * H * W + (size_t)reflect_idx(y0 - 1 - NMS_R + r, H) * W + xx];
+      else
+        in[r] = (double)fused_value(m, plane % nch, s_hz, s_ti, s_tb, r, tid, xx);
+      amax = fmax(amax, fabs(in[r]));
+    }
+    s_cmax[tid] = amax;
+    // Early out, exact: every g of the tile is a positive-weight average (weights sum
+    // to 1) of these inputs, so |g| <= max|in| * (1 + 1e-13) in fp64.  When that stays
+    // below the threshold no pixel can pass `g > thre` and the tile's mask is zero.
+    if (amax >= thre * (1.0 - 1e-9)) s_live = 1;
+  }
+  __syncthreads();
+  if (!s_live) {
+    zero_masks();
     return;
   }
   // Word liveness, the same exact bound per 64-column mask word: word w's outputs (tile
@@ -598,26 +663,300 @@ __device__ __forceinline__ void blur_tile(const T* __restrict__ planes, int H, i
     const int wi = bx * 3 + wd;
     if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = word;
   }
+  TPROF(9, clock64());
 }
 
+// the fp32 filter of one tile; undecided tiles are appended to amb (see above)
 template <typename T, bool FUSED, int WR = NMS_SRC_ROWS, int WC = NMS_SRC_COLS>
-__global__ void __launch_bounds__(256) blur_nms_kernel(const T* __restrict__ planes, int H, int W, int words,
-                                                        unsigned long long* __restrict__ mask, double thre,
-                                                        int mode_hand, MapSrc m, int nch, const int* __restrict__ live,
-                                                        const int* __restrict__ live_count, int tiles_x, int tiles_y,
-                                                        const float* __restrict__ bandmax = nullptr) {
+__device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, int H, int W, int words,
+                                                 unsigned long long* __restrict__ mask, double thre, int mode_hand,
+                                                 const MapSrc& m, int nch, int plane, int by, int bx,
+                                                 const float* __restrict__ bandmax, int* __restrict__ amb,
+                                                 int* __restrict__ amb_count, int tile_id, int margin_mode) {
+  // v, then g in place (15.7 KB); fused: over the low-res window, which only the prologue's
+  // horizontal pass reads
+  constexpr int U = NMS_VR * NMS_VC > (FUSED ? WR * WC : 1) ? NMS_VR * NMS_VC : WR * WC;
+  __shared__ float s_u[U];
+  float(*s_vf)[NMS_VC] = reinterpret_cast<float(*)[NMS_VC]>(s_u);
+  float(*s_low)[WC] = reinterpret_cast<float(*)[WC]>(s_u);
+  __shared__ float s_hz[FUSED ? WR : 1][NMS_VC];
+  __shared__ int4 s_ti[FUSED ? NMS_IR : 1];
+  __shared__ float4 s_tb[FUSED ? NMS_IR : 1];
+  __shared__ long long s_roff[FUSED ? 1 : NMS_IR];   // plane offsets of the window's rows
+  __shared__ double s_cmax[2][NMS_VC];          // max |in| of every window column, per row half
+  __shared__ double s_M;                        // max |in| over the window (the margin)
+  __shared__ int s_live, s_amb;
+  __shared__ int s_wlive[3];
+  const int y0 = by * NMS_TY, x0 = bx * NMS_TX;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  TPROF(0, wall_clock64());
+  TPROF(2, clock64());
+  auto zero_masks = [&]() {
+    for (int it = wave; it < NMS_TY * 3; it += 4) {
+      const int y = y0 + it / 3, wi = bx * 3 + it % 3;
+      if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = 0ull;
+    }
+    TPROF(1, wall_clock64());
+  };
   if constexpr (!FUSED) {
-    blur_tile<T, false>(planes, H, W, words, mask, thre, mode_hand, m, nch, blockIdx.z, blockIdx.y, blockIdx.x, bandmax);
+    if (bandmax && band_dead(bandmax, plane, H, W, words, y0, x0, thre, &s_live)) {
+      zero_masks();
+      return;
+    }
+    if (tid < NMS_IR) s_roff[tid] = (long long)reflect_idx(y0 - 1 - NMS_R + tid, H) * W;
   } else {
-    // grid-stride over the live tiles found by tile_live_kernel (mask pre-zeroed)
+    if (!fused_prologue<WR, WC>(m, nch, plane, H, W, y0, x0, thre, s_low, s_hz, s_ti, s_tb, &s_live)) {
+      zero_masks();
+      return;
+    }
+  }
+  if (tid == 0) {
+    s_live = 0;
+    s_amb = 0;
+  }
+  __syncthreads();
+  TPROF(3, clock64());
+  // the window: column pair cp (window columns 2cp, 2cp+1) of rows vh*9 .. vh*9+32 (v rows
+  // vh*9 .. vh*9+8) per thread, waves 0-1 the first half, 2-3 the second
+  const int cp = tid & 127, vh = tid >> 7;
+  const bool vth = cp < NMS_CP;
+  f2v a[NMS_VH + 2 * NMS_R];
+  if (vth) {
+    const int xa = reflect_idx(x0 - 1 - NMS_R + 2 * cp, W), xb = reflect_idx(x0 - NMS_R + 2 * cp, W);
+    const T* src = planes + (size_t)plane * H * W;
+    double ma = 0.0, mb = 0.0;
+#pragma unroll
+    for (int k = 0; k < NMS_VH + 2 * NMS_R; ++k) {
+      const int r = vh * NMS_VH + k;
+      T va, vb;
+      if constexpr (!FUSED) {
+        const long long ro = s_roff[r];
+        va = src[ro + xa];
+        vb = src[ro + xb];
+      } else {
+        va = fused_value(m, plane % nch, s_hz, s_ti, s_tb, r, 2 * cp, xa);
+        vb = fused_value(m, plane % nch, s_hz, s_ti, s_tb, r, 2 * cp + 1, xb);
+      }
+      a[k] = f2v{(float)va, (float)vb};
+      ma = fmax(ma, fabs((double)va));
+      mb = fmax(mb, fabs((double)vb));
+      // fp64 planes: at most 11 rows' loads in flight (all 33 pairs of doubles hoisted spill)
+      if constexpr (sizeof(T) == 8)
+        if (k % 11 == 10) __builtin_amdgcn_sched_barrier(0);
+    }
+    s_cmax[vh][2 * cp] = ma;
+    s_cmax[vh][2 * cp + 1] = mb;
+    // the exact early out (blur_tile_exact): |g| <= max|in| * (1 + 1e-13)
+    if (fmax(ma, mb) >= thre * (1.0 - 1e-9)) s_live = 1;
+  }
+  __syncthreads();
+  if (!s_live) {
+    zero_masks();
+    return;
+  }
+  TPROF(4, clock64());
+  // word liveness (blur_tile_exact's bound per mask word) and M, in wave 0
+  if (tid < 64) {
+    auto cm = [&](int t) { return fmax(s_cmax[0][t], s_cmax[1][t]); };
+    const double ca = cm(tid), cb = cm(64 + tid), cc = cm(128 + tid);
+    const double cd = tid < NMS_VC - 192 ? cm(192 + tid) : 0.0;
+    double m0 = fmax(ca, tid <= 25 ? cb : 0.0);   // window columns 0..89
+    double m1 = fmax(cb, tid <= 25 ? cc : 0.0);   // 64..153
+    double m2 = fmax(cc, cd);                     // 128..217
+    for (int o = 32; o > 0; o >>= 1) {
+      m0 = fmax(m0, __shfl_xor(m0, o));
+      m1 = fmax(m1, __shfl_xor(m1, o));
+      m2 = fmax(m2, __shfl_xor(m2, o));
+    }
+    if (tid == 0) {
+      s_wlive[0] = m0 >= thre * (1.0 - 1e-9);
+      s_wlive[1] = m1 >= thre * (1.0 - 1e-9);
+      s_wlive[2] = m2 >= thre * (1.0 - 1e-9);
+      s_M = fmax(m0, fmax(m1, m2));
+    }
+  }
+  __syncthreads();
+  const bool wl0 = s_wlive[0], wl1 = s_wlive[1], wl2 = s_wlive[2];
+  auto col_needed = [&](int t) {
+    return (wl0 && t <= 89) || (wl1 && t >= 64 && t <= 153) || (wl2 && t >= 128);
+  };
+  if (vth && (col_needed(2 * cp) || col_needed(2 * cp + 1))) {
+#pragma unroll
+    for (int r = 0; r < NMS_VH; ++r) {
+      f2v o = a[r + NMS_R] * kGaussF[0];
+#pragma unroll
+      for (int j = NMS_R; j >= 1; --j)
+        o = __builtin_elementwise_fma(a[r + NMS_R - j] + a[r + NMS_R + j], f2v{kGaussF[j], kGaussF[j]}, o);
+      *reinterpret_cast<f2v*>(&s_vf[vh * NMS_VH + r][2 * cp]) = o;
+    }
+  }
+  __syncthreads();
+  TPROF(5, clock64());
+  // horizontal: rows 2p, 2p+1 of g columns c0 .. c0+6 (v columns c0 .. c0+30); g columns
+  // c0..c0+6 overlap a live word's g range [64w, 64w+65] (the run's other columns may read v
+  // never computed -- their g is never read)
+  {
+    const int p = tid / NMS_HRUNS, c0 = (tid - p * NMS_HRUNS) * NMS_HSEG, c1 = c0 + NMS_HSEG - 1;
+    const bool act = tid < NMS_VR / 2 * NMS_HRUNS &&
+                     ((wl0 && c0 <= 65) || (wl1 && c1 >= 64 && c0 <= 129) || (wl2 && c1 >= 128));
+    f2v v[NMS_HSEG + 2 * NMS_R];
+    if (act) {
+#pragma unroll
+      for (int k = 0; k < NMS_HSEG + 2 * NMS_R; ++k)
+        v[k] = c0 + k < NMS_VC ? f2v{s_vf[2 * p][c0 + k], s_vf[2 * p + 1][c0 + k]} : f2v{0.f, 0.f};
+    }
+    __syncthreads();   // every v run is in registers: g may overwrite the tile
+    if (act) {
+#pragma unroll
+      for (int k = 0; k < NMS_HSEG; ++k) {
+        f2v o = v[k + NMS_R] * kGaussF[0];
+#pragma unroll
+        for (int j = NMS_R; j >= 1; --j)
+          o = __builtin_elementwise_fma(v[k + NMS_R - j] + v[k + NMS_R + j], f2v{kGaussF[j], kGaussF[j]}, o);
+        if (c0 + k < NMS_GC) {
+          s_vf[2 * p][c0 + k] = o.x;
+          s_vf[2 * p + 1][c0 + k] = o.y;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  TPROF(6, clock64());
+  // (margin_mode 2: a margin of M / 4, the re-run of nearly every live tile -- tests)
+  const double eps = s_M * (margin_mode == 2 ? 0.25 : BLUR_EPS_REL) + 1e-30, e2 = 2.0 * eps;
+  for (int it = wave; it < NMS_TY * 3; it += 4) {
+    const int ty = it / 3, wd = it - ty * 3;
+    const int y = y0 + ty, cx = wd * 64 + lane, x = x0 + cx;
+    bool pk = false, open = false;
+    if (y < H && x < W && s_wlive[wd]) {
+      const int R = ty + 1;
+      const double g = s_vf[R][cx + 1];
+      bool no = g + eps <= thre;                 // surely g <= thre
+      open = !no && !(g - eps > thre);           // g vs thre inside the margin
+      if (!mode_hand) {
+        // per neighbour q: surely g < q (the pixel is out), or g vs q inside the margin
+        const double d0 = g - (y > 0 ? (double)s_vf[R - 1][cx + 1] : 0.0);
+        const double d1 = g - (y + 1 < H ? (double)s_vf[R + 1][cx + 1] : 0.0);
+        const double d2 = g - (x > 0 ? (double)s_vf[R][cx] : 0.0);
+        const double d3 = g - (x + 1 < W ? (double)s_vf[R][cx + 2] : 0.0);
+        no = no || d0 < -e2 || d1 < -e2 || d2 < -e2 || d3 < -e2;
+        open = open || !(d0 >= e2) || !(d1 >= e2) || !(d2 >= e2) || !(d3 >= e2);
+      }
+      pk = !no && !open;
+      open = !no && open;
+    }
+    const unsigned long long word = __ballot(pk);
+    const unsigned long long am = __ballot(open);
+    const int wi = bx * 3 + wd;
+    if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = word;
+    if (lane == 0 && am) s_amb = 1;
+  }
+  __syncthreads();
+  TPROF(7, clock64());
+  TPROF(1, wall_clock64());
+  if (tid == 0 && s_amb) {
+    amb[atomicAdd(amb_count, 1)] = tile_id;   // the exact passes re-run the whole tile
+    TPROF(8, 1);
+  }
+}
+
+// One tile per block (live == nullptr: the grid is tiles_x x tiles_y x planes), or a
+// grid-stride loop over a list of tiles (tile_live_kernel / band_live_kernel / the filter's
+// undecided tiles; the mask pre-zeroed where a list skips tiles).  EXACT: the fp64 passes;
+// else the fp32 filter, appending undecided tiles to amb.
+// (4 waves per SIMD: the register allocation is held to that occupancy, 128 VGPRs; the
+// filter on fp64 planes -- the multi-scale and hand averages -- 3 waves, 168 VGPRs, unspilled)
+template <typename T, bool FUSED, bool EXACT, int WR = NMS_SRC_ROWS, int WC = NMS_SRC_COLS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 && !EXACT ? 3 : 4)))
+    blur_nms_kernel(const T* __restrict__ planes, int H, int W, int words, unsigned long long* __restrict__ mask,
+                    double thre, int mode_hand, MapSrc m, int nch, const int* __restrict__ live,
+                    const int* __restrict__ live_count, int tiles_x, int tiles_y, const float* __restrict__ bandmax,
+                    int* __restrict__ amb, int* __restrict__ amb_count, int margin_mode) {
+  auto run = [&](int plane, int by, int bx) {
+    if constexpr (EXACT)
+      blur_tile_exact<T, FUSED, WR, WC>(planes, H, W, words, mask, thre, mode_hand, m, nch, plane, by, bx, bandmax);
+    else
+      blur_tile_filter<T, FUSED, WR, WC>(planes, H, W, words, mask, thre, mode_hand, m, nch, plane, by, bx, bandmax,
+                                         amb, amb_count, (plane * tiles_y + by) * tiles_x + bx, margin_mode);
+  };
+  if (!live) {
+    run(blockIdx.z, blockIdx.y, blockIdx.x);
+  } else {
     const int cnt = *live_count;
     for (int k = blockIdx.x; k < cnt; k += gridDim.x) {
       const int t = live[k];
       const int bx = t % tiles_x, r = t / tiles_x, by = r % tiles_y, plane = r / tiles_y;
-      blur_tile<T, true, WR, WC>(planes, H, W, words, mask, thre, mode_hand, m, nch, plane, by, bx, nullptr);
+      run(plane, by, bx);
       __syncthreads();   // LDS reuse by the next tile
     }
   }
+}
+
+// ISLPOSE_BLUR_EXACT=1: every live tile on the fp64 passes, without the fp32 filter; =2: the
+// filter with a margin so wide that nearly every live tile falls back (A/B and the filter's
+// tests: the same mask bits either way; per call)
+static int blur_exact_only() {
+  const char* e = getenv("ISLPOSE_BLUR_EXACT");
+  return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
+}
+
+// The blur of one post: the filter launch, then the exact passes over the tiles it could
+// not decide (a grid-stride launch over its list; ISLPOSE_BLUR_EXACT=1: the exact passes
+// over every tile instead).  `grid` / `live`: one tile per block or a live list (as
+// blur_nms_kernel); amb: n_tiles + 1 ints of scratch.
+template <typename T, bool FUSED, int WR = NMS_SRC_ROWS, int WC = NMS_SRC_COLS>
+static int launch_blur(dim3 grid, hipStream_t s, const T* planes, int H, int W, int words, unsigned long long* mask,
+                       double thre, int mode_hand, const MapSrc& m, int nch, const int* live, const int* live_count,
+                       int tiles_x, int tiles_y, const float* bandmax, int* amb) {
+  const int ex = blur_exact_only();
+  if (ex == 1) {
+    hipLaunchKernelGGL((blur_nms_kernel<T, FUSED, true, WR, WC>), grid, dim3(256), 0, s, planes, H, W, words, mask,
+                       thre, mode_hand, m, nch, live, live_count, tiles_x, tiles_y, bandmax, nullptr, nullptr, 0);
+    return hipGetLastError() == hipSuccess ? ISL_OK : ISL_E_HIP;
+  }
+  int* amb_count = amb;
+  if (hipMemsetAsync(amb_count, 0, sizeof(int), s) != hipSuccess) return ISL_E_HIP;
+  hipLaunchKernelGGL((blur_nms_kernel<T, FUSED, false, WR, WC>), grid, dim3(256), 0, s, planes, H, W, words, mask,
+                     thre, mode_hand, m, nch, live, live_count, tiles_x, tiles_y, bandmax, amb + 1, amb_count, ex);
+  if (hipGetLastError() != hipSuccess) return ISL_E_HIP;
+  hipLaunchKernelGGL((blur_nms_kernel<T, FUSED, true, WR, WC>), dim3(256), dim3(256), 0, s, planes, H, W, words, mask,
+                     thre, mode_hand, m, nch, (const int*)(amb + 1), (const int*)amb_count, tiles_x, tiles_y,
+                     (const float*)nullptr, nullptr, nullptr, 0);
+  return hipGetLastError() == hipSuccess ? ISL_OK : ISL_E_HIP;
+}
+
+// The band-maxima bound of the materialised single-scale path, one tile per thread: the
+// tile's window, reflected, against resize_sep_kernel's band x word maxima (blur_tile's own
+// early out, before any block is launched for the tile); live tiles are appended to `live`
+// (one atomic per wave).  The blur then runs over the live tiles only (mask pre-zeroed).
+__global__ void __launch_bounds__(256) band_live_kernel(const float* __restrict__ bandmax, int H, int W, int words,
+                                                        int tiles_x, int tiles_y, int n_tiles, double thre,
+                                                        int* __restrict__ live, int* __restrict__ live_count) {
+  const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63;
+  int lv = 0;
+  if (t < n_tiles) {
+    const int bx = t % tiles_x, r = t / tiles_x, by = r % tiles_y, plane = r / tiles_y;
+    const int y0 = by * NMS_TY, x0 = bx * NMS_TX;
+    int rlo, rhi, clo, chi;
+    reflect_range(y0 - 1 - NMS_R, y0 - 2 - NMS_R + NMS_IR, H, &rlo, &rhi);
+    reflect_range(x0 - 1 - NMS_R, x0 - 2 - NMS_R + NMS_VC, W, &clo, &chi);
+    const int b0 = rlo / BM_ROWS, nb = rhi / BM_ROWS - b0 + 1, w0 = clo / 64, nw = chi / 64 - w0 + 1;
+    const int bands = (H + BM_ROWS - 1) / BM_ROWS;
+    if (nb * nw > 64) {
+      lv = 1;                                   // (tiny planes: no early out, as blur_tile)
+    } else {
+      float mx = 0.f;
+      for (int i = 0; i < nb; ++i)
+        for (int j = 0; j < nw; ++j) mx = fmaxf(mx, bandmax[((size_t)plane * bands + b0 + i) * words + w0 + j]);
+      lv = (double)mx >= thre * (1.0 - 1e-9);
+    }
+  }
+  const unsigned long long bal = __ballot(lv);
+  int base = 0;
+  if (lane == 0 && bal) base = atomicAdd(live_count, (int)__popcll(bal));
+  base = __shfl(base, 0);
+  if (lv) live[base + __popcll(bal & ((1ull << lane) - 1))] = t;
 }
 
 // The low-res bound of the fused path for TL_TILES consecutive blur tiles per block
@@ -743,6 +1082,8 @@ static_assert(sizeof(MapSrcN::m) / sizeof(MapSrc) == MAX_SCALES, "resize_acc_ker
 
 struct GroupArgs {
   MapSrc paf[MAX_SCALES];   // final-resolution PAF of each scale (sampled on demand)
+  MapSrc paf1[MAX_SCALES];  // nested scales: the stage-1 resize that paf[s] reads, never materialised
+  int paf_nested[MAX_SCALES];
   int nscales;
   float div_f;              // len(multiplier), as float32
   int H, W;                 // frame size
@@ -757,15 +1098,76 @@ struct GroupArgs {
   unsigned char* used;      // [n][2][max_peaks]
 };
 
+// One element of the two-stage resize m2(m1(low)) (body.py:68-73 then :74-76 on a frame whose
+// net input is not the frame) without the stage-1 planes: the 4 x 4 stage-1 values the
+// stage-2 taps read, each exactly as resize_sep_kernel computes it (sample()'s order), with
+// the stage-1 horizontal combinations of the <= 5 low-resolution rows they span shared.
+__device__ float sample_nested(const MapSrc& m2, const MapSrc& m1, int f, int c, int y, int x) {
+  int xi[4], yi[4];
+  float a[4], be[4];
+  taps(x, m2.scx, m2.sw, xi, a);
+  taps(y, m2.scy, m2.sh, yi, be);
+  const float* b = m1.base + (size_t)f * m1.fs + chan_off(m1, c);
+  int lxi[4][4], lyi[4][4];
+  float la[4][4], lbe[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    taps(xi[k], m1.scx, m1.sw, lxi[k], la[k]);
+    taps(yi[k], m1.scy, m1.sh, lyi[k], lbe[k]);
+  }
+  const int r0 = lyi[0][0];   // taps are monotone in the index: rows r0 .. lyi[3][3]
+  const int rowlen1 = m1.dw * m1.cn;
+  float s1[4][4];
+  if (lyi[3][3] - r0 < 5) {
+    float h1[5][4];
+#pragma unroll
+    for (int r = 0; r < 5; ++r) {
+      const float* row = b + (size_t)min(r0 + r, lyi[3][3]) * m1.ys;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        h1[r][k] = ((row[lxi[k][0] * m1.xs] * la[k][0] + row[lxi[k][1] * m1.xs] * la[k][1]) +
+                    row[lxi[k][2] * m1.xs] * la[k][2]) + row[lxi[k][3] * m1.xs] * la[k][3];
+    }
+#pragma unroll
+    for (int ky = 0; ky < 4; ++ky) {
+#pragma unroll
+      for (int kx = 0; kx < 4; ++kx) {
+        float h[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int r = lyi[ky][t] - r0;   // 0..4: a select chain, no private array
+          h[t] = r == 0 ? h1[0][kx] : r == 1 ? h1[1][kx] : r == 2 ? h1[2][kx] : r == 3 ? h1[3][kx] : h1[4][kx];
+        }
+        const float* bb = lbe[ky];
+        s1[ky][kx] = xi[kx] * m1.cn + c < rowlen1 - rowlen1 % 4
+                         ? h[0] * bb[0] + (h[1] * bb[1] + (h[2] * bb[2] + h[3] * bb[3]))
+                         : ((h[0] * bb[0] + h[1] * bb[1]) + h[2] * bb[2]) + h[3] * bb[3];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int ky = 0; ky < 4; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 4; ++kx) s1[ky][kx] = sample_row(m1, f, c, lyi[ky], lbe[ky], xi[kx]);
+  }
+  float hz[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hz[k] = ((s1[k][0] * a[0] + s1[k][1] * a[1]) + s1[k][2] * a[2]) + s1[k][3] * a[3];
+  const int rowlen = m2.dw * m2.cn;
+  if (x * m2.cn + c < rowlen - rowlen % 4) return hz[0] * be[0] + (hz[1] * be[1] + (hz[2] * be[2] + hz[3] * be[3]));
+  return ((hz[0] * be[0] + hz[1] * be[1]) + hz[2] * be[2]) + hz[3] * be[3];
+}
+
 __device__ __forceinline__ double paf_value(const GroupArgs& a, int f, int c, int y, int x) {
   double acc = 0.0;
   for (int s = 0; s < a.nscales; ++s) {
-    const float v = sample(a.paf[s], f, c, y, x);
+    const float v = a.paf_nested[s] ? sample_nested(a.paf[s], a.paf1[s], f, c, y, x) : sample(a.paf[s], f, c, y, x);
     acc = acc + (double)(v / a.div_f);   // paf_avg += + paf / len(multiplier)
   }
   return acc;
 }
 
+constexpr int LIMB_ITEMS = 2048;   // (pair, point) items scored in parallel (16 KB of LDS)
 // One workgroup per (limb, frame): score every (A, B) pair (body.py:142-164),
 // stable descending sort by rank counting, greedy matching (body.py:166-175).
 __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
@@ -809,29 +1211,67 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
   }
   const double* pA = peaks + (size_t)A * a.max_peaks * 3;
   const double* pB = peaks + (size_t)B * a.max_peaks * 3;
-  for (int p = tid; p < np; p += 256) {
+  // pair p's direction, norm and sample point I (np.linspace, int(round(.)): half to even)
+  auto point = [&](int p, int I, double* ux, double* uy, double* norm, int* xi, int* yi) {
     const int i = p / nB, j = p - i * nB;
     const long long ax = (long long)pA[i * 3], ay = (long long)pA[i * 3 + 1];
     const long long bx = (long long)pB[j * 3], by = (long long)pB[j * 3 + 1];
     const long long vx = bx - ax, vy = by - ay;
-    double norm = sqrt((double)(vx * vx + vy * vy));     // math.sqrt of an exact integer
-    norm = 0.001 < norm ? norm : 0.001;                   // max(0.001, norm)
-    const double ux = (double)vx / norm, uy = (double)vy / norm;
+    double nr = sqrt((double)(vx * vx + vy * vy));       // math.sqrt of an exact integer
+    nr = 0.001 < nr ? nr : 0.001;                         // max(0.001, norm)
+    *norm = nr;
+    *ux = (double)vx / nr;
+    *uy = (double)vy / nr;
     const double stx = ((double)bx - (double)ax) / 9.0, sty = ((double)by - (double)ay) / 9.0;
-    double sum = 0.0;
-    int cnt = 0;
-    for (int I = 0; I < 10; ++I) {
-      const double sx = I == 9 ? (double)bx : (double)I * stx + (double)ax;   // np.linspace
-      const double sy = I == 9 ? (double)by : (double)I * sty + (double)ay;
-      const int xi = (int)rint(sx), yi = (int)rint(sy);                      // round half to even
-      const double s = paf_value(a, f, mx, yi, xi) * ux + paf_value(a, f, my, yi, xi) * uy;
-      sum = sum + s;                                                          // builtin sum(), left to right
-      cnt += s > 0.05;
-    }
+    const double sx = I == 9 ? (double)bx : (double)I * stx + (double)ax;
+    const double sy = I == 9 ? (double)by : (double)I * sty + (double)ay;
+    *xi = (int)rint(sx);
+    *yi = (int)rint(sy);
+  };
+  auto score_of = [&](int p, double sum, int cnt, double norm) {
     const double prior = 0.5 * (double)a.H / norm - 1.0;
     const double score = sum / 10.0 + (0.0 < prior ? 0.0 : prior);
     pscore[p] = score;
     pkeep[p] = (cnt > 8 && score > 0.0) ? 1 : 0;
+  };
+  if (np * 10 <= LIMB_ITEMS) {
+    // every (pair, point) in parallel (the nested two-stage samples are ~80 loads each), then
+    // each pair's sum in point order
+    __shared__ double s_item[LIMB_ITEMS];
+    for (int it = tid; it < np * 10; it += 256) {
+      double ux, uy, nr;
+      int xi, yi;
+      point(it / 10, it % 10, &ux, &uy, &nr, &xi, &yi);
+      s_item[it] = paf_value(a, f, mx, yi, xi) * ux + paf_value(a, f, my, yi, xi) * uy;
+    }
+    __syncthreads();
+    for (int p = tid; p < np; p += 256) {
+      double sum = 0.0;
+      int cnt = 0;
+      for (int I = 0; I < 10; ++I) {
+        const double s = s_item[p * 10 + I];
+        sum = sum + s;                                                        // builtin sum(), left to right
+        cnt += s > 0.05;
+      }
+      double ux, uy, nr;
+      int xi, yi;
+      point(p, 0, &ux, &uy, &nr, &xi, &yi);
+      score_of(p, sum, cnt, nr);
+    }
+  } else {
+    for (int p = tid; p < np; p += 256) {
+      double sum = 0.0, nr = 0.0;
+      int cnt = 0;
+      for (int I = 0; I < 10; ++I) {
+        double ux, uy;
+        int xi, yi;
+        point(p, I, &ux, &uy, &nr, &xi, &yi);
+        const double s = paf_value(a, f, mx, yi, xi) * ux + paf_value(a, f, my, yi, xi) * uy;
+        sum = sum + s;                                                        // builtin sum(), left to right
+        cnt += s > 0.05;
+      }
+      score_of(p, sum, cnt, nr);
+    }
   }
   for (int i = tid; i < nA; i += 256) usedA[i] = 0;
   for (int j = tid; j < nB; j += 256) usedB[j] = 0;
@@ -2100,6 +2540,34 @@ static int low_src(isl_net* net, const float* p, int which, int n, int C, int h8
   return ISL_OK;
 }
 
+#ifdef ISLPOSE_DEV
+// ISLPOSE_TILE_PROF=1 (development build): the next blur launches stamp their tiles into a
+// device buffer of `tiles` x 10 u64 (zeroed here); isl_dev_tile_prof copies it out
+static unsigned long long* g_prof_buf = nullptr;
+static size_t g_prof_tiles = 0;
+static void tile_prof_arm(size_t tiles, hipStream_t s) {
+  const char* e = getenv("ISLPOSE_TILE_PROF");
+  unsigned long long* p = nullptr;
+  if (e && e[0] == '1') {
+    if (tiles > g_prof_tiles) {
+      if (g_prof_buf) (void)hipFree(g_prof_buf);
+      g_prof_buf = nullptr;
+      if (hipMalloc(&g_prof_buf, tiles * 10 * 8) != hipSuccess) g_prof_buf = nullptr;
+      g_prof_tiles = g_prof_buf ? tiles : 0;
+    }
+    if (g_prof_buf) (void)hipMemsetAsync(g_prof_buf, 0, tiles * 10 * 8, s);
+    p = g_prof_buf;
+  }
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tile_prof), &p, sizeof(p), 0, hipMemcpyHostToDevice, s);
+}
+extern "C" int isl_dev_tile_prof(void* host, size_t tiles) {
+  if (!g_prof_buf || tiles > g_prof_tiles) return ISL_E_ARG;
+  return hipMemcpy(host, g_prof_buf, tiles * 10 * 8, hipMemcpyDeviceToHost) == hipSuccess ? ISL_OK : ISL_E_HIP;
+}
+#else
+static void tile_prof_arm(size_t, hipStream_t) {}
+#endif
+
 extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, const isl_scale_geom* geom,
                              const float* const* d_paf, const float* const* d_heat, const isl_caps* caps,
                              void* d_result, void* stream) {
@@ -2135,22 +2603,27 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   size_t mid_bytes = 0;
   for (int si = 0; si < nscales; ++si) {
     const isl_scale_geom& g = geom[si];
-    if (!(g.valid_h == H && g.valid_w == W)) mid_bytes += (size_t)n * g.valid_h * g.valid_w * (nparts + npaf) * 4;
+    if (!(g.valid_h == H && g.valid_w == W)) mid_bytes += (size_t)n * g.valid_h * g.valid_w * nparts * 4;
   }
   const int words = (W + 63) / 64;
   const size_t mask_bytes = (size_t)n * nparts * H * words * 8;
   const size_t pair_bytes = (size_t)n * nlimbs * caps->max_pairs * (8 + 4 + 4);
   const size_t used_bytes = (size_t)n * nlimbs * 2 * caps->max_peaks;
   const size_t n_tiles_all = (size_t)((W + NMS_TX - 1) / NMS_TX) * ((H + NMS_TY - 1) / NMS_TY) * n * nparts;
-  const size_t live_bytes = fused ? (n_tiles_all + 1) * sizeof(int) : 0;
+  // ISLPOSE_BLUR_LIST=0: the band-maxima early out inside every tile's block instead of a live
+  // list (A/B; per call)
+  const char* ble = getenv("ISLPOSE_BLUR_LIST");
+  const bool band_list = !(ble && ble[0] == '0');
   // single scale, materialised planes: the band maxima of the final resize (blur early out)
   // (ISLPOSE_BLUR_BANDS=0: without, A/B; read per call)
   const char* bme = getenv("ISLPOSE_BLUR_BANDS");
   const bool bands_on = !(bme && bme[0] == '0');
   const size_t bm_bytes = (!fused && !multi && bands_on) ? (size_t)n * nparts * ((H + BM_ROWS - 1) / BM_ROWS) * words * 4 : 0;
+  const size_t live_bytes = (fused || (bm_bytes && band_list)) ? (n_tiles_all + 1) * sizeof(int) : 0;
+  const size_t amb_bytes = (n_tiles_all + 1) * sizeof(int);   // the filter's undecided tiles
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t total = up(heat_bytes) + up(mid_bytes) + up(mask_bytes) + up(pair_bytes) + up(used_bytes) +
-                       up(live_bytes) + up(bm_bytes);
+                       up(live_bytes) + up(bm_bytes) + up(amb_bytes);
   char* base = (char*)net_scratch(net, total);
   if (!base) return ISL_E_HIP;
   char* heat = base;
@@ -2161,6 +2634,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   int* live_count = (int*)(used + up(used_bytes));
   int* live = live_count + 1;
   float* bandmax = bm_bytes ? (float*)((char*)live_count + up(live_bytes)) : nullptr;
+  int* amb = (int*)((char*)live_count + up(live_bytes) + up(bm_bytes));
   bool bm_done = false;
 
   hipLaunchKernelGGL(init_records_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (char*)d_result, lay, n, nlimbs);
@@ -2187,10 +2661,9 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     MapSrc fh, fp;   // final-resolution sources
     if (two_stage) {
       float* mh = (float*)midp;
-      float* mp = mh + (size_t)n * g.valid_h * g.valid_w * nparts;
-      midp += (size_t)n * g.valid_h * g.valid_w * (nparts + npaf) * 4;
+      midp += (size_t)n * g.valid_h * g.valid_w * nparts * 4;
       if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, mh, s))) return rc;
-      if ((rc = launch_resize(lp, n, npaf, g.valid_h, g.valid_w, 1, 1.f, mp, s))) return rc;
+      // the PAF's stage 1 is not materialised: limb_kernel samples both stages on demand
       // stage 2: cv2.resize(crop, (W, H)): inv_scale = W / valid_w, scale = 1 / inv_scale
       auto stage2 = [&](MapSrc& m, const float* p, int C, int cn) {
         m.base = p; m.xs = 1; m.ys = g.valid_w; m.cstr = (long long)g.valid_h * g.valid_w;
@@ -2201,7 +2674,9 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
         m.cn = cn; m.identity = 0;
       };
       stage2(fh, mh, nparts, njoint);
-      stage2(fp, mp, npaf, npaf);
+      stage2(fp, nullptr, npaf, npaf);
+      ga.paf1[si] = lp;
+      ga.paf_nested[si] = 1;
     } else {
       fh = lh;
       fp = lp;
@@ -2226,10 +2701,13 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   }
   // blur + NMS (body.py:86-100)
   dim3 gb((W + NMS_TX - 1) / NMS_TX, (H + NMS_TY - 1) / NMS_TY, n * nparts);
-  if (multi)
-    hipLaunchKernelGGL((blur_nms_kernel<double, false>), gb, dim3(256), 0, s, (const double*)heat, H, W, words, mask,
-                       0.1, 0, MapSrc{}, 0, nullptr, nullptr, 0, 0);
-  else if (fused) {
+  tile_prof_arm((size_t)gb.x * gb.y * gb.z, s);
+  const int tx = (int)gb.x, tyl = (int)gb.y;
+  if (multi) {
+    if ((rc = launch_blur<double, false>(gb, s, (const double*)heat, H, W, words, mask, 0.1, 0, MapSrc{}, 0, nullptr,
+                                         nullptr, tx, tyl, nullptr, amb)))
+      return rc;
+  } else if (fused) {
     // live-tile list (low-res bound), then the fused blur over live tiles only
     const int n_tiles = (int)(gb.x * gb.y * gb.z);
     PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));
@@ -2238,23 +2716,36 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     if (wide) {
 #ifdef ISLPOSE_DEV
       hipLaunchKernelGGL((tile_live_kernel<NMS_WSRC_ROWS, NMS_WSRC_COLS>), tl, dim3(256), 0, s, fused_src, nparts, H, W,
-                         (int)gb.x, (int)gb.y, n_tiles, 0.1, live, live_count);
+                         tx, tyl, n_tiles, 0.1, live, live_count);
       PHIP(hipGetLastError());
-      hipLaunchKernelGGL((blur_nms_kernel<float, true, NMS_WSRC_ROWS, NMS_WSRC_COLS>), dim3(std::min(n_tiles, 256 * 4)),
-                         dim3(256), 0, s, (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts, live,
-                         live_count, (int)gb.x, (int)gb.y);
+      if ((rc = launch_blur<float, true, NMS_WSRC_ROWS, NMS_WSRC_COLS>(
+               dim3(std::min(n_tiles, 256 * 4)), s, (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts,
+               live, live_count, tx, tyl, nullptr, amb)))
+        return rc;
 #endif
     } else {
       hipLaunchKernelGGL((tile_live_kernel<NMS_SRC_ROWS, NMS_SRC_COLS>), tl, dim3(256), 0, s, fused_src, nparts, H, W,
-                         (int)gb.x, (int)gb.y, n_tiles, 0.1, live, live_count);
+                         tx, tyl, n_tiles, 0.1, live, live_count);
       PHIP(hipGetLastError());
-      hipLaunchKernelGGL((blur_nms_kernel<float, true>), dim3(std::min(n_tiles, 256 * 8)), dim3(256), 0, s,
-                         (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts, live, live_count,
-                         (int)gb.x, (int)gb.y);
+      if ((rc = launch_blur<float, true>(dim3(std::min(n_tiles, 256 * 8)), s, (const float*)nullptr, H, W, words, mask,
+                                         0.1, 0, fused_src, nparts, live, live_count, tx, tyl, nullptr, amb)))
+        return rc;
     }
-  } else
-    hipLaunchKernelGGL((blur_nms_kernel<float, false>), gb, dim3(256), 0, s, (const float*)heat, H, W, words, mask,
-                       0.1, 0, MapSrc{}, 0, nullptr, nullptr, 0, 0, bm_done ? (const float*)bandmax : nullptr);
+  } else if (bm_done && band_list) {
+    // live-tile list (the band maxima), then the blur over live tiles only
+    const int n_tiles = (int)(gb.x * gb.y * gb.z);
+    PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));
+    PHIP(hipMemsetAsync(live_count, 0, sizeof(int), s));
+    hipLaunchKernelGGL(band_live_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, s, (const float*)bandmax, H, W,
+                       words, tx, tyl, n_tiles, 0.1, live, live_count);
+    PHIP(hipGetLastError());
+    if ((rc = launch_blur<float, false>(dim3(std::min(n_tiles, 256 * 8)), s, (const float*)heat, H, W, words, mask,
+                                        0.1, 0, MapSrc{}, 0, live, live_count, tx, tyl, nullptr, amb)))
+      return rc;
+  } else if ((rc = launch_blur<float, false>(gb, s, (const float*)heat, H, W, words, mask, 0.1, 0, MapSrc{}, 0, nullptr,
+                                             nullptr, tx, tyl, bm_done ? (const float*)bandmax : nullptr, amb))) {
+    return rc;
+  }
   PHIP(hipGetLastError());
   if (multi)
     hipLaunchKernelGGL((compact_kernel<double, false>), dim3(nparts, n), dim3(256), 0, s, mask, (const double*)heat,
@@ -2304,8 +2795,9 @@ static size_t hand_post_bytes(int n, int h, int w, int nscales, const isl_scale_
   const int cc_rows = std::max(1, CC_CHUNK / w), cc_chunks = (h + cc_rows - 1) / cc_rows;
   const size_t ck_bytes = (size_t)n * nparts * cc_chunks * sizeof(CcChunk);
   const size_t bs_bytes = (size_t)n * nparts * CC_KFAST * (P / 8192 + 1) * 8;
+  const size_t amb_bytes = ((size_t)((w + NMS_TX - 1) / NMS_TX) * ((h + NMS_TY - 1) / NMS_TY) * n * nparts + 1) * 4;
   return up(avg_bytes) + up(mid_bytes) + up(mask_bytes) + up(par_bytes) + up(val_bytes) + up(st_bytes) + up(ck_bytes) +
-         up(bs_bytes);
+         up(bs_bytes) + up(amb_bytes);
 }
 
 // the kernels of one hand post (hand.py:51-74) on stream s, scratch at base
@@ -2333,6 +2825,7 @@ static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, cons
   CcStats* stats = (CcStats*)((char*)vals + up(val_bytes));
   CcChunk* cks = (CcChunk*)((char*)stats + up(st_bytes));
   double* bsum = (double*)((char*)cks + up((size_t)n * nparts * cc_chunks * sizeof(CcChunk)));
+  int* amb = (int*)((char*)bsum + up((size_t)n * nparts * CC_KFAST * (P / 8192 + 1) * 8));
   const float div_f = (float)nscales;
   MapSrcN fin;                        // per scale: the resize that lands on the crop
   float* midp = mid;
@@ -2369,9 +2862,10 @@ static int hand_post_launch(isl_net* net, int n, int h, int w, int nscales, cons
     PHIP(hipGetLastError());
   }
   dim3 gb((w + NMS_TX - 1) / NMS_TX, (h + NMS_TY - 1) / NMS_TY, n * nparts);
-  hipLaunchKernelGGL((blur_nms_kernel<double, false>), gb, dim3(256), 0, s, (const double*)avg, h, w, words, mask, 0.05,
-                     1, MapSrc{}, 0, nullptr, nullptr, 0, 0);
-  PHIP(hipGetLastError());
+  tile_prof_arm((size_t)gb.x * gb.y * gb.z, s);
+  if (int rc = launch_blur<double, false>(gb, s, (const double*)avg, h, w, words, mask, 0.05, 1, MapSrc{}, 0, nullptr,
+                                          nullptr, (int)gb.x, (int)gb.y, nullptr, amb))
+    return rc;
   if (h * w <= CC_LDS_MAX) {
     static bool attr = false;
     if (!attr) {

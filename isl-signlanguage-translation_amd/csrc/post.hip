@@ -130,8 +130,11 @@ constexpr int RS_TY = 64, RS_TX = 256, RS_MAXR = 40;   // 64 rows: amortise the 
 // BM (mode 1, 64-row tiles of 128 columns): also the max |value| of every 16-row band x
 // 64-column word of the output plane into bandmax[plane][oh / 16][ow / 64] (the blur's tile
 // liveness, blur_tile: a tile whose window's bands stay below the threshold loads nothing)
+// V4 (mode 1, TX = 128, not identity, ow % 4 == 0): the vertical pass by 4 adjacent columns x
+// ty/4 rows per thread -- ds_read_b128 of the 4 LDS rows, one 16-byte store per output row (the
+// HBM write path wants 16 bytes per lane) -- and with BM one band per thread (ty = 64).
 constexpr int BM_ROWS = 16;
-template <int TX, int VU = 1, int HU = 8, bool BM = false>
+template <int TX, int VU = 1, int HU = 8, bool BM = false, bool V4 = false>
 __global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int oh, int ow, int ty_rows, int mode,
                                                          float inv_div_f, void* out, float* bandmax = nullptr) {
   __shared__ float s_h[RS_MAXR][TX];
@@ -177,6 +180,47 @@ __global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int o
     }
   }
   __syncthreads();
+  if constexpr (V4) {
+    static_assert(TX == 128, "V4: 32 column groups x 4 row groups");
+    const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+    const int xl = cg * 4, xv = blockIdx.z * TX + xl;
+    const int rows = ty_rows / 4, t0 = rg * rows, t1 = min(t0 + rows, ny);
+    const int rowlen = m.dw * m.cn, body = rowlen - rowlen % 4;
+    bool sv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sv[j] = (xv + j) * m.cn + c < body;
+    float bmx = 0.f;
+#pragma unroll 2
+    for (int t = t0; t < t1; ++t) {
+      const int4 yi = s_yi[t];
+      const float4 be = s_be[t];
+      const float4 h0 = *reinterpret_cast<const float4*>(&s_h[yi.x][xl]);
+      const float4 h1 = *reinterpret_cast<const float4*>(&s_h[yi.y][xl]);
+      const float4 h2 = *reinterpret_cast<const float4*>(&s_h[yi.z][xl]);
+      const float4 h3 = *reinterpret_cast<const float4*>(&s_h[yi.w][xl]);
+      auto vc = [&](bool simd, float a0, float a1, float a2, float a3) {
+        return simd ? a0 * be.x + (a1 * be.y + (a2 * be.z + a3 * be.w))   // VResizeCubicVec_32f body
+                    : ((a0 * be.x + a1 * be.y) + a2 * be.z) + a3 * be.w;   // scalar tail
+      };
+      float4 v;
+      v.x = vc(sv[0], h0.x, h1.x, h2.x, h3.x);
+      v.y = vc(sv[1], h0.y, h1.y, h2.y, h3.y);
+      v.z = vc(sv[2], h0.z, h1.z, h2.z, h3.z);
+      v.w = vc(sv[3], h0.w, h1.w, h2.w, h3.w);
+      if (xv < ow) {
+        *reinterpret_cast<float4*>(&((float*)out)[((size_t)plane * oh + y0 + t) * ow + xv]) = v;
+        if constexpr (BM) bmx = fmaxf(bmx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+      }
+    }
+    if constexpr (BM) {
+      // this thread's rows are one band (ty = 64, y0 % 16 == 0): max over the word's 16 lanes
+      for (int o = 8; o > 0; o >>= 1) bmx = fmaxf(bmx, __shfl_xor(bmx, o));
+      const int words = (ow + 63) / 64, bands = (oh + BM_ROWS - 1) / BM_ROWS;
+      if ((cg & 15) == 0 && xv < ow && t0 < ny)
+        bandmax[((size_t)plane * bands + (y0 + t0) / BM_ROWS) * words + xv / 64] = bmx;
+    }
+    return;
+  }
   if (!BM && x >= ow) return;   // (BM: every lane takes part in the band maxima's shuffles)
   const int rowlen = m.dw * m.cn, body = rowlen - rowlen % 4;
   const bool simd = x * m.cn + c < body;
@@ -2501,11 +2545,24 @@ static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mo
   const long long ty_tiles = (oh + ty - 1) / ty;
   if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "resize: output too tall");
   if (bm_done) *bm_done = false;
+  // (ISLPOSE_RESIZE_V4=0: the one-column vertical pass everywhere; A/B, per call)
+  const char* v4e = getenv("ISLPOSE_RESIZE_V4");
+  const bool v4 = mode == 1 && !m.identity && ow % 4 == 0 && ty % 4 == 0 && !(v4e && v4e[0] == '0');
   if (bandmax && mode == 1 && ty % BM_ROWS == 0) {
-    hipLaunchKernelGGL((resize_sep_kernel<128, 4, 8, true>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128),
-                       dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out, bandmax);
+    if (v4 && ty == 4 * BM_ROWS)
+      hipLaunchKernelGGL((resize_sep_kernel<128, 4, 8, true, true>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128),
+                         dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out, bandmax);
+    else
+      hipLaunchKernelGGL((resize_sep_kernel<128, 4, 8, true>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128),
+                         dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out, bandmax);
     PHIP(hipGetLastError());
     if (bm_done) *bm_done = true;
+    return ISL_OK;
+  }
+  if (v4) {
+    hipLaunchKernelGGL((resize_sep_kernel<128, 4, 8, false, true>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128),
+                       dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out);
+    PHIP(hipGetLastError());
     return ISL_OK;
   }
   // 128-column blocks unless 256 pads less (it never does): fewer idle lanes (ow = 328: 384 vs

@@ -4,7 +4,8 @@ Same constructor (body.py:16-37: model_type 'coco' | 'body25', anything else
 prints a message and falls back to COCO; weights through util.transfer) and
 the same call (body.py:39-235): ``Body(...)(oriImg) -> (candidate, subset)``
 with identical dtypes, shapes and values.  The whole call runs on the GPU
-(pre-processing, network, resize, blur/NMS, PAF, assembly); ``scale_search``
+(pre-processing, network, resize, blur/NMS, PAF, assembly) -- on a host without a
+visible HIP device, on the CPU instead (islpose.cpu, as the reference); ``scale_search``
 defaults to the reference's [0.5] and can be changed per instance.
 ``estimate_batch(frames)`` processes a batch of frames in one pass.
 """
@@ -13,6 +14,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from islpose import cpu
 from islpose.body import BodyEstimator
 
 from . import util
@@ -48,8 +50,18 @@ class Body(object):
 
     def __call__(self, oriImg):
         img = oriImg.cpu().numpy() if isinstance(oriImg, torch.Tensor) else np.asarray(oriImg)
-        return self.estimator().estimate(np.ascontiguousarray(img, dtype=np.uint8))
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        if not torch.cuda.is_available():   # GPU-less host: the product's CPU path (body.py:31-32)
+            return cpu.body_call(img, self._cpu_net, "body25" if self.model_type == "body25" else "coco",
+                                 tuple(self.scale_search))
+        return self.estimator().estimate(img)
+
+    def _cpu_net(self, im):
+        with torch.no_grad():
+            return tuple(o.numpy() for o in self.model(torch.from_numpy(im)))
 
     def estimate_batch(self, frames):
         """frames: uint8 [n, H, W, 3] (numpy or torch, BGR) -> [(candidate, subset)] * n."""
+        if not torch.cuda.is_available():
+            return [self(f) for f in frames]
         return self.estimator().estimate(frames)

@@ -2,13 +2,14 @@
 
 Same constructor (hand.py:16-22) and call (hand.py:24-74): 4-scale pyramid,
 fp64 averaging, blur, connected components, largest-mass component, first
-maximum -- all on the GPU.  ``estimate_batch(crops)`` takes equal-size crops.
+maximum -- all on the GPU (on a host without a visible HIP device, on the CPU: islpose.cpu).  ``estimate_batch(crops)`` takes equal-size crops.
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
 
+from islpose import cpu
 from islpose.hand import HandEstimator
 
 from . import util
@@ -35,7 +36,16 @@ class Hand(object):
 
     def __call__(self, oriImg):
         img = oriImg.cpu().numpy() if isinstance(oriImg, torch.Tensor) else np.asarray(oriImg)
-        return self.estimator().estimate(np.ascontiguousarray(img, dtype=np.uint8))
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        if not torch.cuda.is_available():   # GPU-less host: the product's CPU path (hand.py:18-20)
+            return cpu.hand_call(img, self._cpu_net)
+        return self.estimator().estimate(img)
+
+    def _cpu_net(self, im):
+        with torch.no_grad():
+            return self.model(torch.from_numpy(im)).numpy()
 
     def estimate_batch(self, crops):
+        if not torch.cuda.is_available():
+            return [self(c) for c in crops]
         return self.estimator().estimate(crops)

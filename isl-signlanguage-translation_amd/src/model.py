@@ -7,7 +7,9 @@ model.py:66-407 / util.py:35-44), but whose ``forward`` runs the network in
 libislpose.so (FP32-MFMA HIP kernels).  Parameters are pushed to the native
 net on first use and whenever they change.
 
-There is no CPU path: without a GPU (or without the library) forward raises.
+Without a visible HIP device forward runs the modules themselves on the CPU in the
+reference's dataflow (``cpu_forward``; model.py:171-207, 301-328, 394-407) -- the GPU-less
+path of src/body.py / src/hand.py (islpose.cpu).  With a device it never falls back.
 """
 from __future__ import annotations
 
@@ -75,7 +77,10 @@ class _NativeNet(nn.Module):
 
     def forward(self, x):
         if not torch.cuda.is_available():
-            raise RuntimeError("libislpose runs on the GPU only (no CPU fallback): no HIP device visible")
+            if x.is_cuda:
+                raise RuntimeError("a CUDA tensor without a visible HIP device")
+            with torch.no_grad():
+                return self.cpu_forward(x.float())
         dev = x.device if x.is_cuda else torch.device("cuda", torch.cuda.current_device())
         with torch.no_grad():
             out = self.native(dev.index if dev.index is not None else torch.cuda.current_device()).forward(
@@ -105,6 +110,31 @@ class bodypose_25_model(_NativeNet):
             (k, nn.ModuleList([nn.Sequential(OrderedDict(_conv_layers([c]))) for c in v])) for k, v in blocks.items()))
         self._freeze()
 
+    def cpu_forward(self, x):
+        """model.py:171-207: four L2 stages, then two L1 stages; each Mconv block concatenates
+        its three convs' outputs."""
+        def block(t, key):
+            outs = []
+            for m in self.models[key]:
+                t = m(t)
+                outs.append(t)
+            return torch.cat(outs, 1)
+
+        def stage(t, tag):
+            for v in range(1, 6):
+                t = block(t, "Mconv%d_%s" % (v, tag))
+            m67 = self.models["Mconv6_7_%s" % tag]
+            return m67[1](m67[0](t))
+
+        out0 = self.model0(x)
+        t = out0
+        for s in range(4):
+            l2 = stage(t, "stage%d_L2" % s)
+            t = torch.cat([out0, l2], 1)
+        l1 = stage(t, "stage0_L1")
+        l1 = stage(torch.cat([out0, l1, l2], 1), "stage1_L1")
+        return l2, l1
+
 
 class bodypose_model(_NativeNet):
     """COCO-18 (model.py:210-329): forward(x) -> (PAF [N,38,..], heat [N,19,..])."""
@@ -128,6 +158,14 @@ class bodypose_model(_NativeNet):
                 setattr(self, k, nn.Sequential(OrderedDict(_conv_layers(groups[k]))))
         self._freeze()
 
+    def cpu_forward(self, x):
+        """model.py:301-328: six two-branch stages over the VGG features."""
+        out1 = self.model0(x)
+        t = out1
+        for i in range(1, 6):
+            t = torch.cat([getattr(self, "model%d_1" % i)(t), getattr(self, "model%d_2" % i)(t), out1], 1)
+        return self.model6_1(t), self.model6_2(t)
+
 
 class handpose_model(_NativeNet):
     """hand (model.py:331-407): forward(x) -> heat [N,22,h/8,w/8]."""
@@ -142,3 +180,11 @@ class handpose_model(_NativeNet):
             setattr(self, "model%d" % i,
                     nn.Sequential(OrderedDict(_conv_layers([c for c in specs[17:] if c.name.endswith("_stage%d" % i)]))))
         self._freeze()
+
+    def cpu_forward(self, x):
+        """model.py:394-407: the CPM front, then five refinement stages."""
+        out1_0 = self.model1_0(x)
+        t = self.model1_1(out1_0)
+        for i in range(2, 7):
+            t = getattr(self, "model%d" % i)(torch.cat([t, out1_0], 1))
+        return t

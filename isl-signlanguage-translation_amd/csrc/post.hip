@@ -687,19 +687,22 @@ __device__ __forceinline__ void blur_tile_exact(const T* __restrict__ planes, in
   }
   __syncthreads();
   // one wave per (row, 64-column word) -> one 64-bit mask word
-  for (int it = wave; it < NMS_TY * 3; it += 4) {
+#pragma unroll 2
+  for (int q = 0; q < NMS_TY * 3 / 4; ++q) {
+    const int it = wave + 4 * q;
     const int ty = it / 3, wd = it - ty * 3;
     const int y = y0 + ty, cx = wd * 64 + lane, x = x0 + cx;
     bool pk = false;
-    if (y < H && x < W && s_wlive[wd]) {
-      const double g = s_g[ty + 1][cx + 1];
+    const double g = s_g[ty + 1][cx + 1];   // (the reads lie in the tile: unconditional)
+    const double gu = s_g[ty][cx + 1], gd = s_g[ty + 2][cx + 1], gl = s_g[ty + 1][cx], gr = s_g[ty + 1][cx + 2];
+    if (y < H && x < W && (wd == 0 ? wl0 : wd == 1 ? wl1 : wl2)) {
       if (mode_hand) {
         pk = g > thre;                                  // hand.py:62 binary map
       } else {
-        const double up = y > 0 ? s_g[ty][cx + 1] : 0.0;
-        const double dn = y + 1 < H ? s_g[ty + 2][cx + 1] : 0.0;
-        const double lf = x > 0 ? s_g[ty + 1][cx] : 0.0;
-        const double rt = x + 1 < W ? s_g[ty + 1][cx + 2] : 0.0;
+        const double up = y > 0 ? gu : 0.0;
+        const double dn = y + 1 < H ? gd : 0.0;
+        const double lf = x > 0 ? gl : 0.0;
+        const double rt = x + 1 < W ? gr : 0.0;
         pk = g >= up && g >= dn && g >= lf && g >= rt && g > thre;   // body.py:99-100
       }
     }
@@ -726,7 +729,6 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
   __shared__ float s_hz[FUSED ? WR : 1][NMS_VC];
   __shared__ int4 s_ti[FUSED ? NMS_IR : 1];
   __shared__ float4 s_tb[FUSED ? NMS_IR : 1];
-  __shared__ long long s_roff[FUSED ? 1 : NMS_IR];   // plane offsets of the window's rows
   __shared__ double s_cmax[2][NMS_VC];          // max |in| of every window column, per row half
   __shared__ double s_M;                        // max |in| over the window (the margin)
   __shared__ int s_live, s_amb;
@@ -748,7 +750,6 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
       zero_masks();
       return;
     }
-    if (tid < NMS_IR) s_roff[tid] = (long long)reflect_idx(y0 - 1 - NMS_R + tid, H) * W;
   } else {
     if (!fused_prologue<WR, WC>(m, nch, plane, H, W, y0, x0, thre, s_low, s_hz, s_ti, s_tb, &s_live)) {
       zero_masks();
@@ -763,7 +764,7 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
   TPROF(3, clock64());
   // the window: column pair cp (window columns 2cp, 2cp+1) of rows vh*9 .. vh*9+32 (v rows
   // vh*9 .. vh*9+8) per thread, waves 0-1 the first half, 2-3 the second
-  const int cp = tid & 127, vh = tid >> 7;
+  const int cp = tid & 127, vh = __builtin_amdgcn_readfirstlane(tid >> 7);   // (wave-uniform)
   const bool vth = cp < NMS_CP;
   f2v a[NMS_VH + 2 * NMS_R];
   if (vth) {
@@ -775,9 +776,11 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
       const int r = vh * NMS_VH + k;
       T va, vb;
       if constexpr (!FUSED) {
-        const long long ro = s_roff[r];
-        va = src[ro + xa];
-        vb = src[ro + xb];
+        // the row is wave-uniform: its reflection and offset are scalar work
+        const int rr = y0 - 1 - NMS_R + r;
+        const T* row = src + (size_t)((unsigned)rr < (unsigned)H ? rr : reflect_idx(rr, H)) * W;
+        va = row[xa];
+        vb = row[xb];
       } else {
         va = fused_value(m, plane % nch, s_hz, s_ti, s_tb, r, 2 * cp, xa);
         vb = fused_value(m, plane % nch, s_hz, s_ti, s_tb, r, 2 * cp + 1, xb);
@@ -869,21 +872,27 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
   TPROF(6, clock64());
   // (margin_mode 2: a margin of M / 4, the re-run of nearly every live tile -- tests)
   const double eps = s_M * (margin_mode == 2 ? 0.25 : BLUR_EPS_REL) + 1e-30, e2 = 2.0 * eps;
-  for (int it = wave; it < NMS_TY * 3; it += 4) {
+  // 12 (row, word) items per wave, two at a time; each item's five LDS reads are unconditional (rows
+  // R-1..R+1, columns cx..cx+2 lie in the tile) so they issue together -- behind the plane-edge
+  // branches they were five serialised LDS round trips per item
+#pragma unroll 2
+  for (int q = 0; q < NMS_TY * 3 / 4; ++q) {
+    const int it = wave + 4 * q;
     const int ty = it / 3, wd = it - ty * 3;
     const int y = y0 + ty, cx = wd * 64 + lane, x = x0 + cx;
+    const int R = ty + 1;
+    const double g = s_vf[R][cx + 1];
+    const float fu = s_vf[R - 1][cx + 1], fd = s_vf[R + 1][cx + 1], fl = s_vf[R][cx], fr = s_vf[R][cx + 2];
     bool pk = false, open = false;
-    if (y < H && x < W && s_wlive[wd]) {
-      const int R = ty + 1;
-      const double g = s_vf[R][cx + 1];
+    if (y < H && x < W && (wd == 0 ? wl0 : wd == 1 ? wl1 : wl2)) {
       bool no = g + eps <= thre;                 // surely g <= thre
       open = !no && !(g - eps > thre);           // g vs thre inside the margin
       if (!mode_hand) {
         // per neighbour q: surely g < q (the pixel is out), or g vs q inside the margin
-        const double d0 = g - (y > 0 ? (double)s_vf[R - 1][cx + 1] : 0.0);
-        const double d1 = g - (y + 1 < H ? (double)s_vf[R + 1][cx + 1] : 0.0);
-        const double d2 = g - (x > 0 ? (double)s_vf[R][cx] : 0.0);
-        const double d3 = g - (x + 1 < W ? (double)s_vf[R][cx + 2] : 0.0);
+        const double d0 = g - (y > 0 ? (double)fu : 0.0);
+        const double d1 = g - (y + 1 < H ? (double)fd : 0.0);
+        const double d2 = g - (x > 0 ? (double)fl : 0.0);
+        const double d3 = g - (x + 1 < W ? (double)fr : 0.0);
         no = no || d0 < -e2 || d1 < -e2 || d2 < -e2 || d3 < -e2;
         open = open || !(d0 >= e2) || !(d1 >= e2) || !(d2 >= e2) || !(d3 >= e2);
       }
@@ -927,8 +936,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof
   if (!live) {
     run(blockIdx.z, blockIdx.y, blockIdx.x);
   } else {
+    // XCD-aware: workgroups land on the 8 XCDs round-robin, so XCD x takes the x-th eighth of
+    // the (roughly tile-ordered) list -- neighbouring tiles, whose windows share 26 of 42 rows,
+    // then meet in one L2 (any placement is correct; a grid that is not a multiple of 8 strides)
     const int cnt = *live_count;
-    for (int k = blockIdx.x; k < cnt; k += gridDim.x) {
+    constexpr int NX = 8;
+    const bool part = gridDim.x % NX == 0;
+    const int xcd = part ? blockIdx.x % NX : 0, per = part ? gridDim.x / NX : gridDim.x;
+    const int k0 = part ? (int)((long long)cnt * xcd / NX) : 0;
+    const int k1 = part ? (int)((long long)cnt * (xcd + 1) / NX) : cnt;
+    for (int k = k0 + (part ? blockIdx.x / NX : blockIdx.x); k < k1; k += per) {
       const int t = live[k];
       const int bx = t % tiles_x, r = t / tiles_x, by = r % tiles_y, plane = r / tiles_y;
       run(plane, by, bx);
@@ -2776,7 +2793,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
                          tx, tyl, n_tiles, 0.1, live, live_count);
       PHIP(hipGetLastError());
       if ((rc = launch_blur<float, true, NMS_WSRC_ROWS, NMS_WSRC_COLS>(
-               dim3(std::min(n_tiles, 256 * 4)), s, (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts,
+               dim3(std::min((n_tiles + 7) / 8 * 8, 256 * 4)), s, (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts,
                live, live_count, tx, tyl, nullptr, amb)))
         return rc;
 #endif
@@ -2784,7 +2801,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       hipLaunchKernelGGL((tile_live_kernel<NMS_SRC_ROWS, NMS_SRC_COLS>), tl, dim3(256), 0, s, fused_src, nparts, H, W,
                          tx, tyl, n_tiles, 0.1, live, live_count);
       PHIP(hipGetLastError());
-      if ((rc = launch_blur<float, true>(dim3(std::min(n_tiles, 256 * 8)), s, (const float*)nullptr, H, W, words, mask,
+      if ((rc = launch_blur<float, true>(dim3(std::min((n_tiles + 7) / 8 * 8, 256 * 8)), s, (const float*)nullptr, H, W, words, mask,
                                          0.1, 0, fused_src, nparts, live, live_count, tx, tyl, nullptr, amb)))
         return rc;
     }
@@ -2796,7 +2813,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     hipLaunchKernelGGL(band_live_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, s, (const float*)bandmax, H, W,
                        words, tx, tyl, n_tiles, 0.1, live, live_count);
     PHIP(hipGetLastError());
-    if ((rc = launch_blur<float, false>(dim3(std::min(n_tiles, 256 * 8)), s, (const float*)heat, H, W, words, mask,
+    if ((rc = launch_blur<float, false>(dim3(std::min((n_tiles + 7) / 8 * 8, 256 * 8)), s, (const float*)heat, H, W, words, mask,
                                         0.1, 0, MapSrc{}, 0, live, live_count, tx, tyl, nullptr, amb)))
       return rc;
   } else if ((rc = launch_blur<float, false>(gb, s, (const float*)heat, H, W, words, mask, 0.1, 0, MapSrc{}, 0, nullptr,

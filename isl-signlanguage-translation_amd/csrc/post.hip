@@ -432,7 +432,8 @@ constexpr double CUBIC_ABS_SUM_SQ = 1.890625;      // max over t of (sum_k |cubi
 // so with M = max |in| over the tile's window |v32 - v| <= 14.01 u M and |g32 - g| <= 28.1 u M
 // (u = 2^-24; the fp64 passes and the fp32 rounding of fp64 planes add < 1.1 u M).  With
 // eps = 2^-18 M (64 u M) a pixel whose every comparison clears the margin (g vs thre by eps,
-// g vs a neighbour by 2 eps) has the fp64 decision; a tile with any pixel inside a margin
+// g vs a neighbour by 2 eps; compared in fp32 with the margin doubled, see the NMS below) has
+// the fp64 decision; a tile with any pixel inside a margin
 // (a peak at the threshold, two near-equal neighbours at a peak: rare) is appended to a list
 // that a second launch re-runs on the exact fp64 passes (blur_tile_exact), which rewrite all
 // of the tile's words.  The mask bits are the fp64 ones either way.  The filter's tile keeps
@@ -870,8 +871,12 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
   }
   __syncthreads();
   TPROF(6, clock64());
-  // (margin_mode 2: a margin of M / 4, the re-run of nearly every live tile -- tests)
-  const double eps = s_M * (margin_mode == 2 ? 0.25 : BLUR_EPS_REL) + 1e-30, e2 = 2.0 * eps;
+  // The decisions in fp32: d = fl(g - q) is within 2 u M of g32 - q32 (|g|, |q| <= M) and
+  // thre_f = (float)thre within u thre <= u M of thre (a live tile has M >= thre), so with the
+  // margin doubled to 2^-17 M (128 u M) the three roundings stay far inside it: "surely" still
+  // means the fp64 decision.  (margin_mode 2: M / 4, the re-run of nearly every live tile.)
+  const float eps = (float)(s_M * (margin_mode == 2 ? 0.25 : 2.0 * BLUR_EPS_REL)) + 1e-30f, e2 = 2.f * eps;
+  const float thre_f = (float)thre;
   // 12 (row, word) items per wave, two at a time; each item's five LDS reads are unconditional (rows
   // R-1..R+1, columns cx..cx+2 lie in the tile) so they issue together -- behind the plane-edge
   // branches they were five serialised LDS round trips per item
@@ -881,18 +886,19 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
     const int ty = it / 3, wd = it - ty * 3;
     const int y = y0 + ty, cx = wd * 64 + lane, x = x0 + cx;
     const int R = ty + 1;
-    const double g = s_vf[R][cx + 1];
+    const float g = s_vf[R][cx + 1];
     const float fu = s_vf[R - 1][cx + 1], fd = s_vf[R + 1][cx + 1], fl = s_vf[R][cx], fr = s_vf[R][cx + 2];
     bool pk = false, open = false;
     if (y < H && x < W && (wd == 0 ? wl0 : wd == 1 ? wl1 : wl2)) {
-      bool no = g + eps <= thre;                 // surely g <= thre
-      open = !no && !(g - eps > thre);           // g vs thre inside the margin
+      const float dt = g - thre_f;
+      bool no = dt <= -eps;                      // surely g < thre
+      open = !no && !(dt > eps);                 // g vs thre inside the margin
       if (!mode_hand) {
         // per neighbour q: surely g < q (the pixel is out), or g vs q inside the margin
-        const double d0 = g - (y > 0 ? (double)fu : 0.0);
-        const double d1 = g - (y + 1 < H ? (double)fd : 0.0);
-        const double d2 = g - (x > 0 ? (double)fl : 0.0);
-        const double d3 = g - (x + 1 < W ? (double)fr : 0.0);
+        const float d0 = g - (y > 0 ? fu : 0.f);
+        const float d1 = g - (y + 1 < H ? fd : 0.f);
+        const float d2 = g - (x > 0 ? fl : 0.f);
+        const float d3 = g - (x + 1 < W ? fr : 0.f);
         no = no || d0 < -e2 || d1 < -e2 || d2 < -e2 || d3 < -e2;
         open = open || !(d0 >= e2) || !(d1 >= e2) || !(d2 >= e2) || !(d3 >= e2);
       }

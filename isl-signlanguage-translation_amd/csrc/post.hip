@@ -877,40 +877,48 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
   // means the fp64 decision.  (margin_mode 2: M / 4, the re-run of nearly every live tile.)
   const float eps = (float)(s_M * (margin_mode == 2 ? 0.25 : 2.0 * BLUR_EPS_REL)) + 1e-30f, e2 = 2.f * eps;
   const float thre_f = (float)thre;
-  // 12 (row, word) items per wave, two at a time; each item's five LDS reads are unconditional (rows
-  // R-1..R+1, columns cx..cx+2 lie in the tile) so they issue together -- behind the plane-edge
-  // branches they were five serialised LDS round trips per item
-#pragma unroll 2
-  for (int q = 0; q < NMS_TY * 3 / 4; ++q) {
-    const int it = wave + 4 * q;
-    const int ty = it / 3, wd = it - ty * 3;
-    const int y = y0 + ty, cx = wd * 64 + lane, x = x0 + cx;
-    const int R = ty + 1;
-    const float g = s_vf[R][cx + 1];
-    const float fu = s_vf[R - 1][cx + 1], fd = s_vf[R + 1][cx + 1], fl = s_vf[R][cx], fr = s_vf[R][cx + 2];
-    bool pk = false, open = false;
-    if (y < H && x < W && (wd == 0 ? wl0 : wd == 1 ? wl1 : wl2)) {
-      const float dt = g - thre_f;
-      bool no = dt <= -eps;                      // surely g < thre
-      open = !no && !(dt > eps);                 // g vs thre inside the margin
-      if (!mode_hand) {
-        // per neighbour q: surely g < q (the pixel is out), or g vs q inside the margin
-        const float d0 = g - (y > 0 ? fu : 0.f);
-        const float d1 = g - (y + 1 < H ? fd : 0.f);
-        const float d2 = g - (x > 0 ? fl : 0.f);
-        const float d3 = g - (x + 1 < W ? fr : 0.f);
-        no = no || d0 < -e2 || d1 < -e2 || d2 < -e2 || d3 < -e2;
-        open = open || !(d0 >= e2) || !(d1 >= e2) || !(d2 >= e2) || !(d3 >= e2);
+  // Rows ty = wave, wave+4, .. (wave-uniform), the row's three mask words unrolled: one LDS
+  // base per row with immediate offsets, the five reads of a pixel unconditional (rows R-1..R+1,
+  // columns cx..cx+2 lie in the tile; behind the plane-edge branches they were serialised LDS
+  // round trips), one mask row address per row.
+  bool any_open = false;
+  for (int ty = wave; ty < NMS_TY; ty += 4) {
+    const int y = y0 + ty, R = ty + 1;
+    const float* rp = &s_vf[R][lane];
+    unsigned long long wv[3];
+#pragma unroll
+    for (int wd = 0; wd < 3; ++wd) {
+      const int cx = wd * 64 + lane, x = x0 + cx;
+      const float g = rp[wd * 64 + 1];
+      const float fu = rp[wd * 64 + 1 - NMS_VC], fd = rp[wd * 64 + 1 + NMS_VC], fl = rp[wd * 64], fr = rp[wd * 64 + 2];
+      bool pk = false, open = false;
+      if (y < H && x < W && (wd == 0 ? wl0 : wd == 1 ? wl1 : wl2)) {
+        const float dt = g - thre_f;
+        bool no = dt <= -eps;                      // surely g < thre
+        open = !no && !(dt > eps);                 // g vs thre inside the margin
+        if (!mode_hand) {
+          // per neighbour q: surely g < q (the pixel is out), or g vs q inside the margin
+          const float d0 = g - (y > 0 ? fu : 0.f);
+          const float d1 = g - (y + 1 < H ? fd : 0.f);
+          const float d2 = g - (x > 0 ? fl : 0.f);
+          const float d3 = g - (x + 1 < W ? fr : 0.f);
+          no = no || d0 < -e2 || d1 < -e2 || d2 < -e2 || d3 < -e2;
+          open = open || !(d0 >= e2) || !(d1 >= e2) || !(d2 >= e2) || !(d3 >= e2);
+        }
+        pk = !no && !open;
+        open = !no && open;
       }
-      pk = !no && !open;
-      open = !no && open;
+      wv[wd] = __ballot(pk);
+      any_open = any_open || __ballot(open) != 0;
     }
-    const unsigned long long word = __ballot(pk);
-    const unsigned long long am = __ballot(open);
-    const int wi = bx * 3 + wd;
-    if (lane == 0 && y < H && wi < words) mask[((size_t)plane * H + y) * words + wi] = word;
-    if (lane == 0 && am) s_amb = 1;
+    if (lane == 0 && y < H) {
+      unsigned long long* mrow = mask + ((size_t)plane * H + y) * words + bx * 3;
+#pragma unroll
+      for (int wd = 0; wd < 3; ++wd)
+        if (bx * 3 + wd < words) mrow[wd] = wv[wd];
+    }
   }
+  if (lane == 0 && any_open) s_amb = 1;
   __syncthreads();
   TPROF(7, clock64());
   TPROF(1, wall_clock64());

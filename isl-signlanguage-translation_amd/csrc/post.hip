@@ -136,11 +136,15 @@ constexpr int RS_TY = 64, RS_TX = 256, RS_MAXR = 40;   // 64 rows: amortise the 
 constexpr int BM_ROWS = 16;
 template <int TX, int VU = 1, int HU = 8, bool BM = false, bool V4 = false>
 __global__ void __launch_bounds__(TX) resize_sep_kernel(MapSrc m, int nch, int oh, int ow, int ty_rows, int mode,
-                                                         float inv_div_f, void* out, float* bandmax = nullptr) {
+                                                         float inv_div_f, void* out, float* bandmax = nullptr,
+                                                         const unsigned char* __restrict__ need = nullptr) {
   __shared__ float s_h[RS_MAXR][TX];
   __shared__ int4 s_yi[RS_TY];
   __shared__ float4 s_be[RS_TY];
   const int plane = blockIdx.x, f = plane / nch, c = plane - f * nch;
+  // need (stage2_need_kernel): tiles no live blur window reads are not computed (their band
+  // maxima are never read either: band_live_kernel requires the tile's live_mid first)
+  if (need && !need[((size_t)plane * gridDim.y + blockIdx.y) * gridDim.z + blockIdx.z]) return;
   const int y0 = blockIdx.y * ty_rows, x = blockIdx.z * TX + threadIdx.x;
   const int ny = min(ty_rows, oh - y0);
   const float* b = m.base + (size_t)f * m.fs + chan_off(m, c);
@@ -1001,16 +1005,54 @@ static int launch_blur(dim3 grid, hipStream_t s, const T* planes, int H, int W, 
   return hipGetLastError() == hipSuccess ? ISL_OK : ISL_E_HIP;
 }
 
+// Two-stage single-scale frames (Mode R: the net's valid crop -> stage 1 -> stage 2 to the frame):
+// which blur tiles can be live at all, from the stage-1 planes' band maxima (bm1: 16-row bands
+// x 64-column words, resize_sep_kernel BM), and which stage-2 resize tiles (rows ty2 x 128
+// columns) their windows read.  |stage-2 value| <= 1.890625 max|stage-1 value| over its 4 x 4
+// taps (the cubic weights' absolute sums, squared), fp32 rounding inside the 1.9 factor
+// (blur_tile's fused bound), so a tile whose window's stage-1 source stays below thre / 1.9 is
+// dead; every tile a live window overlaps is marked in `need` (zeroed by the caller).
+__global__ void __launch_bounds__(256) stage2_need_kernel(MapSrc m2, const float* __restrict__ bm1, int H, int W,
+                                                          int tiles_x, int tiles_y, int n_tiles, double thre, int ty2,
+                                                          int ry_tiles, int rx_tiles, unsigned char* __restrict__ live_mid,
+                                                          unsigned char* __restrict__ need) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n_tiles) return;
+  const int bx = t % tiles_x, r = t / tiles_x, by = r % tiles_y, plane = r / tiles_y;
+  const int y0 = by * NMS_TY, x0 = bx * NMS_TX;
+  int rlo, rhi, clo, chi;
+  reflect_range(y0 - 1 - NMS_R, y0 - 2 - NMS_R + NMS_IR, H, &rlo, &rhi);
+  reflect_range(x0 - 1 - NMS_R, x0 - 2 - NMS_R + NMS_VC, W, &clo, &chi);
+  int a[4], b[4];
+  float dmy[4];
+  taps(rlo, m2.scy, m2.sh, a, dmy);
+  taps(rhi, m2.scy, m2.sh, b, dmy);
+  const int mb0 = a[0] / BM_ROWS, mb1 = b[3] / BM_ROWS;
+  taps(clo, m2.scx, m2.sw, a, dmy);
+  taps(chi, m2.scx, m2.sw, b, dmy);
+  const int mw0 = a[0] / 64, mw1 = b[3] / 64;
+  const int bands1 = (m2.sh + BM_ROWS - 1) / BM_ROWS, words1 = (m2.sw + 63) / 64;
+  float mx = 0.f;
+  for (int i = mb0; i <= mb1; ++i)
+    for (int j = mw0; j <= mw1; ++j) mx = fmaxf(mx, bm1[((size_t)plane * bands1 + i) * words1 + j]);
+  const bool lv = (double)mx * 1.9 >= thre * (1.0 - 1e-9);
+  live_mid[t] = lv;
+  if (lv)
+    for (int ry = rlo / ty2; ry <= rhi / ty2; ++ry)
+      for (int rx = clo / 128; rx <= chi / 128; ++rx) need[((size_t)plane * ry_tiles + ry) * rx_tiles + rx] = 1;
+}
+
 // The band-maxima bound of the materialised single-scale path, one tile per thread: the
 // tile's window, reflected, against resize_sep_kernel's band x word maxima (blur_tile's own
 // early out, before any block is launched for the tile); live tiles are appended to `live`
 // (one atomic per wave).  The blur then runs over the live tiles only (mask pre-zeroed).
 __global__ void __launch_bounds__(256) band_live_kernel(const float* __restrict__ bandmax, int H, int W, int words,
                                                         int tiles_x, int tiles_y, int n_tiles, double thre,
-                                                        int* __restrict__ live, int* __restrict__ live_count) {
+                                                        int* __restrict__ live, int* __restrict__ live_count,
+                                                        const unsigned char* __restrict__ live_mid = nullptr) {
   const int t = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63;
   int lv = 0;
-  if (t < n_tiles) {
+  if (t < n_tiles && (!live_mid || live_mid[t])) {   // (stage-2 tiles of a dead window were skipped)
     const int bx = t % tiles_x, r = t / tiles_x, by = r % tiles_y, plane = r / tiles_y;
     const int y0 = by * NMS_TY, x0 = bx * NMS_TX;
     int rlo, rhi, clo, chi;
@@ -2568,11 +2610,21 @@ static int post_fail(int code, const char* msg) {
 // planar resize of n*nch planes (see resize_sep_kernel); rows per tile sized to the LDS window
 // bandmax (mode 1): also write the band maxima of the output planes (resize_sep_kernel BM) when
 // the tiles align with the bands; *bm_done says whether they were written
-static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mode, float div_f, void* out,
-                         hipStream_t s, float* bandmax = nullptr, bool* bm_done = nullptr) {
+static int resize_rows(const MapSrc& m) {   // output rows per resize tile
   int ty = RS_TY;
   if (!m.identity)
     while (ty > 1 && (ty - 1) * m.scy + 5.0 > (double)RS_MAXR) --ty;
+  return ty;
+}
+// the band-maxima form of launch_resize runs (and so `need` may be given)
+static bool resize_bm_v4(const MapSrc& m, int ow) {
+  const char* v4e = getenv("ISLPOSE_RESIZE_V4");
+  return !m.identity && ow % 4 == 0 && resize_rows(m) == 4 * BM_ROWS && !(v4e && v4e[0] == '0');
+}
+static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mode, float div_f, void* out,
+                         hipStream_t s, float* bandmax = nullptr, bool* bm_done = nullptr,
+                         const unsigned char* need = nullptr) {
+  const int ty = resize_rows(m);
   const long long ty_tiles = (oh + ty - 1) / ty;
   if (ty_tiles > 65535) return post_fail(ISL_E_ARG, "resize: output too tall");
   if (bm_done) *bm_done = false;
@@ -2582,7 +2634,9 @@ static int launch_resize(const MapSrc& m, int n, int nch, int oh, int ow, int mo
   if (bandmax && mode == 1 && ty % BM_ROWS == 0) {
     if (v4 && ty == 4 * BM_ROWS)
       hipLaunchKernelGGL((resize_sep_kernel<128, 4, 8, true, true>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128),
-                         dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out, bandmax);
+                         dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out, bandmax, need);
+    else if (need)
+      return post_fail(ISL_E_ARG, "resize: `need` without the band-maxima form");
     else
       hipLaunchKernelGGL((resize_sep_kernel<128, 4, 8, true>), dim3(n * nch, (unsigned)ty_tiles, (ow + 127) / 128),
                          dim3(128), 0, s, m, nch, oh, ow, ty, mode, div_f, out, bandmax);
@@ -2709,9 +2763,26 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   const size_t bm_bytes = (!fused && !multi && bands_on) ? (size_t)n * nparts * ((H + BM_ROWS - 1) / BM_ROWS) * words * 4 : 0;
   const size_t live_bytes = (fused || (bm_bytes && band_list)) ? (n_tiles_all + 1) * sizeof(int) : 0;
   const size_t amb_bytes = (n_tiles_all + 1) * sizeof(int);   // the filter's undecided tiles
+  // two-stage frames: stage-2 tiles that no live window reads are skipped (stage2_need_kernel;
+  // ISLPOSE_RESIZE_SKIP=0 off, A/B, per call).  bm1: the stage-1 planes' band maxima
+  const char* rse = getenv("ISLPOSE_RESIZE_SKIP");
+  const isl_scale_geom& g0 = geom[0];
+  MapSrc m2probe{};
+  m2probe.identity = 0;
+  m2probe.scy = 1.0 / ((double)H / g0.valid_h);
+  MapSrc m1probe{};
+  m1probe.identity = 0;
+  m1probe.scy = 1.0 / 8.0;
+  const bool skip2 = !fused && !multi && two && bm_bytes && band_list && !(rse && rse[0] == '0') &&
+                     resize_bm_v4(m1probe, g0.valid_w) && resize_bm_v4(m2probe, W);
+  const int ty2 = resize_rows(m2probe), ry_tiles = (H + ty2 - 1) / ty2, rx_tiles = (W + 127) / 128;
+  const size_t bm1_bytes = skip2 ? (size_t)n * nparts * ((g0.valid_h + BM_ROWS - 1) / BM_ROWS) * ((g0.valid_w + 63) / 64) * 4 : 0;
+  const size_t lmid_bytes = skip2 ? n_tiles_all : 0;
+  const size_t need_bytes = skip2 ? (size_t)n * nparts * ry_tiles * rx_tiles : 0;
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t total = up(heat_bytes) + up(mid_bytes) + up(mask_bytes) + up(pair_bytes) + up(used_bytes) +
-                       up(live_bytes) + up(bm_bytes) + up(amb_bytes);
+                       up(live_bytes) + up(bm_bytes) + up(amb_bytes) + up(bm1_bytes) + up(lmid_bytes) +
+                       up(need_bytes);
   char* base = (char*)net_scratch(net, total);
   if (!base) return ISL_E_HIP;
   char* heat = base;
@@ -2723,6 +2794,9 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   int* live = live_count + 1;
   float* bandmax = bm_bytes ? (float*)((char*)live_count + up(live_bytes)) : nullptr;
   int* amb = (int*)((char*)live_count + up(live_bytes) + up(bm_bytes));
+  float* bm1 = skip2 ? (float*)((char*)amb + up(amb_bytes)) : nullptr;
+  unsigned char* live_mid = skip2 ? (unsigned char*)bm1 + up(bm1_bytes) : nullptr;
+  unsigned char* need = skip2 ? live_mid + up(lmid_bytes) : nullptr;
   bool bm_done = false;
 
   hipLaunchKernelGGL(init_records_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (char*)d_result, lay, n, nlimbs);
@@ -2750,7 +2824,10 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     if (two_stage) {
       float* mh = (float*)midp;
       midp += (size_t)n * g.valid_h * g.valid_w * nparts * 4;
-      if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, mh, s))) return rc;
+      bool bm1_done = false;
+      if ((rc = launch_resize(lh, n, nparts, g.valid_h, g.valid_w, 1, 1.f, mh, s, skip2 ? bm1 : nullptr, &bm1_done)))
+        return rc;
+      if (skip2 && !bm1_done) return post_fail(ISL_E_HIP, "body post: stage-1 band maxima not written");
       // the PAF's stage 1 is not materialised: limb_kernel samples both stages on demand
       // stage 2: cv2.resize(crop, (W, H)): inv_scale = W / valid_w, scale = 1 / inv_scale
       auto stage2 = [&](MapSrc& m, const float* p, int C, int cn) {
@@ -2771,7 +2848,16 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     }
     if (fused) fused_src = fh;   // no full-resolution heat: blur_nms resizes on the fly
     else if (multi) fin.m[si] = fh;   // every scale's final resize, one fp64 pass below
-    else if ((rc = launch_resize(fh, n, nparts, H, W, 1, div_f, heat, s, bandmax, &bm_done))) return rc;
+    else {
+      if (skip2) {
+        const int tx = (W + NMS_TX - 1) / NMS_TX, tyl = (H + NMS_TY - 1) / NMS_TY, nt = (int)n_tiles_all;
+        PHIP(hipMemsetAsync(need, 0, need_bytes, s));
+        hipLaunchKernelGGL(stage2_need_kernel, dim3((nt + 255) / 256), dim3(256), 0, s, fh, (const float*)bm1, H, W, tx,
+                           tyl, nt, 0.1, ty2, ry_tiles, rx_tiles, live_mid, need);
+        PHIP(hipGetLastError());
+      }
+      if ((rc = launch_resize(fh, n, nparts, H, W, 1, div_f, heat, s, bandmax, &bm_done, need))) return rc;
+    }
     ga.paf[si] = fp;
   }
   if (multi) {
@@ -2825,7 +2911,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));
     PHIP(hipMemsetAsync(live_count, 0, sizeof(int), s));
     hipLaunchKernelGGL(band_live_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, s, (const float*)bandmax, H, W,
-                       words, tx, tyl, n_tiles, 0.1, live, live_count);
+                       words, tx, tyl, n_tiles, 0.1, live, live_count, (const unsigned char*)live_mid);
     PHIP(hipGetLastError());
     if ((rc = launch_blur<float, false>(dim3(std::min((n_tiles + 7) / 8 * 8, 256 * 8)), s, (const float*)heat, H, W, words, mask,
                                         0.1, 0, MapSrc{}, 0, live, live_count, tx, tyl, nullptr, amb)))

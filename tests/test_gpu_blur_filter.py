@@ -91,3 +91,25 @@ def test_hand_filter_matches_fp64_and_oracle(monkeypatch, kind):
     it = iter(per)
     ref = cpu_ref.hand_call(np.zeros((h, w, 3), np.uint8), lambda im: next(it)[None])
     assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("H,W", [(368, 656), (400, 520), (1080, 1920)])
+def test_stage2_skip_matches_full_resize(est25, monkeypatch, H, W):
+    """Mode R geometry (scale 0.5: stage 1 to the net's valid crop, stage 2 to the frame): the
+    stage-2 resize tiles that no live blur window can read are skipped (stage2_need_kernel, from
+    the stage-1 band maxima) -- the same peaks and persons as resizing every tile
+    (ISLPOSE_RESIZE_SKIP=0) and as the oracle, on noisy maps around the threshold, batch 3."""
+    geoms = [g[1:] for g in scale_geometry(H, W, (0.5,))]
+    ms = [_heat(geoms[0][0] // 8, geoms[0][1] // 8, 50 + i, "noise" if i != 1 else "plateau") for i in range(3)]
+    pafs = [torch.from_numpy(np.stack([m[0] for m in ms])).cuda()]
+    heats = [torch.from_numpy(np.stack([m[1] for m in ms])).cuda()]
+    monkeypatch.delenv("ISLPOSE_RESIZE_SKIP", raising=False)
+    got = est25.post_maps(H, W, geoms, pafs, heats)
+    monkeypatch.setenv("ISLPOSE_RESIZE_SKIP", "0")
+    ref = est25.post_maps(H, W, geoms, pafs, heats)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a.candidate, b.candidate) and np.array_equal(a.subset, b.subset)
+    heat_avg, paf_avg = cpu_ref.body_maps(np.zeros((H, W, 3), np.uint8), lambda im: (ms[0][0][None], ms[0][1][None]),
+                                          "body25", (0.5,))
+    cand, subset, _, _ = cpu_ref.body_post(heat_avg, paf_avg, "body25", H)
+    assert np.array_equal(got[0].candidate, cand) and np.array_equal(got[0].subset, subset) and len(cand) > 0

@@ -11,7 +11,7 @@ if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $O/tests.log | head -20; exit
 timeout -k 10 200 python3 tools/tile_prof.py --scale 0.5 > $O/tile_r.json 2> $O/tile.err &&
 timeout -k 10 200 python3 tools/tile_prof.py --scale 1.0 > $O/tile_n.json 2>> $O/tile.err &&
 timeout -k 10 200 python3 tools/post_prof.py --batch 32 --iters 10 > $O/post_r.txt 2>&1 &&
-ISLPOSE_BLUR_EXACT=1 timeout -k 10 200 python3 tools/post_prof.py --batch 32 --iters 10 > $O/post_rx.txt 2>&1 &&
+ISLPOSE_RESIZE_SKIP=0 timeout -k 10 200 python3 tools/post_prof.py --batch 32 --iters 10 > $O/post_rx.txt 2>&1 &&
 timeout -k 10 200 python3 tools/post_prof.py --batch 32 --iters 10 --scale 1.0 > $O/post_n.txt 2>&1 &&
 ISLPOSE_BLUR_EXACT=1 timeout -k 10 200 python3 tools/post_prof.py --batch 32 --iters 10 --scale 1.0 > $O/post_nx.txt 2>&1 &&
 timeout -k 10 200 python3 tools/post_prof.py --batch 1 --iters 20 > $O/post_r1.txt 2>&1 &&

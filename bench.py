@@ -548,8 +548,8 @@ def post_fields(H, W, B, post_ms, pairs):
     prof = os.path.join(REPO, "profiles", "post_traffic.json")
     if os.path.exists(prof):
         pj = json.load(open(prof))
-        out["pmc"] = {k: pj[k] for k in ("blur_nms_kernel", "limb_kernel", "tile_live_kernel", "compact_kernel")
-                      if k in pj}
+        out["pmc"] = {k: pj[k] for k in ("blur_nms_kernel", "blur_nms_exact", "limb_kernel", "tile_live_kernel",
+                                         "band_live_kernel", "compact_kernel", "assemble_kernel") if k in pj}
         out["pmc_source"] = pj.get("source")
         out["pmc_peak_GBps"] = PEAK_HBM_GBPS
         out["pmc_basis"] = pj.get("note")

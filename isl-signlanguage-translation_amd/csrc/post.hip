@@ -987,7 +987,7 @@ static int blur_exact_only() {
 template <typename T, bool FUSED, int WR = NMS_SRC_ROWS, int WC = NMS_SRC_COLS>
 static int launch_blur(dim3 grid, hipStream_t s, const T* planes, int H, int W, int words, unsigned long long* mask,
                        double thre, int mode_hand, const MapSrc& m, int nch, const int* live, const int* live_count,
-                       int tiles_x, int tiles_y, const float* bandmax, int* amb) {
+                       int tiles_x, int tiles_y, const float* bandmax, int* amb, bool amb_zeroed = false) {
   const int ex = blur_exact_only();
   if (ex == 1) {
     hipLaunchKernelGGL((blur_nms_kernel<T, FUSED, true, WR, WC>), grid, dim3(256), 0, s, planes, H, W, words, mask,
@@ -995,7 +995,7 @@ static int launch_blur(dim3 grid, hipStream_t s, const T* planes, int H, int W, 
     return hipGetLastError() == hipSuccess ? ISL_OK : ISL_E_HIP;
   }
   int* amb_count = amb;
-  if (hipMemsetAsync(amb_count, 0, sizeof(int), s) != hipSuccess) return ISL_E_HIP;
+  if (!amb_zeroed && hipMemsetAsync(amb_count, 0, sizeof(int), s) != hipSuccess) return ISL_E_HIP;
   hipLaunchKernelGGL((blur_nms_kernel<T, FUSED, false, WR, WC>), grid, dim3(256), 0, s, planes, H, W, words, mask,
                      thre, mode_hand, m, nch, live, live_count, tiles_x, tiles_y, bandmax, amb + 1, amb_count, ex);
   if (hipGetLastError() != hipSuccess) return ISL_E_HIP;
@@ -1432,8 +1432,15 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
 // LDS ballots instead of dependent global loads; the kept rows are written to
 // the record in one pass at the end.
 constexpr int ASM_LDS_ROWS = 256;   // subset rows that fit the LDS table (256 x 27 doubles = 55 KB)
-__global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds) {
-  extern __shared__ double s_subset[];
+// The frame's connections and the candidate scores the merge adds are staged in LDS first, all
+// lanes loading at once (ASM_CONN_CACHE of them; more: read in place): the serial merge then
+// never waits on a global load (it waited on two per connection, ~75 us per 32-frame batch).
+constexpr int ASM_CONN_CACHE = 512;   // x 5 doubles = 20 KB
+__global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, int conn_cap) {
+  extern __shared__ double s_asm[];
+  double* s_subset = s_asm;
+  double* s_conn = s_asm + (in_lds ? (size_t)a.max_rows * (a.njoint + 1) : 0);   // [ASM_CONN_CACHE][5]
+  __shared__ int s_off[32], s_koff[33];
   const int f = blockIdx.x, lane = threadIdx.x;
   char* rec = a.result + (size_t)f * a.lay.record_bytes;
   int* status = (int*)(rec + a.lay.status);
@@ -1446,11 +1453,44 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds) {
   double* subset = in_lds ? s_subset : out;
   if (*status != ISL_OK) return;
   const int RW = a.njoint + 1;   // subset row width
-  int off[32];
-  for (int p = 0, acc = 0; p < a.njoint - 1; ++p) { off[p] = acc; acc += n_peaks[p]; }
+  {
+    // candidate id offsets per part and connection offsets per limb: exclusive scans over lanes
+    int np = lane < a.njoint - 1 ? n_peaks[lane] : 0;
+    int nc = lane < a.nlimbs ? max(n_conns[lane], 0) : 0;
+    int sp = np, sc = nc;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int up = __shfl_up(sp, o), uc = __shfl_up(sc, o);
+      if (lane >= o) {
+        sp += up;
+        sc += uc;
+      }
+    }
+    if (lane < 32) s_off[lane] = sp - np;
+    if (lane < 33) s_koff[lane] = sc - nc;
+  }
+  __syncthreads();
   auto score_of = [&](int part, double id) {
-    return peaks[((size_t)part * a.max_peaks + (int)(id - off[part])) * 3 + 2];   // candidate[id, 2]
+    return peaks[((size_t)part * a.max_peaks + (int)(id - s_off[part])) * 3 + 2];   // candidate[id, 2]
   };
+  const int total = s_koff[a.nlimbs];
+  const bool cached = total <= conn_cap;
+  if (cached) {
+    for (int it = lane; it < total; it += 64) {
+      int k = 0;
+      while (s_koff[k + 1] <= it) ++k;
+      const int A = a.model == ISL_BODY25 ? kLimbs25[k][0] : kLimbsCoco[k][0];
+      const int B = a.model == ISL_BODY25 ? kLimbs25[k][1] : kLimbsCoco[k][1];
+      const double* c = conns + ((size_t)k * a.max_conns + (it - s_koff[k])) * 5;
+      const double idA = c[0], idB = c[1];
+      double* e = s_conn + (size_t)it * 5;
+      e[0] = idA;
+      e[1] = idB;
+      e[2] = c[2];
+      e[3] = score_of(A, idA);
+      e[4] = score_of(B, idB);
+    }
+    __syncthreads();
+  }
   int rows = 0;
   for (int k = 0; k < a.nlimbs; ++k) {
     const int m = n_conns[k];
@@ -1459,8 +1499,9 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds) {
     const int B = a.model == ISL_BODY25 ? kLimbs25[k][1] : kLimbsCoco[k][1];
     const double* cw = conns + (size_t)k * a.max_conns * 5;
     for (int ci = 0; ci < m; ++ci) {
-      const double* c = cw + (size_t)ci * 5;
+      const double* c = cached ? s_conn + (size_t)(s_koff[k] + ci) * 5 : cw + (size_t)ci * 5;
       const double idA = c[0], idB = c[1], sc = c[2];
+      const double sA = cached ? c[3] : 0.0, sB = cached ? c[4] : 0.0;
       // rows j with subset[j][A] == idA or subset[j][B] == idB, in order (body.py:191-196)
       int hit[2] = {-1, -1}, found = 0;
       for (int r0 = 0; r0 < rows; r0 += 64) {
@@ -1490,7 +1531,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds) {
         if (upd && lane == 0) {
           row[B] = idB;
           row[RW - 1] += 1.0;
-          row[RW - 2] += score_of(B, idB) + sc;
+          row[RW - 2] += (cached ? sB : score_of(B, idB)) + sc;
         }
       } else if (found == 2) {
         double* r1 = subset + (size_t)hit[0] * RW;
@@ -1522,7 +1563,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds) {
         } else if (lane == 0) {
           r1[B] = idB;
           r1[RW - 1] += 1.0;
-          r1[RW - 2] += score_of(B, idB) + sc;
+          r1[RW - 2] += (cached ? sB : score_of(B, idB)) + sc;
         }
       } else if (k < a.njoint - 2) {
         if (rows >= a.max_rows) {
@@ -1530,7 +1571,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds) {
           return;
         }
         double* row = subset + (size_t)rows * RW;
-        const double sAB = lane == 0 ? (score_of(A, idA) + score_of(B, idB)) + sc : 0.0;
+        const double sAB = lane == 0 ? (cached ? sA + sB : score_of(A, idA) + score_of(B, idB)) + sc : 0.0;
         for (int q = lane; q < RW; q += 64) row[q] = -1.0;
         __syncthreads();
         if (lane == 0) {
@@ -2534,8 +2575,14 @@ __global__ void __launch_bounds__(CC_NT) hand_cc_kernel(const double* __restrict
   }
 }
 
-__global__ void init_records_kernel(char* result, isl_layout lay, int n, int nlimbs) {
+// (also zeroes the post's two list counters: z0, z1 -- one launch instead of two memsets)
+__global__ void init_records_kernel(char* result, isl_layout lay, int n, int nlimbs, int* z0 = nullptr,
+                                    int* z1 = nullptr) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f == 0) {
+    if (z0) *z0 = 0;
+    if (z1) *z1 = 0;
+  }
   if (f >= n) return;
   char* rec = result + (size_t)f * lay.record_bytes;
   *(int*)(rec + lay.status) = ISL_OK;
@@ -2799,7 +2846,8 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   unsigned char* need = skip2 ? live_mid + up(lmid_bytes) : nullptr;
   bool bm_done = false;
 
-  hipLaunchKernelGGL(init_records_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (char*)d_result, lay, n, nlimbs);
+  hipLaunchKernelGGL(init_records_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (char*)d_result, lay, n, nlimbs,
+                     live_bytes ? live_count : nullptr, amb);   // (amb[0]: the filter's list count)
   PHIP(hipGetLastError());
 
   GroupArgs ga;
@@ -2879,13 +2927,12 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   const int tx = (int)gb.x, tyl = (int)gb.y;
   if (multi) {
     if ((rc = launch_blur<double, false>(gb, s, (const double*)heat, H, W, words, mask, 0.1, 0, MapSrc{}, 0, nullptr,
-                                         nullptr, tx, tyl, nullptr, amb)))
+                                         nullptr, tx, tyl, nullptr, amb, true)))
       return rc;
   } else if (fused) {
     // live-tile list (low-res bound), then the fused blur over live tiles only
     const int n_tiles = (int)(gb.x * gb.y * gb.z);
-    PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));
-    PHIP(hipMemsetAsync(live_count, 0, sizeof(int), s));
+    PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));   // (live_count: zeroed by init_records_kernel)
     const dim3 tl((n_tiles + TL_TILES - 1) / TL_TILES);
     if (wide) {
 #ifdef ISLPOSE_DEV
@@ -2894,7 +2941,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
       PHIP(hipGetLastError());
       if ((rc = launch_blur<float, true, NMS_WSRC_ROWS, NMS_WSRC_COLS>(
                dim3(std::min((n_tiles + 7) / 8 * 8, 256 * 4)), s, (const float*)nullptr, H, W, words, mask, 0.1, 0, fused_src, nparts,
-               live, live_count, tx, tyl, nullptr, amb)))
+               live, live_count, tx, tyl, nullptr, amb, true)))
         return rc;
 #endif
     } else {
@@ -2902,22 +2949,21 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
                          tx, tyl, n_tiles, 0.1, live, live_count);
       PHIP(hipGetLastError());
       if ((rc = launch_blur<float, true>(dim3(std::min((n_tiles + 7) / 8 * 8, 256 * 8)), s, (const float*)nullptr, H, W, words, mask,
-                                         0.1, 0, fused_src, nparts, live, live_count, tx, tyl, nullptr, amb)))
+                                         0.1, 0, fused_src, nparts, live, live_count, tx, tyl, nullptr, amb, true)))
         return rc;
     }
   } else if (bm_done && band_list) {
     // live-tile list (the band maxima), then the blur over live tiles only
     const int n_tiles = (int)(gb.x * gb.y * gb.z);
-    PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));
-    PHIP(hipMemsetAsync(live_count, 0, sizeof(int), s));
+    PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));   // (live_count: zeroed by init_records_kernel)
     hipLaunchKernelGGL(band_live_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, s, (const float*)bandmax, H, W,
                        words, tx, tyl, n_tiles, 0.1, live, live_count, (const unsigned char*)live_mid);
     PHIP(hipGetLastError());
     if ((rc = launch_blur<float, false>(dim3(std::min((n_tiles + 7) / 8 * 8, 256 * 8)), s, (const float*)heat, H, W, words, mask,
-                                        0.1, 0, MapSrc{}, 0, live, live_count, tx, tyl, nullptr, amb)))
+                                        0.1, 0, MapSrc{}, 0, live, live_count, tx, tyl, nullptr, amb, true)))
       return rc;
   } else if ((rc = launch_blur<float, false>(gb, s, (const float*)heat, H, W, words, mask, 0.1, 0, MapSrc{}, 0, nullptr,
-                                             nullptr, tx, tyl, bm_done ? (const float*)bandmax : nullptr, amb))) {
+                                             nullptr, tx, tyl, bm_done ? (const float*)bandmax : nullptr, amb, true))) {
     return rc;
   }
   PHIP(hipGetLastError());
@@ -2947,8 +2993,10 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   hipLaunchKernelGGL(limb_kernel, dim3(nlimbs, n), dim3(256), 0, s, ga);
   PHIP(hipGetLastError());
   const int asm_lds = caps->max_rows <= ASM_LDS_ROWS;
-  hipLaunchKernelGGL(assemble_kernel, dim3(n), dim3(64), asm_lds ? (size_t)caps->max_rows * (njoint + 1) * 8 : 0, s,
-                     ga, asm_lds);
+  // (the connection cache takes what is left of 64 KB of dynamic LDS, up to ASM_CONN_CACHE)
+  const size_t sub_lds = asm_lds ? (size_t)caps->max_rows * (njoint + 1) * 8 : 0;
+  const int conn_cap = (int)std::min<size_t>(ASM_CONN_CACHE, sub_lds < 65536 ? (65536 - sub_lds) / 40 : 0);
+  hipLaunchKernelGGL(assemble_kernel, dim3(n), dim3(64), sub_lds + (size_t)conn_cap * 40, s, ga, asm_lds, conn_cap);
   PHIP(hipGetLastError());
   return ISL_OK;
 }

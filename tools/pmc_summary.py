@@ -21,6 +21,17 @@ import os
 NET_KERNELS = ("conv_mfma", "wino_f23", "maxpool", "conv_x3", "wino_x3")
 
 
+def kclass(k):
+    """Kernel class of a rocprof kernel name: the function name, except that the blur's exact
+    re-run (blur_nms_kernel<T, FUSED, true, ...>) is its own class, blur_nms_exact."""
+    cls = k.split("(")[0].replace("void ", "").split("<")[0].replace("isl::", "")
+    if cls == "blur_nms_kernel" and "<" in k:
+        args = [a.strip() for a in k.split("<", 1)[1].split(">", 1)[0].split(",")]
+        if len(args) >= 3 and args[2] == "true":
+            return "blur_nms_exact"
+    return cls
+
+
 def load(d, name):
     """Per kernel class: summed counter value and number of dispatches; the net's
     kernels are also summed into the class "net_run"."""
@@ -31,7 +42,7 @@ def load(d, name):
         if r["Counter_Name"] != name:
             continue
         k = r["Kernel_Name"]
-        cls = k.split("(")[0].replace("void ", "").split("<")[0].replace("isl::", "")
+        cls = kclass(k)
         v = float(r["Counter_Value"])
         did = r.get("Dispatch_Id", r.get("Correlation_Id", ""))
         out[cls] += v
@@ -46,14 +57,14 @@ def durations(stats_csv):
     """kernel class -> (calls, average ns) from a rocprofv3 --stats kernel_stats.csv."""
     out = {}
     for r in csv.DictReader(open(stats_csv)):
-        k = r["Name"].split("(")[0].replace("void ", "").split("<")[0].replace("isl::", "")
+        k = kclass(r["Name"])
         c, t = out.get(k, (0, 0.0))
         out[k] = (c + int(r["Calls"]), t + float(r["TotalDurationNs"]))
     return {k: (c, t / c) for k, (c, t) in out.items()}
 
 
-POST_KERNELS = ("blur_nms_kernel", "limb_kernel", "tile_live_kernel", "compact_kernel", "assemble_kernel",
-                "resize_sep_kernel")
+POST_KERNELS = ("blur_nms_kernel", "blur_nms_exact", "limb_kernel", "tile_live_kernel", "band_live_kernel",
+                "stage2_need_kernel", "compact_kernel", "assemble_kernel", "resize_sep_kernel")
 
 
 def post_traffic(res, stats_csv, out_path, src):
@@ -63,8 +74,9 @@ def post_traffic(res, stats_csv, out_path, src):
     t = {"source": src, "peak_GBps": 8000.0,
          "note": "per launch (one launch = the post of one bench step, 32 frames): hbm_bytes = FETCH_SIZE x2 (gfx950 "
                  "wide-read correction) + WRITE_SIZE; avg_us = rocprofv3 --stats average of the same kernel in the "
-                 "trace pass of the same command; GBps = hbm_bytes / avg_us. blur_nms_kernel is bound by fp64 VALU "
-                 "work on live tiles (37 fp64 ops per output per pass, scipy's order), not by HBM"}
+                 "trace pass of the same command; GBps = hbm_bytes / avg_us. blur_nms_kernel (the fp32 filter over the "
+                 "live tiles) is bound by the latency of its per-tile phases (window loads, the two passes, the NMS; "
+                 "tools/tile_prof.py), not by HBM; blur_nms_exact re-runs the few undecided tiles in fp64"}
     for k in POST_KERNELS:
         if k in res and k in dur:
             b = res[k]["hbm_bytes_per_launch"]

@@ -15,7 +15,8 @@ rc=$?
 f=$(find $O/trace -name "*kernel_trace.csv" | head -1)
 [ -n "$f" ] && python3 tools/layer_times.py $f > $O/layers.txt
 st=$(find $O/trace -name "*kernel_stats.csv" | head -1)
-[ -n "$st" ] && python3 tools/pmc_summary.py $O/fetch $O/write --steps 4 --out $O/pmc_summary.json --sq $O/sq --stats $st > $O/pmc_summary.txt 2>&1
+[ -n "$st" ] && python3 tools/pmc_summary.py $O/fetch $O/write --steps 4 --out $O/pmc_summary.json --sq $O/sq --stats $st \
+  --traffic-out $O/conv_traffic.json --post-out $O/post_traffic.json > $O/pmc_summary.txt 2>&1
 echo rc=$rc
 python3 -c "
 import json

@@ -895,23 +895,19 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
       const int cx = wd * 64 + lane, x = x0 + cx;
       const float g = rp[wd * 64 + 1];
       const float fu = rp[wd * 64 + 1 - NMS_VC], fd = rp[wd * 64 + 1 + NMS_VC], fl = rp[wd * 64], fr = rp[wd * 64 + 2];
-      bool pk = false, open = false;
-      if (y < H && x < W && (wd == 0 ? wl0 : wd == 1 ? wl1 : wl2)) {
-        const float dt = g - thre_f;
-        bool no = dt <= -eps;                      // surely g < thre
-        open = !no && !(dt > eps);                 // g vs thre inside the margin
-        if (!mode_hand) {
-          // per neighbour q: surely g < q (the pixel is out), or g vs q inside the margin
-          const float d0 = g - (y > 0 ? fu : 0.f);
-          const float d1 = g - (y + 1 < H ? fd : 0.f);
-          const float d2 = g - (x > 0 ? fl : 0.f);
-          const float d3 = g - (x + 1 < W ? fr : 0.f);
-          no = no || d0 < -e2 || d1 < -e2 || d2 < -e2 || d3 < -e2;
-          open = open || !(d0 >= e2) || !(d1 >= e2) || !(d2 >= e2) || !(d3 >= e2);
-        }
-        pk = !no && !open;
-        open = !no && open;
-      }
+      // (branch-free in the neighbours, so that the five reads are not sunk behind a branch)
+      const float dt = g - thre_f;
+      const float d0 = g - (y > 0 ? fu : 0.f), d1 = g - (y + 1 < H ? fd : 0.f);
+      const float d2 = g - (x > 0 ? fl : 0.f), d3 = g - (x + 1 < W ? fr : 0.f);
+      const float dmin = fminf(fminf(d0, d1), fminf(d2, d3));   // (no NaN: finite planes)
+      const bool nb = !mode_hand;
+      // surely g < thre, or surely g < a neighbour (the pixel is out)
+      const bool no = dt <= -eps || (nb && dmin < -e2);
+      // g vs thre, or g vs a neighbour, inside the margin
+      const bool inm = !(dt > eps) || (nb && !(dmin >= e2));
+      const bool valid = y < H && x < W && (wd == 0 ? wl0 : wd == 1 ? wl1 : wl2);
+      const bool pk = valid && !no && !inm;
+      const bool open = valid && !no && inm;
       wv[wd] = __ballot(pk);
       any_open = any_open || __ballot(open) != 0;
     }

@@ -1489,8 +1489,10 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
   }
   int rows = 0;
   for (int k = 0; k < a.nlimbs; ++k) {
-    const int m = n_conns[k];
-    if (m < 0) continue;                 // special_k
+    // (the staged counts: special_k's -1 is 0 there, and a limb without connections does nothing
+    // either way -- no dependent global load per limb)
+    const int m = s_koff[k + 1] - s_koff[k];
+    if (m <= 0) continue;                // special_k
     const int A = a.model == ISL_BODY25 ? kLimbs25[k][0] : kLimbsCoco[k][0];
     const int B = a.model == ISL_BODY25 ? kLimbs25[k][1] : kLimbsCoco[k][1];
     const double* cw = conns + (size_t)k * a.max_conns * 5;

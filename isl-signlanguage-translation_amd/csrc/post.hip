@@ -1500,14 +1500,23 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
       const double* c = cached ? s_conn + (size_t)(s_koff[k] + ci) * 5 : cw + (size_t)ci * 5;
       const double idA = c[0], idB = c[1], sc = c[2];
       const double sA = cached ? c[3] : 0.0, sB = cached ? c[4] : 0.0;
-      // rows j with subset[j][A] == idA or subset[j][B] == idB, in order (body.py:191-196)
+      // rows j with subset[j][A] == idA or subset[j][B] == idB, in order (body.py:191-196); the
+      // scan also reads the first 64 rows' [B], count and score, which the one-row update takes
+      // by lane exchange instead of dependent LDS reads
       int hit[2] = {-1, -1}, found = 0;
+      double rb = 0.0, rcnt = 0.0, rsc = 0.0;
       for (int r0 = 0; r0 < rows; r0 += 64) {
         const int r = r0 + lane;
         bool hitr = false;
         if (r < rows) {
           const double* row = subset + (size_t)r * RW;
-          hitr = row[A] == idA || row[B] == idB;
+          const double ra = row[A], rbb = row[B];
+          if (r0 == 0) {
+            rb = rbb;
+            rcnt = row[RW - 1];
+            rsc = row[RW - 2];
+          }
+          hitr = ra == idA || rbb == idB;
         }
         unsigned long long mask = __ballot(hitr);
         while (mask && found < 3) {
@@ -1524,12 +1533,22 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
       }
       if (found == 1) {
         double* row = subset + (size_t)hit[0] * RW;
-        const bool upd = row[B] != idB;
-        __syncthreads();
-        if (upd && lane == 0) {
-          row[B] = idB;
-          row[RW - 1] += 1.0;
-          row[RW - 2] += (cached ? sB : score_of(B, idB)) + sc;
+        if (hit[0] < 64) {
+          // (a single wave: its LDS / global operations on the table are ordered, no barrier)
+          const double ob = __shfl(rb, hit[0]), oc = __shfl(rcnt, hit[0]), os = __shfl(rsc, hit[0]);
+          if (ob != idB && lane == 0) {
+            row[B] = idB;
+            row[RW - 1] = oc + 1.0;
+            row[RW - 2] = os + ((cached ? sB : score_of(B, idB)) + sc);
+          }
+        } else {
+          const bool upd = row[B] != idB;
+          __syncthreads();
+          if (upd && lane == 0) {
+            row[B] = idB;
+            row[RW - 1] += 1.0;
+            row[RW - 2] += (cached ? sB : score_of(B, idB)) + sc;
+          }
         }
       } else if (found == 2) {
         double* r1 = subset + (size_t)hit[0] * RW;
@@ -1580,7 +1599,9 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
         }
         ++rows;
       }
-      __syncthreads();
+      // (the LDS table: one wave's LDS operations execute in order, so the next connection's
+      // scan sees these writes without a barrier; the global table keeps it)
+      if (!in_lds) __syncthreads();
     }
   }
   // prune (body.py:227-231): keep rows with count >= 4 and mean score >= 0.4, in order

@@ -475,9 +475,16 @@ __device__ unsigned long long* g_tile_prof = nullptr;
       g_tile_prof[tix * 10 + (k)] = (v);                                                          \
     }                                                                                             \
   } while (0)
+#define ASTAMP(k)                                                        \
+  do {                                                                   \
+    if (g_tile_prof && lane == 0) g_tile_prof[(size_t)f * 10 + (k)] = clock64(); \
+  } while (0)
 #else
 #define TPROF(k, v) \
   do {              \
+  } while (0)
+#define ASTAMP(k) \
+  do {            \
   } while (0)
 #endif
 
@@ -1447,6 +1454,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
   const double* conns = (const double*)(rec + a.lay.conns);
   double* out = (double*)(rec + a.lay.subset);
   double* subset = in_lds ? s_subset : out;
+  ASTAMP(0);
   if (*status != ISL_OK) return;
   const int RW = a.njoint + 1;   // subset row width
   {
@@ -1465,6 +1473,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
     if (lane < 33) s_koff[lane] = sc - nc;
   }
   __syncthreads();
+  ASTAMP(1);
   auto score_of = [&](int part, double id) {
     return peaks[((size_t)part * a.max_peaks + (int)(id - s_off[part])) * 3 + 2];   // candidate[id, 2]
   };
@@ -1487,6 +1496,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
     }
     __syncthreads();
   }
+  ASTAMP(2);
   int rows = 0;
   for (int k = 0; k < a.nlimbs; ++k) {
     // (the staged counts: special_k's -1 is 0 there, and a limb without connections does nothing
@@ -1604,6 +1614,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
       if (!in_lds) __syncthreads();
     }
   }
+  ASTAMP(3);
   // prune (body.py:227-231): keep rows with count >= 4 and mean score >= 0.4, in order
   int w = 0;
   for (int r0 = 0; r0 < rows; r0 += 64) {
@@ -1635,6 +1646,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
     w += __builtin_popcountll(km);
   }
   if (lane == 0) *n_rows = w;
+  ASTAMP(4);
 }
 
 // ---------------------------------------------------------------------------

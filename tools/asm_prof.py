@@ -1,0 +1,36 @@
+"""Phase stamps of assemble_kernel (development build, ISLPOSE_TILE_PROF=1): shader cycles
+from entry to after the count scans, after the connection staging, after the merge loop, and
+to the end, for the Mode R post of --batch designed 3-person frames (dev tool)."""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("ISLPOSE_LIB", os.path.join(REPO, "tools", "libislpose_dev.so"))
+sys.path.insert(0, os.path.join(REPO, "isl-signlanguage-translation_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from islpose import synth  # noqa: E402
+from islpose import runtime as rt  # noqa: E402
+from islpose.body import BodyEstimator, scale_geometry  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+H, W = 368, 656
+est = BodyEstimator(synth.synth_weights(0), "body25")
+geoms = [g[1:] for g in scale_geometry(H, W, (0.5,))]
+nh, nw = geoms[0][0] // 8, geoms[0][1] // 8
+des = [synth.designed_pose_maps(nh, nw, 3, seed=i) for i in range(B)]
+paf = torch.from_numpy(np.stack([p for p, _ in des])).cuda()
+heat = torch.from_numpy(np.stack([h for _, h in des])).cuda()
+est.post(B, H, W, geoms, [paf], [heat])
+os.environ["ISLPOSE_TILE_PROF"] = "1"
+est.post(B, H, W, geoms, [paf], [heat])
+torch.cuda.synchronize()
+tiles = ((W + 191) // 192) * ((H + 15) // 16) * B * 25
+buf = np.zeros((tiles, 10), np.uint64)
+f = rt.lib().isl_dev_tile_prof
+f.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+rt.check(f(buf.ctypes.data, tiles), "isl_dev_tile_prof")
+b = buf[:B, :5].astype(np.int64)
+d = np.diff(b, axis=1)
+print("assemble phases (cycles, mean over frames): scans %.0f staging %.0f merge %.0f prune %.0f" % tuple(d.mean(0)))

@@ -1439,7 +1439,12 @@ constexpr int ASM_LDS_ROWS = 256;   // subset rows that fit the LDS table (256 x
 // lanes loading at once (ASM_CONN_CACHE of them; more: read in place): the serial merge then
 // never waits on a global load (it waited on two per connection, ~75 us per 32-frame batch).
 constexpr int ASM_CONN_CACHE = 512;   // x 5 doubles = 20 KB
-__global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, int conn_cap) {
+// IN_LDS: the subset table in LDS (a template parameter, so that its accesses are ds_* rather
+// than flat instructions: a runtime choice of the table's address space made every access a
+// flat load / store with global latency, ~1600 cycles per connection of the serial merge)
+template <bool IN_LDS>
+__global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int conn_cap) {
+  constexpr bool in_lds = IN_LDS;
   extern __shared__ double s_asm[];
   double* s_subset = s_asm;
   double* s_conn = s_asm + (in_lds ? (size_t)a.max_rows * (a.njoint + 1) : 0);   // [ASM_CONN_CACHE][5]
@@ -1453,7 +1458,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
   const double* peaks = (const double*)(rec + a.lay.peaks);
   const double* conns = (const double*)(rec + a.lay.conns);
   double* out = (double*)(rec + a.lay.subset);
-  double* subset = in_lds ? s_subset : out;
+  double* subset = IN_LDS ? s_subset : out;
   ASTAMP(0);
   if (*status != ISL_OK) return;
   const int RW = a.njoint + 1;   // subset row width
@@ -1498,6 +1503,9 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
   }
   ASTAMP(2);
   int rows = 0;
+  // the merge, instantiated per connection source (cache / record) so that every access is typed
+  auto merge = [&](auto cache_tag) -> bool {
+  constexpr bool CACHED = decltype(cache_tag)::value;
   for (int k = 0; k < a.nlimbs; ++k) {
     // (the staged counts: special_k's -1 is 0 there, and a limb without connections does nothing
     // either way -- no dependent global load per limb)
@@ -1507,9 +1515,21 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
     const int B = a.model == ISL_BODY25 ? kLimbs25[k][1] : kLimbsCoco[k][1];
     const double* cw = conns + (size_t)k * a.max_conns * 5;
     for (int ci = 0; ci < m; ++ci) {
-      const double* c = cached ? s_conn + (size_t)(s_koff[k] + ci) * 5 : cw + (size_t)ci * 5;
-      const double idA = c[0], idB = c[1], sc = c[2];
-      const double sA = cached ? c[3] : 0.0, sB = cached ? c[4] : 0.0;
+      // (two typed branches, so that the cached reads are ds_* and not flat loads)
+      double idA, idB, sc, sA = 0.0, sB = 0.0;
+      if constexpr (CACHED) {
+        const double* c = s_conn + (size_t)(s_koff[k] + ci) * 5;
+        idA = c[0];
+        idB = c[1];
+        sc = c[2];
+        sA = c[3];
+        sB = c[4];
+      } else {
+        const double* c = cw + (size_t)ci * 5;
+        idA = c[0];
+        idB = c[1];
+        sc = c[2];
+      }
       // rows j with subset[j][A] == idA or subset[j][B] == idB, in order (body.py:191-196); the
       // scan also reads the first 64 rows' [B], count and score, which the one-row update takes
       // by lane exchange instead of dependent LDS reads
@@ -1539,7 +1559,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
       }
       if (found == 3) {                  // body.py:196 IndexError
         if (lane == 0) *status = ISL_E_INDEX;
-        return;
+        return false;
       }
       if (found == 1) {
         double* row = subset + (size_t)hit[0] * RW;
@@ -1549,7 +1569,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
           if (ob != idB && lane == 0) {
             row[B] = idB;
             row[RW - 1] = oc + 1.0;
-            row[RW - 2] = os + ((cached ? sB : score_of(B, idB)) + sc);
+            row[RW - 2] = os + ((CACHED ? sB : score_of(B, idB)) + sc);
           }
         } else {
           const bool upd = row[B] != idB;
@@ -1557,7 +1577,7 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
           if (upd && lane == 0) {
             row[B] = idB;
             row[RW - 1] += 1.0;
-            row[RW - 2] += (cached ? sB : score_of(B, idB)) + sc;
+            row[RW - 2] += (CACHED ? sB : score_of(B, idB)) + sc;
           }
         }
       } else if (found == 2) {
@@ -1590,15 +1610,15 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
         } else if (lane == 0) {
           r1[B] = idB;
           r1[RW - 1] += 1.0;
-          r1[RW - 2] += (cached ? sB : score_of(B, idB)) + sc;
+          r1[RW - 2] += (CACHED ? sB : score_of(B, idB)) + sc;
         }
       } else if (k < a.njoint - 2) {
         if (rows >= a.max_rows) {
           if (lane == 0) *status = ISL_E_CAPACITY;
-          return;
+          return false;
         }
         double* row = subset + (size_t)rows * RW;
-        const double sAB = lane == 0 ? (cached ? sA + sB : score_of(A, idA) + score_of(B, idB)) + sc : 0.0;
+        const double sAB = lane == 0 ? (CACHED ? sA + sB : score_of(A, idA) + score_of(B, idB)) + sc : 0.0;
         for (int q = lane; q < RW; q += 64) row[q] = -1.0;
         __syncthreads();
         if (lane == 0) {
@@ -1614,6 +1634,9 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int in_lds, i
       if (!in_lds) __syncthreads();
     }
   }
+  return true;
+  };
+  if (!(cached ? merge(std::true_type{}) : merge(std::false_type{}))) return;
   ASTAMP(3);
   // prune (body.py:227-231): keep rows with count >= 4 and mean score >= 0.4, in order
   int w = 0;
@@ -3027,7 +3050,10 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   // (the connection cache takes what is left of 64 KB of dynamic LDS, up to ASM_CONN_CACHE)
   const size_t sub_lds = asm_lds ? (size_t)caps->max_rows * (njoint + 1) * 8 : 0;
   const int conn_cap = (int)std::min<size_t>(ASM_CONN_CACHE, sub_lds < 65536 ? (65536 - sub_lds) / 40 : 0);
-  hipLaunchKernelGGL(assemble_kernel, dim3(n), dim3(64), sub_lds + (size_t)conn_cap * 40, s, ga, asm_lds, conn_cap);
+  if (asm_lds)
+    hipLaunchKernelGGL(assemble_kernel<true>, dim3(n), dim3(64), sub_lds + (size_t)conn_cap * 40, s, ga, conn_cap);
+  else
+    hipLaunchKernelGGL(assemble_kernel<false>, dim3(n), dim3(64), (size_t)conn_cap * 40, s, ga, conn_cap);
   PHIP(hipGetLastError());
   return ISL_OK;
 }

@@ -345,8 +345,9 @@ def gpu_main(args, rank, local, world):
             torch.distributed.barrier()
         t0 = time.perf_counter()
         # the net / post window events sit on the step before the last: an un-instrumented
-        # step whose conv chain replays its graph like the others (the instrumented
-        # step runs eager); with a single timed step they share it
+        # step like the others (the instrumented step differs; with graph replay
+        # opted in, ISLPOSE_NET_GRAPH=1, it is the one eager step); with a single timed step
+        # they share it
         win = steps - 2 if steps >= 2 else steps - 1
         for i in range(steps):
             # per-op HIP events (each lane's stream) on the last timed step only: an event

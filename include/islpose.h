@@ -143,13 +143,14 @@ int isl_net_get_algo(const isl_net* net);
 int isl_net_set_split_k(isl_net* net, int mode);
 
 /* Graph replay of the conv chain (not in the reference: it replaces the per-op launches of
- * its torch module, src/model.py:171-207, with one HIP graph launch).  on = 1 (default):
+ * its torch module, src/model.py:171-207, with one HIP graph launch).  on = 1:
  * the first isl_net_run / isl_net_forward of a run key (batch size, K-range mode, conv
  * algorithm, ISLPOSE_* environment) on an arena runs eagerly, the second captures the
  * launches on a private stream and launches the graph on the caller's stream, later runs
  * replay it -- the same kernels with the same arguments, the same bits.  Timed runs
  * (isl_net_set_timing) stay eager; weight uploads and workspace growth drop the graphs.
- * on = 0: every run eager.  Env ISLPOSE_NET_GRAPH=0 turns replay off process-wide. */
+ * on = 0 (default; replay measured level at batch 32 and slower at batch 1): every run
+ * eager.  Env ISLPOSE_NET_GRAPH=0|1 turns replay off / on process-wide. */
 int isl_net_set_graph(isl_net* net, int on);
 
 /* Range guard of ISL_ALGO_X3: waits for the device, returns ISL_E_RANGE if any

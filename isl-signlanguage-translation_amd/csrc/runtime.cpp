@@ -267,8 +267,9 @@ struct isl_net {
   bool timing = false;
   std::vector<TimedRun> timed;
   std::vector<int> op_variant;   // per op of the last run: x3_variant_code, -1 pool skipped (vin), 0 other
-  // graph replay of the conv chain (isl_net_set_graph; env ISLPOSE_NET_GRAPH=0 turns it off)
-  int graph = 1;
+  // graph replay of the conv chain (isl_net_set_graph; off by default: measured level at batch 32
+  // and 2.5 % slower at batch 1 in round 4, profiles/r04/r4v; env ISLPOSE_NET_GRAPH=0|1 overrides)
+  int graph = 0;
   bool capturing = false;
   hipStream_t cap_stream = nullptr;
   // conv algorithm (ISL_ALGO_*) and the split-fp16 range flag (isl_net_check)
@@ -1348,8 +1349,8 @@ constexpr size_t kGraphSeenCap = 64;
 
 static bool graph_enabled(const isl_net* net) {
   const char* e = getenv("ISLPOSE_NET_GRAPH");
-  if (e && e[0] == '0') return false;
-  return net->graph && !net->timing && !fold_enabled();
+  const bool on = e && (e[0] == '0' || e[0] == '1') ? e[0] == '1' : net->graph != 0;
+  return on && !net->timing && !fold_enabled();
 }
 
 static int run_ops(isl_net* net, hipStream_t s) {

@@ -282,7 +282,7 @@ class Net:
 
     def set_graph(self, on: bool):
         """Replay the conv chain as a HIP graph after its first runs (isl_net_set_graph;
-        default on, env ISLPOSE_NET_GRAPH=0 turns it off): the same kernels and bits, without
+        default off, env ISLPOSE_NET_GRAPH=0|1 overrides): the same kernels and bits, without
         the per-launch host cost that bounds batch-1 frames."""
         check(lib().isl_net_set_graph(self.h, 1 if on else 0), "isl_net_set_graph")
 

@@ -455,7 +455,7 @@ def test_x3_deep_small_grids_bit_identical(net25, n, monkeypatch):
 
 @pytest.mark.parametrize("n", [1, 4])
 def test_graph_replay_bit_identical(w25, n, monkeypatch):
-    """The conv chain replayed as a HIP graph (isl_net_set_graph, default on): the first run
+    """The conv chain replayed as a HIP graph (isl_net_set_graph, opt-in): the first run
     of a key is eager, the second captures, later runs replay -- every run's maps equal the
     eager net's bit for bit, the op variants are those of the eager run, a changed ISLPOSE_*
     switch is a new key, and new weights drop the captured launches (their scales are kernel
@@ -466,6 +466,7 @@ def test_graph_replay_bit_identical(w25, n, monkeypatch):
     eager.set_graph(False)
     g = rt.Net(rt.ISL_BODY25)
     g.load_weights(w25)
+    g.set_graph(True)
     xs = [torch.from_numpy(_inputs(n, 184, 328, seed=300 + k)).cuda() for k in range(4)]
     ref = [eager.forward(x) for x in xs]
     var0 = eager.op_variants()
@@ -514,6 +515,7 @@ def test_graph_drop_waits_for_queued_replays(w25):
     maps of the last forward equal an eager net's on the new weights."""
     g = rt.Net(rt.ISL_BODY25)
     g.load_weights(w25)
+    g.set_graph(True)
     s = torch.cuda.Stream()
     x = torch.from_numpy(_inputs(2, 184, 328, seed=17)).cuda()
     o0 = torch.empty((2, 52, 23, 41), device="cuda")

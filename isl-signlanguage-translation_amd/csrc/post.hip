@@ -783,6 +783,14 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
     const int xa = reflect_idx(x0 - 1 - NMS_R + 2 * cp, W), xb = reflect_idx(x0 - NMS_R + 2 * cp, W);
     const T* src = planes + (size_t)plane * H * W;
     double ma = 0.0, mb = 0.0;
+    // fused: the 4 stage rows a window row combines (fused_value's taps) move every few rows
+    // (strong upsampling), so the column pair's 8 values are re-read from s_hz only when the
+    // row's taps change -- the taps are wave-uniform, the branch scalar
+    const int rowlen = FUSED ? m.dw * m.cn : 0, fch = FUSED ? plane % nch : 0;
+    const bool sva = FUSED && xa * m.cn + fch < rowlen - rowlen % 4;
+    const bool svb = FUSED && xb * m.cn + fch < rowlen - rowlen % 4;
+    int py0 = -1, py1 = -1, py2 = -1, py3 = -1;
+    float ha0 = 0.f, ha1 = 0.f, ha2 = 0.f, ha3 = 0.f, hb0 = 0.f, hb1 = 0.f, hb2 = 0.f, hb3 = 0.f;
 #pragma unroll
     for (int k = 0; k < NMS_VH + 2 * NMS_R; ++k) {
       const int r = vh * NMS_VH + k;
@@ -794,8 +802,27 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
         va = row[xa];
         vb = row[xb];
       } else {
-        va = fused_value(m, plane % nch, s_hz, s_ti, s_tb, r, 2 * cp, xa);
-        vb = fused_value(m, plane % nch, s_hz, s_ti, s_tb, r, 2 * cp + 1, xb);
+        const int4 t4 = s_ti[r];
+        const int y0t = __builtin_amdgcn_readfirstlane(t4.x), y1t = __builtin_amdgcn_readfirstlane(t4.y);
+        const int y2t = __builtin_amdgcn_readfirstlane(t4.z), y3t = __builtin_amdgcn_readfirstlane(t4.w);
+        if (y0t != py0 || y1t != py1 || y2t != py2 || y3t != py3) {
+          ha0 = s_hz[y0t][2 * cp];
+          hb0 = s_hz[y0t][2 * cp + 1];
+          ha1 = s_hz[y1t][2 * cp];
+          hb1 = s_hz[y1t][2 * cp + 1];
+          ha2 = s_hz[y2t][2 * cp];
+          hb2 = s_hz[y2t][2 * cp + 1];
+          ha3 = s_hz[y3t][2 * cp];
+          hb3 = s_hz[y3t][2 * cp + 1];
+          py0 = y0t;
+          py1 = y1t;
+          py2 = y2t;
+          py3 = y3t;
+        }
+        const float4 be = s_tb[r];
+        // resize_sep_kernel's vertical combine (VResizeCubicVec_32f body / scalar tail)
+        va = sva ? ha0 * be.x + (ha1 * be.y + (ha2 * be.z + ha3 * be.w)) : ((ha0 * be.x + ha1 * be.y) + ha2 * be.z) + ha3 * be.w;
+        vb = svb ? hb0 * be.x + (hb1 * be.y + (hb2 * be.z + hb3 * be.w)) : ((hb0 * be.x + hb1 * be.y) + hb2 * be.z) + hb3 * be.w;
       }
       a[k] = f2v{(float)va, (float)vb};
       ma = fmax(ma, fabs((double)va));

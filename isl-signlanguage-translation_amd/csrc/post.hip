@@ -783,6 +783,7 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
     const int xa = reflect_idx(x0 - 1 - NMS_R + 2 * cp, W), xb = reflect_idx(x0 - NMS_R + 2 * cp, W);
     const T* src = planes + (size_t)plane * H * W;
     double ma = 0.0, mb = 0.0;
+    float mfa = 0.f, mfb = 0.f;
     // fused: the 4 stage rows a window row combines (fused_value's taps) move every few rows
     // (strong upsampling), so the column pair's 8 values are re-read from s_hz only when the
     // row's taps change -- the taps are wave-uniform, the branch scalar
@@ -825,11 +826,20 @@ __device__ __forceinline__ void blur_tile_filter(const T* __restrict__ planes, i
         vb = svb ? hb0 * be.x + (hb1 * be.y + (hb2 * be.z + hb3 * be.w)) : ((hb0 * be.x + hb1 * be.y) + hb2 * be.z) + hb3 * be.w;
       }
       a[k] = f2v{(float)va, (float)vb};
-      ma = fmax(ma, fabs((double)va));
-      mb = fmax(mb, fabs((double)vb));
+      if constexpr (sizeof(T) == 4) {   // (the max of fp32 magnitudes is exact in fp32)
+        mfa = fmaxf(mfa, fabsf((float)va));
+        mfb = fmaxf(mfb, fabsf((float)vb));
+      } else {
+        ma = fmax(ma, fabs((double)va));
+        mb = fmax(mb, fabs((double)vb));
+      }
       // fp64 planes: at most 11 rows' loads in flight (all 33 pairs of doubles hoisted spill)
       if constexpr (sizeof(T) == 8)
         if (k % 11 == 10) __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (sizeof(T) == 4) {
+      ma = (double)mfa;
+      mb = (double)mfb;
     }
     s_cmax[vh][2 * cp] = ma;
     s_cmax[vh][2 * cp + 1] = mb;

@@ -475,9 +475,10 @@ __device__ unsigned long long* g_tile_prof = nullptr;
       g_tile_prof[tix * 10 + (k)] = (v);                                                          \
     }                                                                                             \
   } while (0)
-#define ASTAMP(k)                                                        \
-  do {                                                                   \
-    if (g_tile_prof && lane == 0) g_tile_prof[(size_t)f * 10 + (k)] = clock64(); \
+__device__ unsigned long long* g_asm_prof = nullptr;   // assemble_kernel phases: 8 u64 per frame
+#define ASTAMP(k)                                                       \
+  do {                                                                  \
+    if (g_asm_prof && lane == 0) g_asm_prof[(size_t)f * 8 + (k)] = clock64(); \
   } while (0)
 #else
 #define TPROF(k, v) \
@@ -2840,12 +2841,34 @@ static void tile_prof_arm(size_t tiles, hipStream_t s) {
   }
   (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_tile_prof), &p, sizeof(p), 0, hipMemcpyHostToDevice, s);
 }
+// ISLPOSE_ASM_PROF=1 (development build): assemble_kernel stamps its phases per frame
+static unsigned long long* g_asm_buf = nullptr;
+static size_t g_asm_frames = 0;
+static void asm_prof_arm(size_t frames, hipStream_t s) {
+  const char* e = getenv("ISLPOSE_ASM_PROF");
+  unsigned long long* p = nullptr;
+  if (e && e[0] == '1') {
+    if (frames > g_asm_frames) {
+      if (g_asm_buf) (void)hipFree(g_asm_buf);
+      g_asm_buf = nullptr;
+      if (hipMalloc(&g_asm_buf, frames * 8 * 8) != hipSuccess) g_asm_buf = nullptr;
+      g_asm_frames = g_asm_buf ? frames : 0;
+    }
+    p = g_asm_buf;
+  }
+  (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_asm_prof), &p, sizeof(p), 0, hipMemcpyHostToDevice, s);
+}
+extern "C" int isl_dev_asm_prof(void* host, size_t frames) {
+  if (!g_asm_buf || frames > g_asm_frames) return ISL_E_ARG;
+  return hipMemcpy(host, g_asm_buf, frames * 8 * 8, hipMemcpyDeviceToHost) == hipSuccess ? ISL_OK : ISL_E_HIP;
+}
 extern "C" int isl_dev_tile_prof(void* host, size_t tiles) {
   if (!g_prof_buf || tiles > g_prof_tiles) return ISL_E_ARG;
   return hipMemcpy(host, g_prof_buf, tiles * 10 * 8, hipMemcpyDeviceToHost) == hipSuccess ? ISL_OK : ISL_E_HIP;
 }
 #else
 static void tile_prof_arm(size_t, hipStream_t) {}
+static void asm_prof_arm(size_t, hipStream_t) {}
 #endif
 
 extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, const isl_scale_geom* geom,
@@ -3087,6 +3110,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   // (the connection cache takes what is left of 64 KB of dynamic LDS, up to ASM_CONN_CACHE)
   const size_t sub_lds = asm_lds ? (size_t)caps->max_rows * (njoint + 1) * 8 : 0;
   const int conn_cap = (int)std::min<size_t>(ASM_CONN_CACHE, sub_lds < 65536 ? (65536 - sub_lds) / 40 : 0);
+  asm_prof_arm((size_t)n, s);
   if (asm_lds)
     hipLaunchKernelGGL(assemble_kernel<true>, dim3(n), dim3(64), sub_lds + (size_t)conn_cap * 40, s, ga, conn_cap);
   else

@@ -1,4 +1,4 @@
-"""Phase stamps of assemble_kernel (development build, ISLPOSE_TILE_PROF=1): shader cycles
+"""Phase stamps of assemble_kernel (development build, ISLPOSE_ASM_PROF=1): shader cycles
 from entry to after the count scans, after the connection staging, after the merge loop, and
 to the end, for the Mode R post of --batch designed 3-person frames (dev tool)."""
 import ctypes
@@ -23,14 +23,13 @@ des = [synth.designed_pose_maps(nh, nw, 3, seed=i) for i in range(B)]
 paf = torch.from_numpy(np.stack([p for p, _ in des])).cuda()
 heat = torch.from_numpy(np.stack([h for _, h in des])).cuda()
 est.post(B, H, W, geoms, [paf], [heat])
-os.environ["ISLPOSE_TILE_PROF"] = "1"
+os.environ["ISLPOSE_ASM_PROF"] = "1"
 est.post(B, H, W, geoms, [paf], [heat])
 torch.cuda.synchronize()
-tiles = ((W + 191) // 192) * ((H + 15) // 16) * B * 25
-buf = np.zeros((tiles, 10), np.uint64)
-f = rt.lib().isl_dev_tile_prof
+buf = np.zeros((B, 8), np.uint64)
+f = rt.lib().isl_dev_asm_prof
 f.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-rt.check(f(buf.ctypes.data, tiles), "isl_dev_tile_prof")
+rt.check(f(buf.ctypes.data, B), "isl_dev_asm_prof")
 b = buf[:B, :5].astype(np.int64)
 d = np.diff(b, axis=1)
 print("assemble phases (cycles, mean over frames): scans %.0f staging %.0f merge %.0f prune %.0f" % tuple(d.mean(0)))

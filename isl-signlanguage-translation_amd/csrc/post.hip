@@ -1386,9 +1386,12 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
     *xi = (int)rint(sx);
     *yi = (int)rint(sy);
   };
-  auto score_of = [&](int p, double sum, int cnt, double norm) {
+  auto score_val = [&](double sum, double norm) {
     const double prior = 0.5 * (double)a.H / norm - 1.0;
-    const double score = sum / 10.0 + (0.0 < prior ? 0.0 : prior);
+    return sum / 10.0 + (0.0 < prior ? 0.0 : prior);
+  };
+  auto score_of = [&](int p, double sum, int cnt, double norm) {
+    const double score = score_val(sum, norm);
     pscore[p] = score;
     pkeep[p] = (cnt > 8 && score > 0.0) ? 1 : 0;
   };
@@ -1402,6 +1405,11 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
       point(it / 10, it % 10, &ux, &uy, &nr, &xi, &yi);
       s_item[it] = paf_value(a, f, mx, yi, xi) * ux + paf_value(a, f, my, yi, xi) * uy;
     }
+    // (these pairs' scores, keep flags, rank order and used flags live in LDS: the rank sort and
+    // the serial greedy below then wait on no global load)
+    __shared__ double s_ps[LIMB_ITEMS / 10];
+    __shared__ int s_pk[LIMB_ITEMS / 10], s_or[LIMB_ITEMS / 10];
+    __shared__ unsigned char s_ua[LIMB_ITEMS / 10], s_ub[LIMB_ITEMS / 10];
     __syncthreads();
     for (int p = tid; p < np; p += 256) {
       double sum = 0.0;
@@ -1414,8 +1422,45 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
       double ux, uy, nr;
       int xi, yi;
       point(p, 0, &ux, &uy, &nr, &xi, &yi);
-      score_of(p, sum, cnt, nr);
+      const double score = score_val(sum, nr);
+      s_ps[p] = score;
+      s_pk[p] = (cnt > 8 && score > 0.0) ? 1 : 0;
     }
+    for (int i = tid; i < nA; i += 256) s_ua[i] = 0;   // (nA, nB <= np <= LIMB_ITEMS / 10)
+    for (int j = tid; j < nB; j += 256) s_ub[j] = 0;
+    __syncthreads();
+    // stable descending sort of the kept pairs (sorted(..., reverse=True)): rank = #(better)
+    for (int p = tid; p < np; p += 256) {
+      if (!s_pk[p]) continue;
+      const double sp = s_ps[p];
+      int rank = 0;
+      for (int q = 0; q < np; ++q)
+        if (s_pk[q] && (s_ps[q] > sp || (s_ps[q] == sp && q < p))) ++rank;
+      s_or[rank] = p;
+      atomicAdd(&s_nkeep, 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double* cw = conns + (size_t)k * a.max_conns * 5;
+      const int lim = nA < nB ? nA : nB;
+      int m = 0;
+      for (int r = 0; r < s_nkeep && m < lim; ++r) {
+        const int p = s_or[r];
+        const int i = p / nB, j = p - i * nB;
+        if (s_ua[i] || s_ub[j]) continue;
+        s_ua[i] = s_ub[j] = 1;
+        if (m >= a.max_conns) { atomicExch(status, ISL_E_CAPACITY); break; }
+        double* c = cw + (size_t)m * 5;
+        c[0] = (double)(s_offA + i);
+        c[1] = (double)(s_offB + j);
+        c[2] = s_ps[p];
+        c[3] = (double)i;
+        c[4] = (double)j;
+        ++m;
+      }
+      n_conns[k] = m;
+    }
+    return;
   } else {
     for (int p = tid; p < np; p += 256) {
       double sum = 0.0, nr = 0.0;

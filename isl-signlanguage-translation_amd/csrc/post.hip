@@ -2712,14 +2712,16 @@ __global__ void __launch_bounds__(CC_NT) hand_cc_kernel(const double* __restrict
   }
 }
 
-// (also zeroes the post's two list counters: z0, z1 -- one launch instead of two memsets)
+// (also zeroes the post's two list counters z0, z1 and z16 16-byte words at zb -- one launch
+// instead of three memsets)
 __global__ void init_records_kernel(char* result, isl_layout lay, int n, int nlimbs, int* z0 = nullptr,
-                                    int* z1 = nullptr) {
+                                    int* z1 = nullptr, uint4* zb = nullptr, long long z16 = 0) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f == 0) {
     if (z0) *z0 = 0;
     if (z1) *z1 = 0;
   }
+  for (long long i = f; i < z16; i += (long long)gridDim.x * blockDim.x) zb[i] = make_uint4(0u, 0u, 0u, 0u);
   if (f >= n) return;
   char* rec = result + (size_t)f * lay.record_bytes;
   *(int*)(rec + lay.status) = ISL_OK;
@@ -3005,8 +3007,11 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   unsigned char* need = skip2 ? live_mid + up(lmid_bytes) : nullptr;
   bool bm_done = false;
 
-  hipLaunchKernelGGL(init_records_kernel, dim3((n + 63) / 64), dim3(64), 0, s, (char*)d_result, lay, n, nlimbs,
-                     live_bytes ? live_count : nullptr, amb);   // (amb[0]: the filter's list count)
+  // (amb[0]: the filter's list count; need: zeroed here for stage2_need_kernel)
+  const long long need16 = (long long)(up(need_bytes) / 16);
+  hipLaunchKernelGGL(init_records_kernel, dim3(std::max<long long>((n + 63) / 64, std::min<long long>((need16 + 255) / 256, 64))),
+                     dim3(64), 0, s, (char*)d_result, lay, n, nlimbs, live_bytes ? live_count : nullptr, amb,
+                     (uint4*)need, need16);
   PHIP(hipGetLastError());
 
   GroupArgs ga;
@@ -3058,7 +3063,6 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
     else {
       if (skip2) {
         const int tx = (W + NMS_TX - 1) / NMS_TX, tyl = (H + NMS_TY - 1) / NMS_TY, nt = (int)n_tiles_all;
-        PHIP(hipMemsetAsync(need, 0, need_bytes, s));
         hipLaunchKernelGGL(stage2_need_kernel, dim3((nt + 255) / 256), dim3(256), 0, s, fh, (const float*)bm1, H, W, tx,
                            tyl, nt, 0.1, ty2, ry_tiles, rx_tiles, live_mid, need);
         PHIP(hipGetLastError());

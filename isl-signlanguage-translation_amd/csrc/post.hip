@@ -2712,16 +2712,19 @@ __global__ void __launch_bounds__(CC_NT) hand_cc_kernel(const double* __restrict
   }
 }
 
-// (also zeroes the post's two list counters z0, z1 and z16 16-byte words at zb -- one launch
-// instead of three memsets)
+// (also zeroes the post's two list counters z0, z1, z16 16-byte words at zb and y16 at yb -- one
+// launch instead of four memsets)
 __global__ void init_records_kernel(char* result, isl_layout lay, int n, int nlimbs, int* z0 = nullptr,
-                                    int* z1 = nullptr, uint4* zb = nullptr, long long z16 = 0) {
+                                    int* z1 = nullptr, uint4* zb = nullptr, long long z16 = 0,
+                                    uint4* yb = nullptr, long long y16 = 0) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f == 0) {
     if (z0) *z0 = 0;
     if (z1) *z1 = 0;
   }
-  for (long long i = f; i < z16; i += (long long)gridDim.x * blockDim.x) zb[i] = make_uint4(0u, 0u, 0u, 0u);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = f; i < z16; i += stride) zb[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (long long i = f; i < y16; i += stride) yb[i] = make_uint4(0u, 0u, 0u, 0u);
   if (f >= n) return;
   char* rec = result + (size_t)f * lay.record_bytes;
   *(int*)(rec + lay.status) = ISL_OK;
@@ -3007,11 +3010,14 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   unsigned char* need = skip2 ? live_mid + up(lmid_bytes) : nullptr;
   bool bm_done = false;
 
-  // (amb[0]: the filter's list count; need: zeroed here for stage2_need_kernel)
+  // (amb[0]: the filter's list count; need: zeroed here for stage2_need_kernel; the peak mask
+  // too when the blur runs over a live list, which writes the live tiles' words only)
   const long long need16 = (long long)(up(need_bytes) / 16);
-  hipLaunchKernelGGL(init_records_kernel, dim3(std::max<long long>((n + 63) / 64, std::min<long long>((need16 + 255) / 256, 64))),
-                     dim3(64), 0, s, (char*)d_result, lay, n, nlimbs, live_bytes ? live_count : nullptr, amb,
-                     (uint4*)need, need16);
+  const long long mask16 = live_bytes ? (long long)(up(mask_bytes) / 16) : 0;
+  hipLaunchKernelGGL(init_records_kernel,
+                     dim3(std::max<long long>((n + 255) / 256, std::min<long long>((need16 + mask16 + 1023) / 1024, 2048))),
+                     dim3(256), 0, s, (char*)d_result, lay, n, nlimbs, live_bytes ? live_count : nullptr, amb,
+                     (uint4*)need, need16, (uint4*)mask, mask16);
   PHIP(hipGetLastError());
 
   GroupArgs ga;
@@ -3095,7 +3101,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   } else if (fused) {
     // live-tile list (low-res bound), then the fused blur over live tiles only
     const int n_tiles = (int)(gb.x * gb.y * gb.z);
-    PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));   // (live_count: zeroed by init_records_kernel)
+    // (mask, live_count: zeroed by init_records_kernel)
     const dim3 tl((n_tiles + TL_TILES - 1) / TL_TILES);
     if (wide) {
 #ifdef ISLPOSE_DEV
@@ -3118,7 +3124,7 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   } else if (bm_done && band_list) {
     // live-tile list (the band maxima), then the blur over live tiles only
     const int n_tiles = (int)(gb.x * gb.y * gb.z);
-    PHIP(hipMemsetAsync(mask, 0, mask_bytes, s));   // (live_count: zeroed by init_records_kernel)
+    // (mask, live_count: zeroed by init_records_kernel)
     hipLaunchKernelGGL(band_live_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, s, (const float*)bandmax, H, W,
                        words, tx, tyl, n_tiles, 0.1, live, live_count, (const unsigned char*)live_mid);
     PHIP(hipGetLastError());

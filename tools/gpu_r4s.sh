@@ -9,4 +9,5 @@ rc=$?
 tail -3 $O/tests.log
 if [ $rc -ne 0 ]; then grep -E "FAIL|Error|assert" $O/tests.log | head -20; exit $rc; fi
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t1 -o run -- python3 tools/post_prof.py --batch 1 --iters 20 > $O/t1.log 2>&1 &&
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t32 -o run -- python3 tools/post_prof.py --batch 32 --iters 5 > $O/t32.log 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/t32 -o run -- python3 tools/post_prof.py --batch 32 --iters 5 > $O/t32.log 2>&1 &&
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tn -o run -- python3 tools/post_prof.py --batch 32 --iters 5 --scale 1.0 > $O/tn.log 2>&1

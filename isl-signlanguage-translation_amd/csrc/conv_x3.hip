@@ -1666,6 +1666,34 @@ static bool x3_g2(const ConvLaunch& c) {
   return !(e && e[0] == '0');
 }
 
+// Small grids whose K ranges run across blocks (batch-1 Mode R's 23x41 stage layers: 8 pixel
+// tiles x S ranges, far under one block per CU) on 64-pixel tiles: the 96-channel tiles as 6
+// waves of 32co x 32px (not 12 on 128 pixels), the half-channel blocks of the 128-channel tiles
+// (VAR 256) as 4 waves of 32co x 32px (not 4 of 64co x 32px on 128 pixels) -- twice the blocks,
+// each with half the MFMAs and staging per K step.  Each output sees the same MFMA sequence (same
+// ranges, same K order): same bits.  Batch-1 Mode R net 1.955 -> 1.828 ms (profiles/r04/r4ai/).
+// ISLPOSE_X3_PX64=0: the 128-pixel blocks, =1: the 96-channel tiles only (A/B; read per launch).
+static int x3_px64_mode() {
+  const char* e = getenv("ISLPOSE_X3_PX64");
+  return e ? atoi(e) : 2;
+}
+static bool x3_px64(const ConvLaunch& c) {
+  if (c.ks > 3 || c.bco != 96 || c.fold || c.vin || c.ksplit < 2 || !c.ws) return false;
+  return x3_px64_mode() >= 1;
+}
+
+// Small 3x3 grids without K ranges (batch-1 conv2_x / conv3_x: at most half a block per CU) on
+// half-channel blocks (VAR 256): twice the blocks; same MFMA sequence per output, same bits.
+// Batch-1 Mode R net 1.828 -> 1.817 ms; the 1x1 layers (the two-launch Mconv6) measured slower
+// and the deep-prefetch form level (profiles/r04/r4ai/).  ISLPOSE_X3_HALFSMALL=0 off (A/B).
+static bool x3_halfsmall(const ConvLaunch& c) {
+  const char* e = getenv("ISLPOSE_X3_HALFSMALL");
+  if ((e && e[0] == '0') || c.ks != 3 || c.bco != 128 || c.fold || c.vin || c.ksplit > 1) return false;
+  const int tpx = tile_pixels(c, 128, x3_segmax(128));
+  const long long blocks = (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * ((c.cout + c.bco - 1) / c.bco);
+  return 2 * blocks <= device_cus();
+}
+
 // Small grids (the 128-pixel family) with the inputs and weights prefetched two K steps
 // ahead (VAR 128): by default the 3x3 layers whose grid has at most one block per CU and
 // whose K ranges (if any) run in one block -- Mode R's 23x41 stage layers at batch 32, -5 to
@@ -1975,6 +2003,9 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
         if (x3_g2(c)) return launch_t<KS, 2, 4, 2, 1, 1024 | 32, 1>(c, s);   // two K groups of 8 waves
       }
       if constexpr (KS <= 3) {
+        if (!split && !ranged && x3_halfsmall(c)) return launch_t<KS, 1, 4, 2, 1, 256, 4>(c, s);
+      }
+      if constexpr (KS <= 3) {
         if (x3_deep(c)) {   // prefetch two K steps ahead
           switch (c.bco) {
             case 128:
@@ -2005,18 +2036,20 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
       }
 #endif
       if (c.bco == 128 && x3_halfco(c)) {   // two blocks of 4 waves (64co x 32px) per 128-channel tile
+        if (split && x3_px64_mode() >= 2) return launch_t<KS, 2, 2, 1, 1, 2048 | 256, 4>(c, s);
         if (split) return launch_t<KS, 1, 4, 2, 1, 2048 | 256, 4>(c, s);
 #ifdef ISLPOSE_DEV
         if (ranged) return launch_t<KS, 1, 4, 2, 1, 1024 | 256, 4>(c, s);
-        return launch_t<KS, 1, 4, 2, 1, 256, 4>(c, s);
 #endif
+        if (!ranged) return launch_t<KS, 1, 4, 2, 1, 256, 4>(c, s);
       }
       switch (c.bco) {
         case 128:   // 8 waves of 64co x 32px
           if (split) return launch_t<KS, 2, 4, 2, 1, 2048, 2>(c, s);
           if (ranged) return launch_t<KS, 2, 4, 2, 1, 1024, 2>(c, s);
           return launch_t<KS, 2, 4, 2, 1, 0, 2>(c, s);
-        case 96:    // 12 waves of 32co x 32px
+        case 96:    // 12 waves of 32co x 32px (6 on 64-pixel tiles: x3_px64)
+          if (split && x3_px64(c)) return launch_t<KS, 3, 2, 1, 1, 2048, 4>(c, s);
           if (split) return launch_t<KS, 3, 4, 1, 1, 2048, 2>(c, s);
           if (ranged) return launch_t<KS, 3, 4, 1, 1, 1024, 2>(c, s);
           return launch_t<KS, 3, 4, 1, 1, 0, 2>(c, s);

@@ -1318,7 +1318,7 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
 static const char* const kRunKeySwitches[] = {
     "ISLPOSE_X3_DEEP",   "ISLPOSE_RGB_CONV", "ISLPOSE_FUSED_POOL", "ISLPOSE_POOL_INPUT", "ISLPOSE_CONV_STAGING",
     "ISLPOSE_X3_TILES",  "ISLPOSE_X3_UNION", "ISLPOSE_X3_HALF64",  "ISLPOSE_X3_WIDE7",   "ISLPOSE_X3_ACROSS",
-    "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67", "ISLPOSE_X3_G2",
+    "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67", "ISLPOSE_X3_G2", "ISLPOSE_X3_PX64", "ISLPOSE_X3_HALFSMALL",
 #ifdef ISLPOSE_DEV
     "ISLPOSE_X3_HALFCO", "ISLPOSE_X3_PPS2",  "ISLPOSE_X3_M16",     "ISLPOSE_X3_WINO",    "ISLPOSE_X3_ABL",
 #endif

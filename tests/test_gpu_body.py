@@ -496,16 +496,49 @@ def test_graph_replay_bit_identical(w25, n, monkeypatch):
 @pytest.mark.parametrize("n", [1, 32])
 def test_x3_halfco_default_selection(net25, n):
     """Half-channel blocks (VAR 256: two 64-channel blocks per 128-channel tile) are the
-    product default only where the canonical K ranges run across blocks (batch-1 Mode R);
-    at batch 32 (ranges in one block) none.  Same bits either way: the batch-invariance test
-    compares the two executions."""
+    product default where the canonical K ranges run across blocks (batch-1 Mode R) and on the
+    3x3 grids of at most half a block per CU (x3_halfsmall); at batch 32 none.  Same bits
+    either way: the batch-invariance test compares the two executions."""
     x = torch.from_numpy(_inputs(n, 184, 328, seed=91 + n)).cuda()
     net25.forward(x)
     torch.cuda.synchronize()
     var = [rt.decode_variant(v) for _, v in net25.op_variants()]
     halves = sum(1 for v in var if v.get("var", 0) & 256)
     assert halves >= 40 if n == 1 else halves == 0
-    assert all(v.get("var", 0) & 2048 for v in var if v.get("var", 0) & 256)
+    # without ranges only on the small 3x3 grids (x3_halfsmall: batch-1 conv2_x / conv3_x)
+    assert all(v.get("var", 0) & 2048 or v["ks"] == 3 for v in var if v.get("var", 0) & 256)
+
+
+@pytest.mark.parametrize("n", [1, 2])
+@pytest.mark.parametrize("env", [None, ("ISLPOSE_X3_PX64", "1"), ("ISLPOSE_X3_HALFSMALL", "0")])
+def test_x3_px64_c96_split_bit_identical(net25, n, env, monkeypatch):
+    """Small-grid block forms == the 128-pixel full-channel blocks (ISLPOSE_X3_PX64=0,
+    ISLPOSE_X3_HALFSMALL=0) bit for bit, by default and in the A/B forms: where the canonical K
+    ranges run across blocks (the 23x41 stage layers at small batch) the 96-channel tiles and
+    the half-channel blocks on 64 pixels (x3_px64; =1 the 96-channel ones only), and the small
+    3x3 grids without ranges on half-channel blocks (x3_halfsmall) -- same K order per output."""
+    x = torch.from_numpy(_inputs(n, 184, 328, seed=77 + n)).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_PX64", "0")
+    monkeypatch.setenv("ISLPOSE_X3_HALFSMALL", "0")
+    paf0, heat0 = net25.forward(x)
+    torch.cuda.synchronize()
+    var0 = [rt.decode_variant(v) for _, v in net25.op_variants()]
+    monkeypatch.delenv("ISLPOSE_X3_PX64")
+    monkeypatch.delenv("ISLPOSE_X3_HALFSMALL")
+    if env:
+        monkeypatch.setenv(*env)
+    paf1, heat1 = net25.forward(x)
+    torch.cuda.synchronize()
+    var1 = [rt.decode_variant(v) for _, v in net25.op_variants()]
+    px64 = [v for v in var1 if v.get("bco") == 96 and v.get("bpx") == 64]
+    assert len(px64) >= 10 and all(v["split"] for v in px64)
+    assert not any(v.get("bco") == 96 and v.get("bpx") == 64 for v in var0)
+    half64 = sum(1 for v in var1 if v.get("var", 0) & 256 and v["bpx"] == 64)
+    assert half64 >= 20 if env != ("ISLPOSE_X3_PX64", "1") else half64 == 0
+    if n == 1:
+        small = sum(1 for v in var1 if v.get("var", 0) & 256 and not v["split"])
+        assert small >= 2 if env != ("ISLPOSE_X3_HALFSMALL", "0") else small == 0
+    assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
 
 
 def test_graph_drop_waits_for_queued_replays(w25):

@@ -1,4 +1,5 @@
-# Round 4 (A/B): the split small-grid blocks on 32 pixels (ISLPOSE_X3_PX64=3) vs 64 (default).
+# Round 4 (A/B, done): the split small-grid blocks on 32 pixels (ISLPOSE_X3_PX64=3) vs 64 (default);
+# measured level, profiles/r04/r4al/, and not built: =3 now runs the 64-pixel blocks.
 T=${1:-r4al}; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
 ISLPOSE_X3_PX64=3 timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread \

@@ -1,4 +1,5 @@
-# Round 4 (A/B): Mode R batch 32's ranged c96 deep layers on 64-pixel blocks (ISLPOSE_X3_PX64B=1).
+# Round 4 (A/B, done): Mode R batch 32's ranged c96 deep layers on 64-pixel blocks (ISLPOSE_X3_PX64B=1;
+# measured 38-45 % slower per layer, profiles/r04/r4am/, and removed: the switch no longer exists).
 T=${1:-r4am}; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
 ISLPOSE_X3_PX64B=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread \

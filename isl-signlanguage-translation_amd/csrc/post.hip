@@ -1522,11 +1522,74 @@ constexpr int ASM_LDS_ROWS = 256;   // subset rows that fit the LDS table (256 x
 // lanes loading at once (ASM_CONN_CACHE of them; more: read in place): the serial merge then
 // never waits on a global load (it waited on two per connection, ~75 us per 32-frame batch).
 constexpr int ASM_CONN_CACHE = 512;   // x 5 doubles = 20 KB
+// The merge with the table in registers: lane r holds subset row r, the limbs unrolled at compile
+// time so that row[A] / row[B] are fixed registers.  The common connections -- one hit (a
+// predicated update in the hit lane) or none (a new row) -- are then two compares and a ballot,
+// with no LDS round trip on the chain.  The rare ones (two or three hits: the row merge and
+// delete, the IndexError; a 65th row; the row cap) leave the register loop: the rows go to the
+// table, the table merge takes that one connection (all the rest past 64 rows), and the rows come
+// back.  Same operations in the same order as the table merge (body.py:186-226), so the same bits.
+// (Unrolling the rare paths per limb too made a 200 KB kernel bound by instruction fetch.)
+constexpr int kRegA25[24] = {1, 1, 2, 3, 1, 5, 6, 1, 8, 9, 10, 8, 12, 13, 0, 0, 15, 16, 11, 11, 14, 14, 22, 19};
+constexpr int kRegB25[24] = {0, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 24, 22, 21, 19, 23, 20};
+constexpr int kRegACoco[19] = {1, 1, 2, 3, 5, 6, 1, 8, 9, 1, 11, 12, 1, 0, 14, 0, 15, 2, 5};
+constexpr int kRegBCoco[19] = {2, 5, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 0, 14, 16, 15, 17, 16, 17};
+constexpr int reg_limb_a(int model, int k) { return model == ISL_BODY25 ? kRegA25[k] : kRegACoco[k]; }
+constexpr int reg_limb_b(int model, int k) { return model == ISL_BODY25 ? kRegB25[k] : kRegBCoco[k]; }
+
+// limbs K .. NL-1 from connection (k_from, ci_from); returns 0 done, 2 stopped at (stop_k, stop_ci)
+template <int MODEL, int RW, int NL, int K>
+__device__ __forceinline__ int asm_reg_limbs(double (&v)[RW], int& rows, const double* s_conn, const int* s_koff,
+                                             int lane, int max_rows, int k_from, int ci_from, int& stop_k,
+                                             int& stop_ci) {
+  if constexpr (K == NL) {
+    return 0;
+  } else {
+    constexpr int A = reg_limb_a(MODEL, K), B = reg_limb_b(MODEL, K);
+    constexpr bool NEW = MODEL == ISL_BODY25 ? true : K < 17;   // k < njoint - 2 (body.py:220)
+    if (K >= k_from) {
+      const int k0 = s_koff[K], m = s_koff[K + 1] - k0;
+      for (int ci = K == k_from ? ci_from : 0; ci < m; ++ci) {
+        const double* c = s_conn + (size_t)(k0 + ci) * 5;
+        const double idA = c[0], idB = c[1];
+        const bool hit = lane < rows && (v[A] == idA || v[B] == idB);
+        const unsigned long long mask = __ballot(hit);
+        const int found = __builtin_popcountll(mask);
+        if (found >= 2 || (found == 0 && NEW && (rows >= 64 || rows >= max_rows))) {
+          stop_k = K;
+          stop_ci = ci;
+          return 2;
+        }
+        if (found == 1) {
+          if (lane == __builtin_ctzll(mask) && v[B] != idB) {
+            v[B] = idB;
+            v[RW - 1] = v[RW - 1] + 1.0;
+            v[RW - 2] = v[RW - 2] + (c[4] + c[2]);
+          }
+        } else if constexpr (NEW) {
+          if (lane == rows) {
+#pragma unroll
+            for (int q = 0; q < RW; ++q) v[q] = -1.0;
+            v[A] = idA;
+            v[B] = idB;
+            v[RW - 1] = 2.0;
+            v[RW - 2] = (c[3] + c[4]) + c[2];
+          }
+          ++rows;
+        }
+      }
+    }
+    return asm_reg_limbs<MODEL, RW, NL, K + 1>(v, rows, s_conn, s_koff, lane, max_rows, k_from, ci_from, stop_k,
+                                                stop_ci);
+  }
+}
+
 // IN_LDS: the subset table in LDS (a template parameter, so that its accesses are ds_* rather
 // than flat instructions: a runtime choice of the table's address space made every access a
 // flat load / store with global latency, ~1600 cycles per connection of the serial merge)
-template <bool IN_LDS>
-__global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int conn_cap) {
+// MODEL: ISL_BODY25 / ISL_COCO (the register merge); use_reg = 0 the table merge only (A/B)
+template <bool IN_LDS, int MODEL>
+__global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int conn_cap, int use_reg) {
   constexpr bool in_lds = IN_LDS;
   extern __shared__ double s_asm[];
   double* s_subset = s_asm;
@@ -1587,9 +1650,11 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int conn_cap)
   ASTAMP(2);
   int rows = 0;
   // the merge, instantiated per connection source (cache / record) so that every access is typed
-  auto merge = [&](auto cache_tag) -> bool {
+  // (k_start, ci_start): the first connection; limit: how many to take (the register merge hands
+  // over single connections)
+  auto merge = [&](auto cache_tag, int k_start, int ci_start, int limit) -> bool {
   constexpr bool CACHED = decltype(cache_tag)::value;
-  for (int k = 0; k < a.nlimbs; ++k) {
+  for (int k = k_start; k < a.nlimbs; ++k) {
     // (the staged counts: special_k's -1 is 0 there, and a limb without connections does nothing
     // either way -- no dependent global load per limb)
     const int m = s_koff[k + 1] - s_koff[k];
@@ -1597,7 +1662,8 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int conn_cap)
     const int A = a.model == ISL_BODY25 ? kLimbs25[k][0] : kLimbsCoco[k][0];
     const int B = a.model == ISL_BODY25 ? kLimbs25[k][1] : kLimbsCoco[k][1];
     const double* cw = conns + (size_t)k * a.max_conns * 5;
-    for (int ci = 0; ci < m; ++ci) {
+    for (int ci = k == k_start ? ci_start : 0; ci < m; ++ci) {
+      if (limit-- == 0) return true;
       // (two typed branches, so that the cached reads are ds_* and not flat loads)
       double idA, idB, sc, sA = 0.0, sB = 0.0;
       if constexpr (CACHED) {
@@ -1719,7 +1785,42 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int conn_cap)
   }
   return true;
   };
-  if (!(cached ? merge(std::true_type{}) : merge(std::false_type{}))) return;
+  if (cached && use_reg) {
+    constexpr int RWC = MODEL == ISL_BODY25 ? 27 : 20, NLC = MODEL == ISL_BODY25 ? 24 : 19;
+    if (RW != RWC || a.nlimbs != NLC) {
+      if (lane == 0) *status = ISL_E_ARG;
+      return;
+    }
+    double v[RWC];
+#pragma unroll
+    for (int q = 0; q < RWC; ++q) v[q] = -1.0;
+    int k_from = 0, ci_from = 0;
+    while (true) {
+      int stop_k = 0, stop_ci = 0;
+      const int rc = asm_reg_limbs<MODEL, RWC, NLC, 0>(v, rows, s_conn, s_koff, lane, a.max_rows, k_from, ci_from,
+                                                        stop_k, stop_ci);
+      // the rows to the table (the prune below and the table merge read them there)
+      if (lane < rows) {
+#pragma unroll
+        for (int q = 0; q < RWC; ++q) subset[(size_t)lane * RWC + q] = v[q];
+      }
+      __syncthreads();
+      if (rc == 0) break;
+      // the stopping connection on the table merge; past 64 rows (or at the cap) all the rest
+      const bool rest = rows >= 64 || rows >= a.max_rows;
+      if (!merge(std::true_type{}, stop_k, stop_ci, rest ? 0x7fffffff : 1)) return;
+      if (rest) break;
+      __syncthreads();
+      if (lane < rows) {
+#pragma unroll
+        for (int q = 0; q < RWC; ++q) v[q] = subset[(size_t)lane * RWC + q];
+      }
+      k_from = stop_k;
+      ci_from = stop_ci + 1;
+    }
+  } else if (!(cached ? merge(std::true_type{}, 0, 0, 0x7fffffff) : merge(std::false_type{}, 0, 0, 0x7fffffff))) {
+    return;
+  }
   ASTAMP(3);
   // prune (body.py:227-231): keep rows with count >= 4 and mean score >= 0.4, in order
   int w = 0;
@@ -3166,10 +3267,24 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   const size_t sub_lds = asm_lds ? (size_t)caps->max_rows * (njoint + 1) * 8 : 0;
   const int conn_cap = (int)std::min<size_t>(ASM_CONN_CACHE, sub_lds < 65536 ? (65536 - sub_lds) / 40 : 0);
   asm_prof_arm((size_t)n, s);
-  if (asm_lds)
-    hipLaunchKernelGGL(assemble_kernel<true>, dim3(n), dim3(64), sub_lds + (size_t)conn_cap * 40, s, ga, conn_cap);
-  else
-    hipLaunchKernelGGL(assemble_kernel<false>, dim3(n), dim3(64), (size_t)conn_cap * 40, s, ga, conn_cap);
+  // ISLPOSE_ASM_REG=0: the table merge only (A/B; read per call)
+  const char* are = getenv("ISLPOSE_ASM_REG");
+  const int use_reg = !(are && are[0] == '0');
+  if (kind == ISL_BODY25) {
+    if (asm_lds)
+      hipLaunchKernelGGL((assemble_kernel<true, ISL_BODY25>), dim3(n), dim3(64), sub_lds + (size_t)conn_cap * 40, s, ga,
+                         conn_cap, use_reg);
+    else
+      hipLaunchKernelGGL((assemble_kernel<false, ISL_BODY25>), dim3(n), dim3(64), (size_t)conn_cap * 40, s, ga, conn_cap,
+                         use_reg);
+  } else {
+    if (asm_lds)
+      hipLaunchKernelGGL((assemble_kernel<true, ISL_COCO>), dim3(n), dim3(64), sub_lds + (size_t)conn_cap * 40, s, ga,
+                         conn_cap, use_reg);
+    else
+      hipLaunchKernelGGL((assemble_kernel<false, ISL_COCO>), dim3(n), dim3(64), (size_t)conn_cap * 40, s, ga, conn_cap,
+                         use_reg);
+  }
   PHIP(hipGetLastError());
   return ISL_OK;
 }

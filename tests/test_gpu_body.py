@@ -169,6 +169,35 @@ def estcoco():
     return BodyEstimator(synth.synth_weights(1), "coco")
 
 
+@pytest.mark.parametrize("kind,persons,drop", [("body25", 3, ()), ("body25", 80, ()), ("coco", 40, (12,)),
+                                               ("coco", 70, (12,))])
+def test_assemble_register_merge_equals_table(est25, estcoco, monkeypatch, kind, persons, drop):
+    """Person assembly with the subset rows in lane registers (the default) == the table merge
+    (ISLPOSE_ASM_REG=0) == the oracle (body.py:164-232).  368 x 4096 frames (46 x 512 low-res)
+    with up to 80 designed persons: more than 64 subset rows spill the registers to the table
+    mid-merge; COCO with the neck -> nose limb dropped makes every head its own row until the ear
+    limbs merge it into its body (the found == 2 branch and its row delete)."""
+    est = est25 if kind == "body25" else estcoco
+    H, W = 368, 4096
+    geoms = [g[1:] for g in scale_geometry(H, W, (1.0,))]
+    nh, nw = geoms[0][0] // 8, geoms[0][1] // 8
+    ms = [synth.designed_pose_maps(nh, nw, persons, seed=300 + i, model_type=kind, drop_limbs=drop) for i in range(2)]
+    pafs = [torch.from_numpy(np.stack([m[0] for m in ms])).cuda()]
+    heats = [torch.from_numpy(np.stack([m[1] for m in ms])).cuda()]
+    monkeypatch.delenv("ISLPOSE_ASM_REG", raising=False)
+    got = est.post_maps(H, W, geoms, pafs, heats)
+    monkeypatch.setenv("ISLPOSE_ASM_REG", "0")
+    ref = est.post_maps(H, W, geoms, pafs, heats)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a.candidate, b.candidate) and np.array_equal(a.subset, b.subset)
+    if persons > 64:
+        assert len(got[0].subset) > 64
+    heat_avg, paf_avg = cpu_ref.body_maps(np.zeros((H, W, 3), np.uint8), lambda im: (ms[0][0][None], ms[0][1][None]),
+                                          kind, (1.0,))
+    cand, subset, _, _ = cpu_ref.body_post(heat_avg, paf_avg, kind, H)
+    assert np.array_equal(got[0].candidate, cand) and np.array_equal(got[0].subset, subset)
+
+
 def test_body_post_golden_bit_exact(est25, estcoco):
     """Designed low-res maps replayed through the GPU post kernels == reference Body.__call__."""
     z, names = _golden_cases()

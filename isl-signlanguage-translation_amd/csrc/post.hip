@@ -1399,11 +1399,32 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
     // every (pair, point) in parallel (the nested two-stage samples are ~80 loads each), then
     // each pair's sum in point order
     __shared__ double s_item[LIMB_ITEMS];
-    for (int it = tid; it < np * 10; it += 256) {
-      double ux, uy, nr;
-      int xi, yi;
-      point(it / 10, it % 10, &ux, &uy, &nr, &xi, &yi);
-      s_item[it] = paf_value(a, f, mx, yi, xi) * ux + paf_value(a, f, my, yi, xi) * uy;
+    // small pair sets (np * 20 <= LIMB_ITEMS: a batch-1 frame's limbs) take the two PAF channels
+    // of a point on two threads, so a thread's chain is one sample; the products are added in the
+    // same order after the barrier (vx * ux + vy * uy)
+    const bool split = np * 20 <= LIMB_ITEMS;
+    if (split) {
+      for (int it = tid; it < np * 20; it += 256) {
+        const int item = it >> 1, ch = it & 1;
+        double ux, uy, nr;
+        int xi, yi;
+        point(item / 10, item % 10, &ux, &uy, &nr, &xi, &yi);
+        s_item[it] = paf_value(a, f, ch ? my : mx, yi, xi) * (ch ? uy : ux);
+      }
+      __syncthreads();
+      double sv[LIMB_ITEMS / 2 / 256 + 1];
+      int nv = 0;
+      for (int it = tid; it < np * 10; it += 256) sv[nv++] = s_item[2 * it] + s_item[2 * it + 1];
+      __syncthreads();
+      nv = 0;
+      for (int it = tid; it < np * 10; it += 256) s_item[it] = sv[nv++];
+    } else {
+      for (int it = tid; it < np * 10; it += 256) {
+        double ux, uy, nr;
+        int xi, yi;
+        point(it / 10, it % 10, &ux, &uy, &nr, &xi, &yi);
+        s_item[it] = paf_value(a, f, mx, yi, xi) * ux + paf_value(a, f, my, yi, xi) * uy;
+      }
     }
     // (these pairs' scores, keep flags, rank order and used flags live in LDS: the rank sort and
     // the serial greedy below then wait on no global load)

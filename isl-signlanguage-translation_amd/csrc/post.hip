@@ -1588,9 +1588,7 @@ __device__ __forceinline__ int asm_reg_limbs(double (&v)[RW], int& rows, const d
             v[RW - 2] = v[RW - 2] + (c[4] + c[2]);
           }
         } else if constexpr (NEW) {
-          if (lane == rows) {
-#pragma unroll
-            for (int q = 0; q < RW; ++q) v[q] = -1.0;
+          if (lane == rows) {   // (lanes >= rows hold -1 everywhere: the caller keeps them so)
             v[A] = idA;
             v[B] = idB;
             v[RW - 1] = 2.0;
@@ -1832,10 +1830,8 @@ __global__ void __launch_bounds__(64) assemble_kernel(GroupArgs a, int conn_cap,
       if (!merge(std::true_type{}, stop_k, stop_ci, rest ? 0x7fffffff : 1)) return;
       if (rest) break;
       __syncthreads();
-      if (lane < rows) {
 #pragma unroll
-        for (int q = 0; q < RWC; ++q) v[q] = subset[(size_t)lane * RWC + q];
-      }
+      for (int q = 0; q < RWC; ++q) v[q] = lane < rows ? subset[(size_t)lane * RWC + q] : -1.0;
       k_from = stop_k;
       ci_from = stop_ci + 1;
     }

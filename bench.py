@@ -388,7 +388,9 @@ def gpu_main(args, rank, local, world):
     if args.mode_r and args.scale == 1.0 and not args.no_op_timing:
         mode_r = {}
         for key, bb, st, wu in (("batch32", 32, args.steps, max(1, args.warmup)),
-                                ("batch1", 1, max(30, args.steps), max(3, args.warmup))):
+                                # (batch 1: 200 timed steps, ~0.35 s, so that one host hiccup does not
+                                # decide the rate; 30 steps read 467-575 frames/s box to box, r4ax)
+                                ("batch1", 1, max(200, args.steps), max(10, args.warmup))):
             mr = measure(0.5, bb, st, wu, 1, True)
             rf = roofline_of(mr["ops"])
             mode_r[key] = {"frames_per_s": round(mr["fps"], 2), "batch_per_gpu": bb, "steps": st, "warmup": wu,

@@ -352,7 +352,7 @@ def gpu_main(args, rank, local, world):
         for i in range(steps):
             # per-op HIP events (each lane's stream) on the last timed step only: an event
             # between every launch costs ~8 us of dispatch gap (1.8 % of the step when every
-            # step carried them, tools/gpu_optiming.sh); one instrumented step of K still gives
+            # step carried them, tools/archive/gpu_optiming.sh); one instrumented step of K still gives
             # the per-launch averages of every kernel, inside the timed region
             last = i == steps - 1
             if last and op_timing:

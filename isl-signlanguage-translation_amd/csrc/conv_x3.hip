@@ -109,6 +109,7 @@ struct X3Args {
   const float* slope7;
   float wscale7_inv;
   int cout7, act7;
+  int bco_pack;                 // conv_x3_wr: output channels per tile of the weight packing (c.bco)
 };
 
 // u / d for 0 <= u < 2^20, d >= 1, through the fp32 reciprocal r = 1/d: (u + 0.5) / d sits
@@ -145,7 +146,7 @@ __device__ __forceinline__ void x3_split8(const f32x4& a, const f32x4& b, f16x8&
     const f16x2 h = __builtin_convertvector(x, f16x2);
     const f32x2 hf = __builtin_convertvector(h, f32x2);
     // two scalar subtractions: hipcc would pack them into v_pk_add_f32, which beside the
-    // other waves' MFMAs measured 0.6 % slower (tools/gpu_split_ab.sh, profiles/r02/split_ab/)
+    // other waves' MFMAs measured 0.6 % slower (tools/archive/gpu_split_ab.sh, profiles/r02/split_ab/)
     f32x2 r;
     asm volatile("v_sub_f32 %0, %1, %2" : "=v"(r.x) : "v"(x.x), "v"(hf.x));
     asm volatile("v_sub_f32 %0, %1, %2" : "=v"(r.y) : "v"(x.y), "v"(hf.y));
@@ -1398,7 +1399,7 @@ hipError_t launch_conv_x3_rgb(const ConvLaunch& c, hipStream_t s) {
   a.H = c.H; a.W = c.W; a.cin_chunks = 1; a.pairs = 1; a.cout = c.cout;
   a.co_tiles = 1;
   // 256-pixel blocks: 3 % faster than 512 (more blocks resident per CU), 128 lost 16 %
-  // (tools/gpu_rgb_bpx.sh)
+  // (tools/archive/gpu_rgb_bpx.sh)
   constexpr int bpx = RGB_TILE;
   a.px_tiles = (c.H * c.W + bpx - 1) / bpx;
   a.tpx = bpx;
@@ -1500,6 +1501,163 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (co + e < a.cout) oc[e] = v[e];
+  }
+  if (bad) atomicOr(a.range_flag, 1);
+}
+
+
+// ---------------------------------------------------------------------------
+// Wave-range kernel (VAR 8): the small grids whose canonical K ranges would run across blocks
+// (x3_ranges: fewer 128-pixel blocks than CUs -- batch-1 Mode R's 23x41 stage layers, conv4_x
+// and Mconv7, the hand's 23^2 scale at small crop counts).  There the split-K form costs two
+// dependent launches per layer (the range blocks, then x3_splitk_reduce reading their partial
+// sums back from the workspace), and every block walks a chain of L2 round trips through LDS
+// staging and barriers (~13 us per layer).
+// Here one block is one output tile of 32 channels x 32 WN pixels of one frame, and wave r of
+// the block sums canonical K range r (blockDim = 64 S).  A wave loads its operands straight
+// into registers, DEPTH taps ahead: the pre-split weight fragments of its 32 rows (16 B per
+// lane and half, the pack_x3 slab) and the 8-channel input chunk of its pixel (32 B per lane,
+// split in registers by x3_split8).  No LDS staging, no barrier in the K loop.  Each wave runs
+// exactly the MFMA sequence of its range in conv_x3_f16 -- (pair, ky, kx), then hi*hi, hi*lo,
+// lo*hi, from zero, a missing odd chunk as zeros (the generic loop) -- the range sums meet in
+// LDS and are added in x3_canonical_order, then the epilogue of x3_splitk_reduce: the same bits
+// as the split-K launches and as the in-block ranges of larger batches, in one launch.
+template <int KS, int WN, int DEPTH>
+__global__ void __launch_bounds__(512) conv_x3_wr(X3Args a) {
+  constexpr int P = KS / 2;
+  constexpr int TP = KS * KS;                     // taps per chunk pair
+  const int S = a.ksplit;                         // waves = K ranges
+  int bid = blockIdx.x;
+  {   // XCD-aware order (conv_x3_f16): the channel tiles of a pixel tile on one XCD / L2
+    const int nb = a.nblocks, q = nb >> 3, r = nb & 7, xcd = bid & 7, k = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int co_t = bid % a.co_tiles;              // 32-channel tiles
+  const int rest = bid / a.co_tiles;
+  const int pt = rest % a.px_tiles;
+  const int n = rest / a.px_tiles;
+  const int HW = a.H * a.W;
+  const int m0 = pt * 32 * WN;
+  const int mlast = min(m0 + 32 * WN, HW) - 1;
+  const int Wi = a.W + 2 * a.in_pad;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, l32 = lane & 31;
+  const float* in_f = a.in + (size_t)n * a.in_fs;
+  // padded linear index of this lane's pixels at tap (ky, kx) = (0, 0)
+  int Lb[WN];
+#pragma unroll
+  for (int wn = 0; wn < WN; ++wn) {
+    const int m = min(m0 + wn * 32 + l32, mlast);
+    const int y = m / a.W, x = m - y * a.W;
+    Lb[wn] = (y + a.in_pad - P) * Wi + x + a.in_pad - P;
+  }
+  // this wave's range (conv_x3_f16 SPLIT: ceil(pairs / S) pairs per range, none empty)
+  const int pps = (a.pairs + S - 1) / S;
+  const int c2a = wave * pps, c2b = min(a.pairs, c2a + pps);
+  const int U = (c2b - c2a) * TP;
+  const int BCO = a.bco_pack, WS1 = KS * 4 * BCO;
+  const int co0 = co_t * 32, cpk = co0 / BCO;
+  const f16x8* wb = a.wpk + (size_t)cpk * a.pairs * KS * WS1 + h * BCO + (co0 - cpk * BCO) + l32;
+
+  f16x8 A[DEPTH][2];
+  f32x4 B[DEPTH][WN][2];
+  // tap u of the range -> its operands; past the end the last tap is read again (every load
+  // unconditional: the same count in flight on every path, so the waits stay counted)
+  auto load = [&](int u, f16x8 (&Ad)[2], f32x4 (&Bd)[WN][2]) __attribute__((always_inline)) {
+    u = min(u, U - 1);
+    const int pr = u / TP, r = u - pr * TP, ky = r / KS, kx = r - ky * KS;
+    const int c2 = c2a + pr;
+    const f16x8* w = wb + (size_t)(c2 * KS + ky) * WS1 + kx * 4 * BCO;
+    Ad[0] = w[0];
+    Ad[1] = w[2 * BCO];
+    const int c = min(2 * c2 + h, a.cin_chunks - 1);
+    const float* src = in_f + (size_t)c * a.in_chs + (size_t)(ky * Wi + kx) * 8;
+#pragma unroll
+    for (int wn = 0; wn < WN; ++wn) {
+      Bd[wn][0] = *(const f32x4*)(src + (size_t)Lb[wn] * 8);
+      Bd[wn][1] = *(const f32x4*)(src + (size_t)Lb[wn] * 8 + 4);
+    }
+  };
+  f32x16 acc[WN];
+#pragma unroll
+  for (int wn = 0; wn < WN; ++wn)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[wn][r] = 0.f;
+  auto compute = [&](int u, const f16x8 (&Ad)[2], const f32x4 (&Bd)[WN][2]) __attribute__((always_inline)) {
+    const int pr = u / TP;
+    const bool real = 2 * (c2a + pr) + h < a.cin_chunks;   // a missing odd chunk: zeros
+#pragma unroll
+    for (int wn = 0; wn < WN; ++wn) {
+      f16x8 bh, bl;
+      const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+      x3_split8(real ? Bd[wn][0] : z, real ? Bd[wn][1] : z, bh, bl);
+      acc[wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ad[0], bh, acc[wn], 0, 0, 0);
+      acc[wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ad[0], bl, acc[wn], 0, 0, 0);
+      acc[wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ad[1], bh, acc[wn], 0, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) load(d, A[d], B[d]);
+  for (int u0 = 0; u0 < U; u0 += DEPTH) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      if (u0 + d < U) compute(u0 + d, A[d], B[d]);   // (uniform)
+      load(u0 + d + DEPTH, A[d], B[d]);
+    }
+  }
+
+  // the ranges' sums through LDS: [range][wn][q][lane] x 4 floats (registers 4q .. 4q + 3)
+  __shared__ f32x4 xch[8 * WN * 4 * 64];
+#pragma unroll
+  for (int wn = 0; wn < WN; ++wn)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      xch[((wave * WN + wn) * 4 + q) * 64 + lane] =
+          f32x4{acc[wn][4 * q], acc[wn][4 * q + 1], acc[wn][4 * q + 2], acc[wn][4 * q + 3]};
+  __syncthreads();
+  // x3_canonical_order over the (wn, q) groups, spread over the waves; then x3_splitk_reduce's
+  // epilogue
+  const int hh = (S + 1) / 2, Wo = a.W + 2 * a.out_pad;
+  float* out_f = a.out + (size_t)n * a.out_fs;
+  bool bad = false;
+  for (int g = wave; g < WN * 4; g += S) {
+    const int wn = g >> 2, q = g & 3;
+    const int m = m0 + wn * 32 + l32;
+    const int co = co0 + 8 * q + 4 * h;
+    f32x4 lo = f32x4{0.f, 0.f, 0.f, 0.f}, hi = lo;   // onto +0, as the in-block sums
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k >= S) break;
+      const f32x4 v = xch[((k * WN + wn) * 4 + q) * 64 + lane];
+      if (k < hh) lo += v;
+      else hi += v;
+    }
+    const f32x4 sum = S > hh ? lo + hi : lo;
+    if (m > mlast || co >= a.cout) continue;
+    const f32x4 b = *(const f32x4*)(a.bias + co);
+    const f32x4 sl = a.act == ACT_PRELU ? *(const f32x4*)(a.slope + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = sum[e] * a.wscale_inv + b[e];
+    if (a.act == ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+    } else if (a.act == ACT_PRELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bad |= co + e < a.cout && !(__builtin_fabsf(v[e]) < 65504.f);
+    const int y = m / a.W, x = m - y * a.W;
+    float* oc = out_f + (size_t)(co >> 3) * a.out_chs + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8 + (co & 7);
+    if (co + 3 < a.cout) {
+      *(f32x4*)oc = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (co + e < a.cout) oc[e] = v[e];
+    }
   }
   if (bad) atomicOr(a.range_flag, 1);
 }
@@ -1758,13 +1916,13 @@ static int x3_canonical_ranges(const ConvLaunch& c) {
 // layers with canonical K ranges (their second accumulator set needs the 128-pixel
 // family's register budget).  512-pixel tiles are used only when they fill the
 // chip: a layer with fewer such blocks than CUs runs ~2x faster on the 128-pixel,
-// 4-wave family (tools/gpu_tiles.sh).
+// 4-wave family (tools/archive/gpu_tiles.sh).
 static bool x3_union(const ConvLaunch& c);
 
 // 64-channel 3x3 layers off the row union (full-resolution conv1_2 / hand conv1_2: 12 K
 // steps) run 256-pixel blocks of 8 waves (64co x 32px each), two blocks per CU, so that one
 // block's prologue and epilogue overlap the other's K loop: -4 to -5 % against the 16-wave
-// 512-pixel block (tools/gpu_mid.sh; the 128-channel layers stay on 512 pixels, where every
+// 512-pixel block (tools/archive/gpu_mid.sh; the 128-channel layers stay on 512 pixels, where every
 // 256-pixel shape lost 4-7 %).  ISLPOSE_X3_HALF64=0: the 512-pixel block (A/B).
 static bool x3_half64(const ConvLaunch& c) {
   static const bool on = !(getenv("ISLPOSE_X3_HALF64") && getenv("ISLPOSE_X3_HALF64")[0] == '0');
@@ -1784,7 +1942,7 @@ static bool x3_big_tiles(const ConvLaunch& c) {
 // every stage: 384/288 -> 512/256) also pack their split filters for 256-channel
 // tiles.  On big grids they run 16 waves of 64co x 64px over 256 pixels with two chunk
 // pairs per K step (VAR 4096: 24 MFMAs per wave between barriers instead of 12, and
-// the input read for half as many channel tiles): +7-12 % (tools/gpu_k1.sh).  Small
+// the input read for half as many channel tiles): +7-12 % (tools/archive/gpu_k1.sh).  Small
 // grids (K ranges, the 128-pixel family) keep the 128-channel packing: 256-channel
 // tiles there halve the blocks and lost 30 %.
 bool x3_wide1_layer(int ks, int cout, int cin_phys) {
@@ -1801,10 +1959,10 @@ bool x3_wide1(const ConvLaunch& c) {
 // time of a 128-pixel block (half the weight bytes per MFMA), so the choice is per
 // launch, by grid quantisation: rounds of one block per CU, a 256-pixel block costing
 // X3_WIDE7_COST 128-pixel blocks (measured over 92^2 / 69^2 / 46x82 grids at batch
-// 13-64, tools/gpu_wide7.sh).  Both pack the weights for 128-channel tiles.
+// 13-64, tools/archive/gpu_wide7.sh).  Both pack the weights for 128-channel tiles.
 constexpr double X3_WIDE7_COST = 1.74;
 // a round of 384-pixel blocks (12 waves, one input buffer): 2.58 rounds of 128 pixels,
-// from the hand's 92^2 layers (tools/gpu_w384.sh, profiles/r02/w384/)
+// from the hand's 92^2 layers (tools/archive/gpu_w384.sh, profiles/r02/w384/)
 constexpr double X3_W384_COST = 2.58;
 
 static int x3_wide7_mode() {   // ISLPOSE_X3_WIDE7: 0 never, 1 always (A/B), default by the estimate
@@ -1869,7 +2027,7 @@ static bool x3_m16(const ConvLaunch&) { return false; }    // rejected (profiles
 
 // K-range plan of a launch on the 128-pixel family: S ranges, computed across S blocks
 // per tile (split-K, partials through the workspace) when the plain grid has fewer
-// blocks than CUs, else in one block (tools/gpu_across.sh: across wins 10-50 % at
+// blocks than CUs, else in one block (tools/archive/gpu_across.sh: across wins 10-50 % at
 // 64-160 blocks, in-block wins 20-70 % at 256-1024 -- same bits either way).  With isl_net_set_split_k(net, 2) (latency
 // mode) layers without canonical ranges also split when their grid is that small --
 // an adaptive S that depends on the batch, so those layers' bits then do too.
@@ -1972,7 +2130,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
   // (Mode R's 23x41 stages: one block per CU at batch 32), and two or three waves per
   // SIMD hide the staging: -8 to -22 % on the 23x41 3x3 stage layers, -12 to -31 % on
   // their 1x1 layers, -5 to -14 % on the hand's 23^2 7x7 layers, -20 % on its 23^2 c512
-  // layers (tools/gpu_s8.sh, gpu_s8b.sh).  ISLPOSE_X3_S8=0: the 4-wave layouts (A/B).
+  // layers (tools/archive/gpu_s8.sh, gpu_s8b.sh).  ISLPOSE_X3_S8=0: the 4-wave layouts (A/B).
   static const int more = getenv("ISLPOSE_X3_S8") ? atoi(getenv("ISLPOSE_X3_S8")) : 1;
   if (more) {
     {
@@ -2155,11 +2313,76 @@ double conv_x3_fused67_mfma_flops(const ConvLaunch& c) {
   return 3.0 * 2.0 * px * ((double)c.cout * k6 + 32.0 * ((c.cout7 + 31) / 32) * c.cout);
 }
 
+
+// conv_x3_wr for the launches whose K ranges would run across blocks (x3_ranges), by default;
+// ISLPOSE_X3_WR=0: the split-K launches + x3_splitk_reduce (A/B), =2: also the small grids
+// without K ranges (one wave per block summing the whole K; A/B); ISLPOSE_X3_WR_WN=2: 64-pixel
+// tiles (two 32-pixel accumulator tiles per wave sharing the weight fragments).  Read per launch.
+static int x3_wr_mode() {
+  const char* e = getenv("ISLPOSE_X3_WR");
+  return e ? atoi(e) : 1;
+}
+
+template <int KS, int WN, int DEPTH>
+static hipError_t launch_wr_t(const ConvLaunch& c, int S, hipStream_t s) {
+  constexpr int P = KS / 2;
+  if (c.in_pad < P) { set_error("conv_x3_wr: input ring narrower than kernel radius"); return hipErrorInvalidValue; }
+  if ((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 7) { set_error("conv_x3_wr: slice not on a chunk"); return hipErrorInvalidValue; }
+  if (!c.wx3 || !c.range_flag) { set_error("conv_x3_wr: split weights / range flag missing"); return hipErrorInvalidValue; }
+  if (c.hpool || c.vin || c.fold || c.fold_out || c.cout7 > 0) {
+    set_error("conv_x3_wr: plain layers only (no fused pool, fold or pair)");
+    return hipErrorInvalidValue;
+  }
+  const int pairs = (c.cin_chunks + 1) / 2;
+  if (S < 1 || S > 8 || S > pairs || c.bco % 32 || c.bco <= 0) { set_error("conv_x3_wr: bad range count / tile"); return hipErrorInvalidValue; }
+  X3Args a{};
+  a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
+  a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
+  a.in_fs = a.in_chs * (c.in_cs / 8);
+  a.out_fs = a.out_chs * (c.out_cs / 8);
+  a.in = c.in + (c.in_coff / 8) * a.in_chs;
+  a.out = c.out + (c.out_coff / 8) * a.out_chs;
+  a.wpk = (const f16x8*)c.wx3; a.bias = c.bias; a.slope = c.slope;
+  a.range_flag = c.range_flag;
+  a.wscale_inv = c.wscale_inv;
+  a.in_pad = c.in_pad; a.out_pad = c.out_pad;
+  a.H = c.H; a.W = c.W; a.cin_chunks = c.cin_chunks; a.pairs = pairs; a.cout = c.cout;
+  a.co_tiles = (c.cout + 31) / 32;
+  a.tpx = 32 * WN;
+  a.px_tiles = (c.H * c.W + a.tpx - 1) / a.tpx;
+  a.act = c.act;
+  a.ksplit = S;
+  a.nfr = c.n;
+  a.bco_pack = c.bco;
+  const long long nb = (long long)c.n * a.px_tiles * a.co_tiles;
+  if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3_wr: bad grid"); return hipErrorInvalidValue; }
+  a.nblocks = (int)nb;
+  t_last_variant = x3_variant_code(8 | (S > 1 ? 1024 : 0), KS, 32 * WN, 32);
+  hipLaunchKernelGGL((conv_x3_wr<KS, WN, DEPTH>), dim3(a.nblocks), dim3(64 * S), 0, s, a);
+  return hipGetLastError();
+}
+
+static hipError_t launch_x3_wr(const ConvLaunch& c, int S, hipStream_t s) {
+  const char* e = getenv("ISLPOSE_X3_WR_WN");
+  const bool wn2 = e && e[0] == '2';
+  switch (c.ks) {
+    case 1: return wn2 ? launch_wr_t<1, 2, 6>(c, S, s) : launch_wr_t<1, 1, 8>(c, S, s);
+    case 3: return wn2 ? launch_wr_t<3, 2, 6>(c, S, s) : launch_wr_t<3, 1, 8>(c, S, s);
+    case 7: return wn2 ? launch_wr_t<7, 2, 6>(c, S, s) : launch_wr_t<7, 1, 8>(c, S, s);
+  }
+  set_error("conv_x3_wr: unsupported kernel size");
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_conv_x3(const ConvLaunch& c0, hipStream_t s) {
   if (c0.cout7 > 0) return launch_x3_fused67(c0, s);
   ConvLaunch c = c0;
   const X3Ranges r = x3_ranges(c);
   c.ksplit = r.S;
+  if (r.across_blocks && x3_wr_mode() >= 1 && !c.fold_out) return launch_x3_wr(c, r.S, s);
+  if (x3_wr_mode() >= 2 && r.S == 1 && c.ks <= 3 && !c.hpool && !c.vin && !c.fold && !x3_big_tiles(c) &&
+      x3_7x7_bpx(c) == 128)
+    return launch_x3_wr(c, 1, s);
   if (r.across_blocks) {
     if (!c.ws || (size_t)r.S * c.n * ((c.cout + 7) / 8) * 8 * c.H * c.W > c.ws_floats) {
       set_error("conv_x3: split-K workspace too small");

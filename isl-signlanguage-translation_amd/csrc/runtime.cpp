@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -242,12 +243,15 @@ struct isl_net {
     // algorithm, ISLPOSE_* environment) the eager runs seen and the instantiated graph
     struct Graph {
       hipGraphExec_t exec = nullptr;
+      hipEvent_t done = nullptr;     // recorded behind its latest replay, on the replay's stream
       std::vector<int> op_variant;
       unsigned long long last_use = 0;
     };
     std::map<unsigned long long, Graph> graphs;
     unsigned long long graph_clock = 0;
     std::map<unsigned long long, int> graph_seen;
+    std::set<unsigned long long> graph_failed;   // keys whose capture failed: eager for good
+    std::vector<Graph> graph_retired;            // evicted, freed once their `done` has passed
   };
   std::map<long long, Arena> plans;
   Arena* cur = nullptr;        // the arena of the current plan
@@ -626,8 +630,12 @@ static void plan_fuse67(isl_net* net) {
     // next op that writes it (every stage's Mconv6 reuses one buffer)
     bool other = false;
     for (size_t j = k + 2; j < net->ops.size(); ++j) {
-      if (net->ops[j].in == a.out) { other = true; break; }
-      if (net->ops[j].out == a.out) break;
+      const Op& o = net->ops[j];
+      if (o.in == a.out) { other = true; break; }
+      // only a write of every channel op k wrote ends its live range; after a partial one a
+      // later reader could still see channels the fused launch never writes
+      const int wc = o.type == 0 ? net->layers[o.layer].cout : o.C;
+      if (o.out == a.out && o.out_coff == 0 && wc >= la.cout) break;
     }
     if (other) continue;
     a.fuse67 = true;
@@ -836,20 +844,40 @@ static size_t arena_budget() {
 // Instantiated graphs hold the pointers and scalars of the launches they captured: any
 // reallocation of a buffer they name (arena, split-K workspace, weights re-uploaded with new
 // scales) drops them.  A replay may still be queued on any stream (the caller's, not ours), so
-// the device drains before an exec is destroyed: drops are rare (weights, workspace growth,
-// arena eviction, the per-arena cap), the wait is cheap next to them.
-static void destroy_exec(hipGraphExec_t exec) {
-  (void)hipDeviceSynchronize();
-  (void)hipGraphExecDestroy(exec);
+// a drop drains the device before the execs are destroyed: drops are rare (weights, workspace
+// growth, arena eviction), the wait is cheap next to them.
+// The per-arena cap's evictions (run_ops) do not drain the device on the launch path: the
+// evicted exec is retired behind the event recorded after its latest replay and destroyed once
+// that event has passed (reap_graphs, at the next run_ops); a retired exec is never launched again.
+static void free_graph(isl_net::Arena::Graph& g) {
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.done) (void)hipEventDestroy(g.done);
+  g.exec = nullptr;
+  g.done = nullptr;
+}
+
+static void reap_graphs(isl_net::Arena& ar) {
+  auto& v = ar.graph_retired;
+  for (size_t i = 0; i < v.size();) {
+    if (!v[i].done || hipEventQuery(v[i].done) == hipSuccess) {
+      free_graph(v[i]);
+      v[i] = v.back();
+      v.pop_back();
+    } else {
+      ++i;
+    }
+  }
+  (void)hipGetLastError();   // a not-ready query leaves hipErrorNotReady behind
 }
 
 static void drop_graphs(isl_net::Arena& ar) {
-  bool any = false;
+  bool any = !ar.graph_retired.empty();
   for (auto& kv : ar.graphs) any |= kv.second.exec != nullptr;
   if (any) (void)hipDeviceSynchronize();
-  for (auto& kv : ar.graphs)
-    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+  for (auto& kv : ar.graphs) free_graph(kv.second);
+  for (auto& g : ar.graph_retired) free_graph(g);
   ar.graphs.clear();
+  ar.graph_retired.clear();
 }
 
 static void drop_all_graphs(isl_net* net) {
@@ -1319,6 +1347,7 @@ static const char* const kRunKeySwitches[] = {
     "ISLPOSE_X3_DEEP",   "ISLPOSE_RGB_CONV", "ISLPOSE_FUSED_POOL", "ISLPOSE_POOL_INPUT", "ISLPOSE_CONV_STAGING",
     "ISLPOSE_X3_TILES",  "ISLPOSE_X3_UNION", "ISLPOSE_X3_HALF64",  "ISLPOSE_X3_WIDE7",   "ISLPOSE_X3_ACROSS",
     "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67", "ISLPOSE_X3_G2", "ISLPOSE_X3_PX64", "ISLPOSE_X3_HALFSMALL",
+    "ISLPOSE_X3_WR",     "ISLPOSE_X3_WR_WN",
 #ifdef ISLPOSE_DEV
     "ISLPOSE_X3_HALFCO", "ISLPOSE_X3_PPS2",  "ISLPOSE_X3_M16",     "ISLPOSE_X3_WINO",    "ISLPOSE_X3_ABL",
 #endif
@@ -1357,13 +1386,21 @@ static int run_ops(isl_net* net, hipStream_t s) {
   if (!graph_enabled(net)) return run_ops_eager(net, s);
   isl_net::Arena& ar = *net->cur;
   const unsigned long long key = run_key(net);
+  if (!ar.graph_retired.empty()) reap_graphs(ar);
+  // after a replay, the event its eviction would wait for
+  auto launch = [&](isl_net::Arena::Graph& G) -> int {
+    HIP_OK(hipGraphLaunch(G.exec, s));
+    if (!G.done) HIP_OK(hipEventCreateWithFlags(&G.done, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(G.done, s));
+    return ISL_OK;
+  };
   auto g = ar.graphs.find(key);
   if (g != ar.graphs.end()) {
     net->op_variant = g->second.op_variant;
     g->second.last_use = ++ar.graph_clock;
-    HIP_OK(hipGraphLaunch(g->second.exec, s));
-    return ISL_OK;
+    return launch(g->second);
   }
+  if (ar.graph_failed.count(key)) return run_ops_eager(net, s);
   if (ar.graph_seen.size() >= kGraphSeenCap && !ar.graph_seen.count(key)) ar.graph_seen.clear();
   int& seen = ar.graph_seen[key];
   if (seen++ < 1) return run_ops_eager(net, s);
@@ -1382,22 +1419,22 @@ static int run_ops(isl_net* net, hipStream_t s) {
     // nothing ran: the chain was only recorded.  Run it eagerly, and keep this key eager
     (void)hipGetLastError();
     if (exec) (void)hipGraphExecDestroy(exec);
-    seen = -(1 << 30);
+    ar.graph_failed.insert(key);   // kept apart from graph_seen, whose cap clears it
+    ar.graph_seen.erase(key);
     return run_ops_eager(net, s);
   }
   while (ar.graphs.size() >= kGraphsPerArena) {
     auto lru = ar.graphs.begin();
     for (auto j = ar.graphs.begin(); j != ar.graphs.end(); ++j)
       if (j->second.last_use < lru->second.last_use) lru = j;
-    destroy_exec(lru->second.exec);
+    ar.graph_retired.push_back(lru->second);
     ar.graphs.erase(lru);
   }
   isl_net::Arena::Graph& G = ar.graphs[key];
   G.exec = exec;
   G.op_variant = net->op_variant;
   G.last_use = ++ar.graph_clock;
-  HIP_OK(hipGraphLaunch(exec, s));
-  return ISL_OK;
+  return launch(G);
 }
 
 static int copy_outputs(isl_net* net, float* d_out0, float* d_out1, hipStream_t s) {

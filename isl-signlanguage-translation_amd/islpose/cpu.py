@@ -194,6 +194,10 @@ def _assemble(all_peaks, connection_all, special_k, model_type, njoint):
         for c in conn:
             pa, pb = c[0], c[1]
             hits = [r for r in range(len(subset)) if subset[r][ia] == pa or subset[r][ib] == pb]
+            if len(hits) > 2:
+                # body.py:193-196: subset_idx has two slots, the third match's store raises
+                # (the GPU path flags it as ISL_E_INDEX and raises the same)
+                raise IndexError("list assignment index out of range")
             if len(hits) == 1 or (len(hits) == 2 and
                                   ((subset[hits[0]] >= 0).astype(int) + (subset[hits[1]] >= 0).astype(int))[:-2]
                                   .max() == 2):

@@ -89,6 +89,27 @@ def test_cpu_hand_post_matches_reference():
         assert peaks.dtype == z[c + "/peaks"].dtype and np.array_equal(peaks, z[c + "/peaks"]), c
 
 
+def test_cpu_assemble_third_match_raises_index_error():
+    """body.py:193-196: a connection matching three subset rows stores subset_idx[2] and raises
+    IndexError.  Crafted connections reach it: limb 1 (neck -> r-shoulder) makes rows R0 / R1,
+    a third connection overlapping both takes the found == 2 'as found == 1' branch and leaves
+    shoulder 3 in two rows; limb 2 (r-shoulder -> r-elbow) makes R2 with elbow 5, and (3, 5)
+    then matches R0, R1 and R2.  The GPU assembly flags the same case (ISL_E_INDEX)."""
+    all_peaks = [[(i, i, 0.5 + 0.01 * i, i) for i in range(8)]] + [[] for _ in range(24)]
+    conns = [np.zeros((0, 5)) for _ in range(24)]
+    conns[1] = np.array([[0, 2, 0.5, 0, 0], [1, 3, 0.5, 1, 1], [0, 3, 0.4, 0, 1]], np.float64)
+    conns[2] = np.array([[4, 5, 0.5, 0, 0], [3, 5, 0.4, 1, 0]], np.float64)
+    with pytest.raises(IndexError):
+        cpu._assemble(all_peaks, conns, [], "body25", 26)
+    with pytest.raises(IndexError):
+        cpu_ref.assemble(all_peaks, conns, [], "body25")
+    # without the last connection both return the same rows
+    conns[2] = conns[2][:1]
+    cand, subset = cpu._assemble(all_peaks, conns, [], "body25", 26)
+    rc, rs = cpu_ref.assemble(all_peaks, conns, [], "body25")
+    assert np.array_equal(cand, rc) and np.array_equal(subset, rs)
+
+
 @pytest.mark.skipif(torch.cuda.is_available(), reason="the GPU-less seam (with a device Body runs on it)")
 def test_body_and_hand_without_gpu_match_oracle():
     """src.body.Body / src.hand.Hand on a GPU-less host: frame in, (candidate, subset) / peaks

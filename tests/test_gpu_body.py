@@ -470,6 +470,7 @@ def test_x3_deep_small_grids_bit_identical(net25, n, monkeypatch):
     the waits are counted, raw barriers) run the same MFMA sequence as the default loop:
     bit-identical maps, with the stage layers on the variant (isl_net_op_info)."""
     x = torch.from_numpy(_inputs(n, 184, 328, seed=600 + n)).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_WR", "0")     # the split-K form (wave ranges take precedence)
     monkeypatch.setenv("ISLPOSE_X3_G2", "0")     # two K groups take precedence over the deep loop
     monkeypatch.setenv("ISLPOSE_X3_DEEP", "0")
     paf0, heat0 = net25.forward(x)
@@ -523,11 +524,12 @@ def test_graph_replay_bit_identical(w25, n, monkeypatch):
 
 
 @pytest.mark.parametrize("n", [1, 32])
-def test_x3_halfco_default_selection(net25, n):
+def test_x3_halfco_default_selection(net25, n, monkeypatch):
     """Half-channel blocks (VAR 256: two 64-channel blocks per 128-channel tile) are the
-    product default where the canonical K ranges run across blocks (batch-1 Mode R) and on the
-    3x3 grids of at most half a block per CU (x3_halfsmall); at batch 32 none.  Same bits
-    either way: the batch-invariance test compares the two executions."""
+    default of the split-K form (ISLPOSE_X3_WR=0) where the canonical K ranges run across blocks
+    (batch-1 Mode R) and on the 3x3 grids of at most half a block per CU (x3_halfsmall); at batch
+    32 none.  Same bits either way: the batch-invariance test compares the two executions."""
+    monkeypatch.setenv("ISLPOSE_X3_WR", "0")
     x = torch.from_numpy(_inputs(n, 184, 328, seed=91 + n)).cuda()
     net25.forward(x)
     torch.cuda.synchronize()
@@ -547,6 +549,7 @@ def test_x3_px64_c96_split_bit_identical(net25, n, env, monkeypatch):
     the half-channel blocks on 64 pixels (x3_px64; =1 the 96-channel ones only), and the small
     3x3 grids without ranges on half-channel blocks (x3_halfsmall) -- same K order per output."""
     x = torch.from_numpy(_inputs(n, 184, 328, seed=77 + n)).cuda()
+    monkeypatch.setenv("ISLPOSE_X3_WR", "0")      # the split-K form's block shapes
     monkeypatch.setenv("ISLPOSE_X3_PX64", "0")
     monkeypatch.setenv("ISLPOSE_X3_HALFSMALL", "0")
     paf0, heat0 = net25.forward(x)
@@ -597,6 +600,39 @@ def test_graph_drop_waits_for_queued_replays(w25):
     rp, rh = eager.forward(x)
     torch.cuda.synchronize()
     assert torch.equal(o0, rp) and torch.equal(o1, rh)
+
+
+def test_graph_cap_evicts_without_draining(w25):
+    """More run keys than the per-arena cap (8 instantiated graphs): each new capture retires the
+    least recently launched exec behind the event of its last replay instead of a device-wide
+    synchronisation; the retired execs are freed once those events have passed.
+    Ten batch sizes, each captured and replayed on a non-default stream with no host wait, then
+    every size again: all maps equal an eager net's."""
+    g = rt.Net(rt.ISL_BODY25)
+    g.load_weights(w25)
+    g.set_graph(True)
+    eager = rt.Net(rt.ISL_BODY25)
+    eager.load_weights(w25)
+    eager.set_graph(False)
+    s = torch.cuda.Stream()
+    sh = rt.stream_handle(s)
+    x = torch.from_numpy(_inputs(10, 64, 96, seed=23)).cuda()
+    outs = {}
+    s.wait_stream(torch.cuda.current_stream())
+    for rnd in range(2):
+        for n in range(1, 11):
+            o0 = torch.empty((n, 52, 8, 12), device="cuda")
+            o1 = torch.empty((n, 26, 8, 12), device="cuda")
+            for _ in range(3):   # eager, capture + replay, replay
+                rt.check(rt.lib().isl_net_forward(g.h, rt.ptr(x), n, 64, 96, rt.ptr(o0), rt.ptr(o1), sh))
+            outs[(rnd, n)] = (o0, o1)
+    s.synchronize()
+    assert g.range_ok()
+    for n in range(1, 11):
+        rp, rh = eager.forward(x[:n])
+        torch.cuda.synchronize()
+        for rnd in range(2):
+            assert torch.equal(outs[(rnd, n)][0], rp) and torch.equal(outs[(rnd, n)][1], rh), (rnd, n)
 
 
 @pytest.mark.parametrize("n", [32, 40])   # >= one block per CU: the ranges run in one block

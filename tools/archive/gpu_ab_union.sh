@@ -1,6 +1,6 @@
 # A/B of the union-path variants per layer shape (ISLPOSE_X3_UNION=1 old loop,
 # 2 role-split loop + LDS epilogue, 4 = 2 with s_memtime stamps), parity with mode 2, bench A/B.
-# usage: bash tools/gpu_ab_union.sh <tag> [bench]
+# usage: bash tools/archive/gpu_ab_union.sh <tag> [bench]
 export TMPDIR=/tmp
 T=${1:-ab}; O=gpurun_out/$T; mkdir -p $O
 CB=tools/convbench

@@ -1,5 +1,5 @@
 # One GPU call: parity tests, smoke, bench (with CPU baseline), kernel-trace profile.
-# usage: bash tools/gpu_check.sh <tag>
+# usage: bash tools/archive/gpu_check.sh <tag>
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:-chk}; O=gpurun_out/$T; mkdir -p $O

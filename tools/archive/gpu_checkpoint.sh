@@ -1,5 +1,5 @@
 # Checkpoint: the -m gpu suite, the default bench line, Mode R at batch 1 and 32, and the C3/C4/C5 configs.
-# usage: bash tools/gpu_checkpoint.sh <tag>   (outputs under gpurun_out/<tag>)
+# usage: bash tools/archive/gpu_checkpoint.sh <tag>   (outputs under gpurun_out/<tag>)
 T=${1:-ck}; O=gpurun_out/$T; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/gputest.log 2>&1
 rc=$?

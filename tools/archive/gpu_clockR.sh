@@ -1,5 +1,5 @@
 # Effective clock and MFMA busy of the conv kernels in Mode R batch 32 (net 184x328), DEEP off / on:
-# kernel trace (durations) + one SQ/GRBM pass each.  usage: bash tools/gpu_clockR.sh <tag>
+# kernel trace (durations) + one SQ/GRBM pass each.  usage: bash tools/archive/gpu_clockR.sh <tag>
 export TMPDIR=/tmp
 T=${1:-clkr}; O=gpurun_out/$T; mkdir -p $O
 B="python3 bench.py --scale 0.5 --no-cpu --no-mode-r --e2e-steps 0 --steps 10 --warmup 2"

@@ -1,4 +1,4 @@
-# Conv microbenchmarks + SQ counters (development).  usage: bash tools/gpu_convbench.sh <tag> [algos]
+# Conv microbenchmarks + SQ counters (development).  usage: bash tools/archive/gpu_convbench.sh <tag> [algos]
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:-cb}; A=${2:-x3,direct,wino}; O=gpurun_out/$T; mkdir -p $O

@@ -1,6 +1,6 @@
 # A/B: small grids with inputs and weights two K steps ahead (x3d, ISLPOSE_X3_DEEP=1) vs the
 # default 128-pixel loop (x3): bit-identity test, per-layer timings (Mode R 23x41, batch 32
-# and 1), then Mode R bench at batch 32 and 1.  usage: bash tools/gpu_deep.sh <tag> [bench]
+# and 1), then Mode R bench at batch 32 and 1.  usage: bash tools/archive/gpu_deep.sh <tag> [bench]
 T=${1:-deep}; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_body.py -x -v --timeout 300 --timeout-method thread \

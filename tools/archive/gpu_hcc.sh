@@ -1,5 +1,5 @@
 # Hand post (CC path) check: hand GPU tests, C5 (overlapped) and a hand-post timing on dense maps.
-# usage: bash tools/gpu_hcc.sh <tag>
+# usage: bash tools/archive/gpu_hcc.sh <tag>
 export TMPDIR=/tmp
 T=${1:-hcc}; O=gpurun_out/$T; mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest tests/test_gpu_hand.py -v --timeout 120 --timeout-method thread > $O/hand_tests.log 2>&1

@@ -1,6 +1,6 @@
 # A/B: the row union on 16x16x32 (x3m) vs 32x32x16 (x3), interleaved per layer shape, then the
 # M16 parity test and the bench with ISLPOSE_X3_M16=0/1.
-# usage: bash tools/gpu_m16.sh <tag>
+# usage: bash tools/archive/gpu_m16.sh <tag>
 T=${1:-m16}; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
 CB=tools/convbench

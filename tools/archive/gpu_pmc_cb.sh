@@ -1,4 +1,4 @@
-# SQ / TA / TCP counters of the conv microbenchmark.  usage: bash tools/gpu_pmc_cb.sh <tag> "<shape>" <algos>
+# SQ / TA / TCP counters of the conv microbenchmark.  usage: bash tools/archive/gpu_pmc_cb.sh <tag> "<shape>" <algos>
 set -o pipefail
 export TMPDIR=/tmp
 T=$1; S=$2; A=$3; O=gpurun_out/$T; mkdir -p $O

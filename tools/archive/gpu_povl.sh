@@ -1,6 +1,6 @@
 # Post overlap (--post-overlap: the post of batch k on its own stream beside the net of batch k+1) vs
 # post on the net's stream (default): the launch(post_stream) parity test, then Mode N,
-# Mode R batch 32 and batch 1, interleaved twice.  usage: bash tools/gpu_povl.sh <tag>
+# Mode R batch 32 and batch 1, interleaved twice.  usage: bash tools/archive/gpu_povl.sh <tag>
 T=${1:-povl}; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_body.py -x -v --timeout 300 --timeout-method thread \

@@ -1,4 +1,4 @@
-# parity tests (body) + bench (x3) + kernel trace.  usage: bash tools/gpu_quick.sh <tag>
+# parity tests (body) + bench (x3) + kernel trace.  usage: bash tools/archive/gpu_quick.sh <tag>
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:-q}; O=gpurun_out/$T; mkdir -p $O

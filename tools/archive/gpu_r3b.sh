@@ -1,4 +1,4 @@
-# Round 3: split-K fold A/B at batch 1 (Mode R), then the 16x16x32 union A/B (tools/gpu_m16.sh).
+# Round 3: split-K fold A/B at batch 1 (Mode R), then the 16x16x32 union A/B (tools/archive/gpu_m16.sh).
 T=${1:-r3b}; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_body.py -x -q --timeout 120 --timeout-method thread \
@@ -19,4 +19,4 @@ for i in (1,2):
     d=json.load(open('$O/b1_fold%d_%d.json'%(f,i)))
     print('fold=%d'%f, d['value'], 'frac', d['roofline']['frac'])
 "
-bash tools/gpu_m16.sh $T
+bash tools/archive/gpu_m16.sh $T

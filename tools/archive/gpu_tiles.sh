@@ -1,5 +1,5 @@
 # Tile-family A/B per layer shape (default 512-px tiles vs ISLPOSE_X3_TILES=small).
-# usage: bash tools/gpu_tiles.sh <tag> [shapes-file]
+# usage: bash tools/archive/gpu_tiles.sh <tag> [shapes-file]
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:-tiles}; O=gpurun_out/$T; mkdir -p $O

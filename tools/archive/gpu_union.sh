@@ -1,5 +1,5 @@
 # Row-union staging A/B (VAR 512 vs the per-(pair, ky) runs), per layer shape.
-# usage: bash tools/gpu_union.sh <tag>
+# usage: bash tools/archive/gpu_union.sh <tag>
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:-union}; O=gpurun_out/$T; mkdir -p $O

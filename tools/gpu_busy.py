@@ -1,7 +1,7 @@
 """GPU busy fraction over the tail of a rocprofv3 kernel trace: the union of kernel
 intervals / wall span, for the kernels after the last gap longer than --skip-gap-ms
 (i.e. the last timed phase), plus the largest idle gaps.  usage:
-  python3 tools/gpu_busy.py run_kernel_trace.csv [--tail-s 2.0]"""
+  python3 tools/archive/gpu_busy.py run_kernel_trace.csv [--tail-s 2.0]"""
 import csv
 import sys
 

@@ -1,5 +1,13 @@
-"""Per-layer durations of the last bench step from a rocprofv3 kernel trace."""
+"""Per-layer durations of the last bench step from a rocprofv3 kernel trace.
+
+Kernel launches map onto the netspec convs in order; a fused Mconv6 -> Mconv7 launch
+(conv_x3_f16 with VAR bit 16, csrc/conv_x3.hip) covers two convs and is counted as both
+(its row is labelled "pair"), so the rows stay aligned after the fusion.  Split-K reduces,
+pools and the post kernels are listed by name.  TF is the direct-conv count (fp32-eq) per
+second; a row above a third of the FP16 peak (838.9 TF-eq) cannot be real and is flagged.
+"""
 import csv
+import re
 import sys
 
 sys.path.insert(0, "isl-signlanguage-translation_amd")
@@ -23,21 +31,32 @@ def main(path, h=368, w=656, B=32, kind=0, quiet=False):
         n = r["Kernel_Name"]
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         tot += d
-        if "conv_mfma" in n or "wino_f23" in n or "conv_x3" in n or "wino_x3" in n:
+        if "conv_mfma" in n or "wino_f23" in n or "conv_x3_f16" in n or "conv_x3_rgb" in n or "wino_x3" in n:
+            targs = re.search(r"conv_x3_f16<([^>]*)>", n)
+            fused = bool(targs) and (int(targs.group(1).split(",")[5]) & 16) != 0
             c = convs[ci]
             fl = 2 * c.cout * c.cin * c.k * c.k * h * w * B
-            key = "%dx%d c%d->%d k%d %s" % (h, w, c.cin, c.cout, c.k, "WX" if "wino_x3" in n else ("W" if "wino" in n else ("X" if "x3" in n else "D")))
+            tag = "WX" if "wino_x3" in n else ("W" if "wino" in n else ("X" if "x3" in n else "D"))
+            if fused:   # Mconv6 and Mconv7 in one launch
+                c7 = convs[ci + 1]
+                fl += 2 * c7.cout * c7.cin * c7.k * c7.k * h * w * B
+                key = "%dx%d c%d->%d->%d k1 pair %s" % (h, w, c.cin, c.cout, c7.cout, tag)
+            else:
+                key = "%dx%d c%d->%d k%d %s" % (h, w, c.cin, c.cout, c.k, tag)
             g = groups.setdefault(key, [0, 0.0, 0.0])
             g[0] += 1; g[1] += d; g[2] += fl
             if c.name in ("conv1_2", "conv2_2", "conv3_4"):
                 h //= 2; w //= 2
-            ci += 1
+            ci += 2 if fused else 1
         else:
             g = groups.setdefault(n.split("(")[0][:40], [0, 0.0, 0.0])
             g[0] += 1; g[1] += d
     for k, (cnt, d, fl) in sorted(groups.items(), key=lambda t: -t[1][1]):
-        print("%-42s x%-3d %9.1f us  %5.1f%%  %s" % (k, cnt, d, 100 * d / tot, ("%.1f TF" % (fl / d / 1e6)) if fl else ""))
-    print("total %.1f us" % tot)
+        tf = fl / d / 1e6 if fl else 0.0
+        print("%-46s x%-3d %9.1f us  %5.1f%%  %s%s" % (k, cnt, d, 100 * d / tot, ("%.1f TF" % tf) if fl else "",
+                                                     "  (above the FP16 peak / 3: misaligned)" if tf > 838.9 else ""))
+    print("total %.1f us (sum of the rows: %.1f us), %d of %d convs mapped"
+          % (tot, sum(g[1] for g in groups.values()), ci, len(convs)))
 
 
 if __name__ == "__main__":

@@ -1,4 +1,4 @@
-"""Per-kernel averages of the counters collected by tools/gpu_pmc_cb.sh."""
+"""Per-kernel averages of the counters collected by tools/archive/gpu_pmc_cb.sh."""
 import collections
 import csv
 import glob

@@ -140,7 +140,7 @@ def main():
     p.add_argument("--traffic-out", default=None)
     p.add_argument("--sq", default=None, help="SQ/GRBM pass dir (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)")
     p.add_argument("--stats", default=None, help="kernel_stats.csv of the trace pass of the same command")
-    p.add_argument("--clock-ghz", type=float, default=None, help="in-kernel clock from a stamp build (tools/gpu_clock.sh)")
+    p.add_argument("--clock-ghz", type=float, default=None, help="in-kernel clock from a stamp build (tools/archive/gpu_clock.sh)")
     p.add_argument("--post-out", default=None, help="write the post kernels' traffic here (profiles/post_traffic.json)")
     a = p.parse_args()
     (fe, nfe), (wr, nwr) = load(a.fetch, "FETCH_SIZE"), load(a.write, "WRITE_SIZE")

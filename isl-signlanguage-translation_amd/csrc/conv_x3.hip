@@ -1584,6 +1584,25 @@ __global__ void __launch_bounds__(512) conv_x3_wr(X3Args a) {
   for (int wn = 0; wn < WN; ++wn)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[wn][r] = 0.f;
+#ifdef ISLPOSE_DEV
+  // development (tools/convbench, CONVBENCH_WRSTAMP=1): s_memtime phase stamps of wave 0 of every
+  // block -- start, first operands in, K loop done, ranges combined, stores issued -- and
+  // s_memrealtime at start and end (the clock)
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if (a.dbg && wave == 0 && lane == 0) {
+      if (k == 0 || k == 5) a.dbg[(size_t)blockIdx.x * 8 + (k == 0 ? 6 : 7)] = __builtin_amdgcn_s_memrealtime();
+      if (k < 5) a.dbg[(size_t)blockIdx.x * 8 + k] = __builtin_amdgcn_s_memtime();
+    }
+  };
+#else
+  auto stamp = [&](int) __attribute__((always_inline)) {};
+#endif
+  stamp(0);
+  // the epilogue's bias / slopes requested before the K loop (its first group: the only one
+  // when 4 WN <= S), not one memory round trip after the range sums meet
+  const int co_e = min(co0 + 8 * (wave & 3) + 4 * h, a.cout - 1) & ~3;
+  const f32x4 bias_e = *(const f32x4*)(a.bias + co_e);
+  const f32x4 slope_e = a.act == ACT_PRELU ? *(const f32x4*)(a.slope + co_e) : f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int u, const f16x8 (&Ad)[2], const f32x4 (&Bd)[WN][2]) __attribute__((always_inline)) {
     const int pr = u / TP;
     const bool real = 2 * (c2a + pr) + h < a.cin_chunks;   // a missing odd chunk: zeros
@@ -1597,16 +1616,27 @@ __global__ void __launch_bounds__(512) conv_x3_wr(X3Args a) {
       acc[wn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ad[1], bh, acc[wn], 0, 0, 0);
     }
   };
+  // Slot d's loads are issued in slot order (sched_barrier: the scheduler must not reorder them
+  // across slots, or the wait-count pass sees a slot's registers loaded last in the prologue and
+  // drains the pipeline at the loop head), so at slot d's compute DEPTH - 1 slots of loads stay
+  // in flight (vmcnt((DEPTH - 1) * (2 + 2 WN)), counted by the compiler).
 #pragma unroll
-  for (int d = 0; d < DEPTH; ++d) load(d, A[d], B[d]);
+  for (int d = 0; d < DEPTH; ++d) {
+    load(d, A[d], B[d]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   for (int u0 = 0; u0 < U; u0 += DEPTH) {
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {
       if (u0 + d < U) compute(u0 + d, A[d], B[d]);   // (uniform)
+      if (u0 == 0 && d == 0) stamp(1);
+      __builtin_amdgcn_sched_barrier(0);
       load(u0 + d + DEPTH, A[d], B[d]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
+  stamp(2);
   // the ranges' sums through LDS: [range][wn][q][lane] x 4 floats (registers 4q .. 4q + 3)
   __shared__ f32x4 xch[8 * WN * 4 * 64];
 #pragma unroll
@@ -1616,6 +1646,7 @@ __global__ void __launch_bounds__(512) conv_x3_wr(X3Args a) {
       xch[((wave * WN + wn) * 4 + q) * 64 + lane] =
           f32x4{acc[wn][4 * q], acc[wn][4 * q + 1], acc[wn][4 * q + 2], acc[wn][4 * q + 3]};
   __syncthreads();
+  stamp(3);
   // x3_canonical_order over the (wn, q) groups, spread over the waves; then x3_splitk_reduce's
   // epilogue
   const int hh = (S + 1) / 2, Wo = a.W + 2 * a.out_pad;
@@ -1635,8 +1666,9 @@ __global__ void __launch_bounds__(512) conv_x3_wr(X3Args a) {
     }
     const f32x4 sum = S > hh ? lo + hi : lo;
     if (m > mlast || co >= a.cout) continue;
-    const f32x4 b = *(const f32x4*)(a.bias + co);
-    const f32x4 sl = a.act == ACT_PRELU ? *(const f32x4*)(a.slope + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool first = g == wave;               // the group whose operands were prefetched
+    const f32x4 b = first ? bias_e : *(const f32x4*)(a.bias + co);
+    const f32x4 sl = first ? slope_e : a.act == ACT_PRELU ? *(const f32x4*)(a.slope + co) : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 v;
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = sum[e] * a.wscale_inv + b[e];
@@ -1659,6 +1691,8 @@ __global__ void __launch_bounds__(512) conv_x3_wr(X3Args a) {
         if (co + e < a.cout) oc[e] = v[e];
     }
   }
+  stamp(4);
+  stamp(5);
   if (bad) atomicOr(a.range_flag, 1);
 }
 
@@ -2314,10 +2348,11 @@ double conv_x3_fused67_mfma_flops(const ConvLaunch& c) {
 }
 
 
-// conv_x3_wr for the launches whose K ranges would run across blocks (x3_ranges), by default;
-// ISLPOSE_X3_WR=0: the split-K launches + x3_splitk_reduce (A/B), =2: also the small grids
-// without K ranges (one wave per block summing the whole K; A/B); ISLPOSE_X3_WR_WN=2: 64-pixel
-// tiles (two 32-pixel accumulator tiles per wave sharing the weight fragments).  Read per launch.
+// conv_x3_wr for the launches whose K ranges would run across blocks (x3_ranges), by default
+// those with at most 4 ranges; ISLPOSE_X3_WR=0: the split-K launches + x3_splitk_reduce (A/B),
+// =2: also the small grids without K ranges (one wave per block summing the whole K; A/B), =3:
+// every range count; ISLPOSE_X3_WR_WN=2: 64-pixel tiles (two 32-pixel accumulator tiles per wave
+// sharing the weight fragments).  Read per launch.
 static int x3_wr_mode() {
   const char* e = getenv("ISLPOSE_X3_WR");
   return e ? atoi(e) : 1;
@@ -2354,6 +2389,7 @@ static hipError_t launch_wr_t(const ConvLaunch& c, int S, hipStream_t s) {
   a.ksplit = S;
   a.nfr = c.n;
   a.bco_pack = c.bco;
+  a.dbg = c.dbg;   // development stamps (tools/convbench); never set by the runtime
   const long long nb = (long long)c.n * a.px_tiles * a.co_tiles;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3_wr: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
@@ -2366,9 +2402,9 @@ static hipError_t launch_x3_wr(const ConvLaunch& c, int S, hipStream_t s) {
   const char* e = getenv("ISLPOSE_X3_WR_WN");
   const bool wn2 = e && e[0] == '2';
   switch (c.ks) {
-    case 1: return wn2 ? launch_wr_t<1, 2, 6>(c, S, s) : launch_wr_t<1, 1, 8>(c, S, s);
-    case 3: return wn2 ? launch_wr_t<3, 2, 6>(c, S, s) : launch_wr_t<3, 1, 8>(c, S, s);
-    case 7: return wn2 ? launch_wr_t<7, 2, 6>(c, S, s) : launch_wr_t<7, 1, 8>(c, S, s);
+    case 1: return wn2 ? launch_wr_t<1, 2, 8>(c, S, s) : launch_wr_t<1, 1, 12>(c, S, s);
+    case 3: return wn2 ? launch_wr_t<3, 2, 8>(c, S, s) : launch_wr_t<3, 1, 12>(c, S, s);
+    case 7: return wn2 ? launch_wr_t<7, 2, 8>(c, S, s) : launch_wr_t<7, 1, 12>(c, S, s);
   }
   set_error("conv_x3_wr: unsupported kernel size");
   return hipErrorInvalidValue;
@@ -2379,8 +2415,12 @@ hipError_t launch_conv_x3(const ConvLaunch& c0, hipStream_t s) {
   ConvLaunch c = c0;
   const X3Ranges r = x3_ranges(c);
   c.ksplit = r.S;
-  if (r.across_blocks && x3_wr_mode() >= 1 && !c.fold_out) return launch_x3_wr(c, r.S, s);
-  if (x3_wr_mode() >= 2 && r.S == 1 && c.ks <= 3 && !c.hpool && !c.vin && !c.fold && !x3_big_tiles(c) &&
+  // wave ranges where a layer has at most 4 K ranges: with 8 a block's 8 waves load 2x the
+  // operand bytes per CU of the split-K blocks (no sharing between ranges), and in the net the
+  // c384 / c288 stage layers ran 20-35 % slower on it (profiles/r05/r5c/ops_*.txt)
+  if (r.across_blocks && !c.fold_out && (x3_wr_mode() >= 3 || (x3_wr_mode() >= 1 && r.S <= 4)))
+    return launch_x3_wr(c, r.S, s);
+  if (x3_wr_mode() == 2 && r.S == 1 && c.ks <= 3 && !c.hpool && !c.vin && !c.fold && !x3_big_tiles(c) &&
       x3_7x7_bpx(c) == 128)
     return launch_x3_wr(c, 1, s);
   if (r.across_blocks) {

@@ -85,19 +85,39 @@ class ISLSignPos(object):
     def handpos(self, oriImg):
         return self._estimators()[1].estimate(np.ascontiguousarray(_as_numpy(oriImg), dtype=np.uint8))
 
-    def _hands(self, img, candidate, subset):
-        out = []
-        for x, y, w, is_left in util.handDetect(candidate, subset, img):
-            peaks = self.handpos(img[y:y + w, x:x + w, :])
-            peaks[:, 0] = np.where(peaks[:, 0] == 0, peaks[:, 0], peaks[:, 0] + x)
-            peaks[:, 1] = np.where(peaks[:, 1] == 0, peaks[:, 1], peaks[:, 1] + y)
-            out.append(peaks)
-        return out
-
     def call(self, oriImg):
-        img = _as_numpy(oriImg)
-        candidate, subset = self.bodypos(img)
-        return (candidate, subset, self._hands(img, candidate, subset))
+        """ISL_Model_parameter.py:51-60 on one frame (the extract_features_mp.py:125-130 /
+        demo pattern): body pose, handDetect, hand peaks per crop offset into the frame.  The
+        frame goes to the GPU once (_upload) and every hand crop of it runs as one batch per
+        scale (HandEstimator.estimate_crops) instead of one 4-scale chain per crop in turn; the
+        results equal the reference's per-crop handpos (tests/test_gpu_configs.py)."""
+        return self.call_batch(self._upload(oriImg))[0]
+
+    def _upload(self, img):
+        """One host frame [H, W, 3] -> cuda uint8 [1, H, W, 3] BGR.  The scripts pass
+        frame[:, :, ::-1] of a decoded RGB frame (extract_features_mp.py:130): that view is
+        uploaded as the contiguous RGB buffer it reverses and flipped on the GPU, not copied
+        into a contiguous BGR array on the host first; the copy goes through a reused pinned
+        buffer (one memcpy, then a DMA) instead of a pageable upload."""
+        body = self._estimators()[0]
+        dev = torch.device("cuda:%d" % body.device)
+        if isinstance(img, torch.Tensor) and img.is_cuda:
+            return img.to(dev).contiguous()[None]
+        a = _as_numpy(img)
+        flip = a.ndim == 3 and a.shape[2] == 3 and a.strides[2] < 0 and a[:, :, ::-1].flags.c_contiguous
+        src = np.ascontiguousarray(a[:, :, ::-1] if flip else a, dtype=np.uint8)
+        buf = getattr(self, "_pinned", None)
+        if buf is None or buf.numel() < src.size:
+            buf = self._pinned = torch.empty(src.size, dtype=torch.uint8, pin_memory=True)
+            self._pinned_ev = None
+        if self._pinned_ev is not None:
+            self._pinned_ev.synchronize()          # the previous upload has left the buffer
+        host = buf[:src.size].view(src.shape)
+        np.copyto(host.numpy(), src)
+        t = host.to(dev, non_blocking=True)
+        self._pinned_ev = torch.cuda.Event()
+        self._pinned_ev.record(torch.cuda.current_stream(dev))
+        return (t.flip(-1) if flip else t)[None]
 
     __call__ = call
 

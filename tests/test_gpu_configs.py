@@ -156,3 +156,35 @@ def test_c5_pipeline_1080p_json_vs_oracle(tmp_path, hand_w):
     im, _, _ = cpu_ref.net_input(bgr[0], 0.5 * 368 / 1080)
     rp, rh = cpu_ref.make_net_fn("body25", wb)(im)
     assert _rel(pafs[0][0:1].cpu().numpy(), rp) < TOL and _rel(heats[0][0:1].cpu().numpy(), rh) < TOL
+
+
+def test_isl_call_per_frame_1080p_equals_batch_and_per_crop(hand_w):
+    """The unchanged scripts' per-frame call (extract_features_mp.py:125-130:
+    model(frame[:, :, ::-1]) on one 1080x1920 frame at a time) == call_batch over the same frames
+    == the reference's composition (Body, handDetect, Hand per crop, offsets;
+    ISL_Model_parameter.py:51-60) bit for bit, with hand crops present."""
+    from src import util
+    from src.body import Body
+    from src.hand import Hand
+    from src.ISL_Model_parameter import ISLSignPos
+    rgb = synth.synth_frames(3, 1080, 1920, seed=58)
+    bgr = np.ascontiguousarray(rgb[..., ::-1])
+    wb = _tame.tame_body(synth.synth_weights(0), bgr[0], scale=0.5 * 368 / 1080, gain=0.05)
+    tw = lambda d: {k: torch.from_numpy(v) for k, v in d.items()}  # noqa: E731
+    body, hand = Body(tw(wb), "body25"), Hand(tw(hand_w))
+    isl = ISLSignPos(body.model, hand.model)
+    batch = isl.call_batch(bgr)
+    n_hands = 0
+    for i in range(3):
+        cand, subset, hands = isl.call(rgb[i][:, :, ::-1])       # a non-contiguous view, as the script
+        c2, s2, h2 = batch[i]
+        assert np.array_equal(cand, c2) and np.array_equal(subset, s2) and len(hands) == len(h2)
+        boxes = util.handDetect(cand, subset, bgr[i])
+        assert len(boxes) == len(hands)
+        for (x, y, w, _), pk, pb in zip(boxes, hands, h2):
+            ref = hand(bgr[i, y:y + w, x:x + w])
+            ref[:, 0] = np.where(ref[:, 0] == 0, ref[:, 0], ref[:, 0] + x)
+            ref[:, 1] = np.where(ref[:, 1] == 0, ref[:, 1], ref[:, 1] + y)
+            assert np.array_equal(pk, ref) and np.array_equal(pk, pb)
+        n_hands += len(hands)
+    assert n_hands >= 1, "the tamed weights should produce hand crops"

@@ -9,6 +9,10 @@
 
   C5  the video -> JSON pipeline (islpose.pipeline) on 1080x1920 RGB frames, body
       (Mode R) + batched hand crops + per-frame JSON files, sequential vs overlapped.
+  FRAME  the unchanged scripts' per-frame path: ISLSignPos.call on one 1080x1920 frame at a
+      time (extract_features_mp.py:125-130, model(frame[:, :, ::-1])), with the C5 tamed body
+      weights (hand crops up to ~1000 px); wall time per call, split into the body part
+      (bodypos + handDetect on the same frames) and the hand part (the rest).
   C6  translator head: the HIP sign classifier (csrc/sign.hip) on [B, 20, 156]
       windows -- latency of one window (the demo's per-frame call) and throughput
       of a batch of 4096 windows; plus translate_stream over a 64-frame clip
@@ -176,6 +180,50 @@ def c5(args):
     return res
 
 
+def frame(args):
+    """ISLSignPos.call per frame, 1080x1920 RGB frames flipped to BGR as a view (the script's
+    frame[:, :, ::-1]); every call returns to the host (numpy results), as in the script."""
+    from islpose import synth
+    from islpose.body import BodyEstimator
+    from src import util
+    from src.body import Body
+    from src.hand import Hand
+    from src.ISL_Model_parameter import ISLSignPos
+    T, H, W = args.frame_count, 1080, 1920
+    rgb = synth.synth_frames(T, H, W, seed=57)
+    wb = synth.synth_weights(0)
+    cal = BodyEstimator(wb, "body25", scale_search=(0.5,))
+    _, _, heats = cal.run_scales(torch.from_numpy(np.ascontiguousarray(rgb[:1, ..., ::-1])).cuda(), keep_maps=True)
+    wb = synth.tame_heat_layer(wb, heats[0].cpu().numpy(), "body25", gain=0.05)
+    del cal
+    tw = lambda d: {k: torch.from_numpy(v) for k, v in d.items()}  # noqa: E731
+    isl = ISLSignPos(Body(tw(wb), "body25").model, Hand(tw(synth.synth_weights(2))).model)
+    body = isl._estimators()[0]
+    for i in range(min(5, T)):          # warm-up: arenas of the body and of the hand crop sizes
+        isl.call(rgb[i][:, :, ::-1])
+    torch.cuda.synchronize()
+    crops, widths = 0, []
+    t0 = time.perf_counter()
+    for i in range(T):
+        _, _, hands = isl.call(rgb[i][:, :, ::-1])
+        crops += len(hands)
+    dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for i in range(T):
+        f = rgb[i][:, :, ::-1]
+        (c, sb), = body.estimate(isl._upload(f))
+        widths += [w for _, _, w, _ in util.handDetect(c, sb, f)]
+    db = time.perf_counter() - t0
+    return {"config": "FRAME ISLSignPos.call per 1080x1920 frame (extract_features_mp.py:130 pattern)",
+            "frames": T, "frames_per_s": round(T / dt, 2), "ms_per_frame": round(dt / T * 1e3, 3),
+            "body_ms_per_frame": round(db / T * 1e3, 3), "hand_ms_per_frame": round((dt - db) / T * 1e3, 3),
+            "hand_crops_per_frame": round(crops / T, 2),
+            "crop_width_px": [int(min(widths)), int(max(widths))] if widths else [],
+            "basis": "wall time of T sequential calls (host frame -> pinned H2D -> GPU flip -> body net + post -> "
+                     "handDetect -> hand crops batched per scale -> peaks on the host); body = upload + estimate + "
+                     "handDetect on the same frames, hand = the rest"}
+
+
 def c6(args):
     from islpose import synth, translate
     from src.body import Body
@@ -213,7 +261,8 @@ def c6(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", choices=["c3", "c4", "c5", "c6", "all"], default="all")
+    ap.add_argument("--config", choices=["c3", "c4", "c5", "c6", "frame", "all"], default="all")
+    ap.add_argument("--frame-count", type=int, default=64, help="FRAME: sequential per-frame calls timed")
     ap.add_argument("--batch", type=int, default=16, help="C3 / C4 frames per step")
     ap.add_argument("--c5-batch", type=int, default=32, help="C5 frames per pipeline batch")
     ap.add_argument("--steps", type=int, default=3)
@@ -224,7 +273,7 @@ def main():
     ap.add_argument("--raw-hand-maps", dest="designed_hands", action="store_false",
                     help="C3: run the hand post on the raw net maps instead of designed maps")
     a = ap.parse_args()
-    for name, fn in (("c3", c3), ("c4", c4), ("c5", c5), ("c6", c6)):
+    for name, fn in (("c3", c3), ("c4", c4), ("c5", c5), ("c6", c6), ("frame", frame)):
         if a.config in (name, "all"):
             print(json.dumps(fn(a)), flush=True)
 

@@ -89,6 +89,14 @@ int main(int argc, char** argv) {
     CK(hipMemset(dbg, 0, ((size_t)16 * T * 4 + 4) * 8));
     L.dbg = dbg;
   }
+  // CONVBENCH_WRSTAMP=1: phase stamps of the wave-range kernel (conv_x3_wr, wave 0 of every block)
+  const bool wrstamp = getenv("CONVBENCH_WRSTAMP") && atoi(getenv("CONVBENCH_WRSTAMP"));
+  const size_t wr_blocks = 1 << 16;
+  if (wrstamp) {
+    CK(hipMalloc(&dbg, wr_blocks * 8 * 8));
+    CK(hipMemset(dbg, 0, wr_blocks * 8 * 8));
+    L.dbg = dbg;
+  }
   const double flops = 2.0 * cout * cin * ks * ks * (double)H * W * n;
   // the polluter of CONVBENCH_POLLUTE: a 1x1 layer on the same buffers (cin chunks of this
   // shape, 32 output channels), default variant
@@ -160,7 +168,24 @@ int main(int argc, char** argv) {
              flops / us / 1e6, fac * flops / us / 1e6);
     }
   }
-  if (dbg) {
+  if (dbg && wrstamp) {
+    std::vector<unsigned long long> h(wr_blocks * 8);
+    CK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    double ph[4] = {0, 0, 0, 0}, t0min = 1e300, t0max = 0, t4max = 0, clk = 0;
+    int nb = 0;
+    for (size_t b = 0; b < wr_blocks && h[b * 8]; ++b, ++nb) {
+      for (int k = 0; k < 4; ++k) ph[k] += (double)h[b * 8 + k + 1] - (double)h[b * 8 + k];
+      t0min = std::min(t0min, (double)h[b * 8]);
+      t0max = std::max(t0max, (double)h[b * 8]);
+      t4max = std::max(t4max, (double)h[b * 8 + 4]);
+      const double dr = (double)h[b * 8 + 7] - (double)h[b * 8 + 6];
+      if (dr > 0) clk += ((double)h[b * 8 + 4] - (double)h[b * 8]) / dr * 0.1;
+    }
+    if (nb)
+      printf("  wr stamps (%d blocks, cycles, mean): first operands %.0f, K loop %.0f, combine %.0f, epilogue %.0f; "
+             "block starts spread %.0f, first start to last end %.0f; clock %.2f GHz\n", nb, ph[0] / nb, ph[1] / nb,
+             ph[2] / nb, ph[3] / nb, t0max - t0min, t4max - t0min, clk / nb);
+  } else if (dbg) {
     // per step: issue (0->1), compute (1->2), store (2->3), barrier (3 -> next 0), for
     // the earliest and latest wave, averaged over the steps of the last launch
     std::vector<unsigned long long> h((size_t)16 * T * 4 + 4);

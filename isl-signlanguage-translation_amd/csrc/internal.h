@@ -74,6 +74,7 @@ struct ConvLaunch {
   // by folding consumers, so its x3_splitk_reduce launch is skipped (a producer).
   const X3Fold* fold = nullptr;
   int fold_out = 0;
+
   // The fused 1x1 pair (conv_x3 VAR 16; Mconv6 -> Mconv7 of a stage, model.py:108-109):
   // cout7 > 0 makes this launch the pair.  The fields above describe Mconv6 (wx3 packed for a
   // tile of all its cout channels) with `out` / out_* describing Mconv7's output; these
@@ -117,6 +118,11 @@ bool x3_vin_ok(const ConvLaunch& c);
 bool x3_rgb_fits(const ConvLaunch& c);
 hipError_t launch_conv_x3_rgb(const ConvLaunch& c, hipStream_t s);
 double conv_x3_rgb_mfma_flops(const ConvLaunch& c);
+// conv1_1 -> conv1_2 -> pair-max (conv_c12.hip): l1 = conv1_1 (rgb-packed wx3), l2 = conv1_2 with
+// its hpool output
+bool x3_c12_fits(const ConvLaunch& l1, const ConvLaunch& l2);
+hipError_t launch_conv_x3_c12(const ConvLaunch& l1, const ConvLaunch& l2, hipStream_t s);
+double conv_x3_c12_mfma_flops(const ConvLaunch& l1);
 hipError_t launch_conv_x3(const ConvLaunch& c, hipStream_t s);
 bool x3_fits(const ConvLaunch& c);
 // whether launch_conv_x3 can run c with hpool (even W, not split across blocks)
@@ -129,6 +135,8 @@ double conv_x3_mfma_flops(const ConvLaunch& c);
 // (ks / 2) at bits 29-30.
 constexpr int X3V_RGB = 1 << 18;
 constexpr int X3V_FOLD_OUT = 1 << 19;   // a split-K producer whose reduce was folded into its consumers
+constexpr int X3V_C12 = 4;              // conv1_1 -> conv1_2 -> pair-max in one launch (conv_c12.hip)
+
 constexpr int x3_variant_code(int var, int ks, int bpx, int bco) {
   return (var & 0xfffff) | ((bpx / 32) << 20) | ((bco / 32) << 25) | ((ks / 2) << 29);
 }

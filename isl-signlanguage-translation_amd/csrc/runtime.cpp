@@ -628,14 +628,22 @@ static void plan_fuse67(isl_net* net) {
     if (net->out0.buf == a.out || (net->n_out > 1 && net->out1.buf == a.out)) continue;
     // the value op k writes is read by op k + 1 only: no later op reads the buffer before the
     // next op that writes it (every stage's Mconv6 reuses one buffer)
+    // channel by channel: a later op may read the buffer only where a later write has replaced
+    // op k's value (the fused launch never writes Mconv6's channels)
     bool other = false;
-    for (size_t j = k + 2; j < net->ops.size(); ++j) {
+    std::vector<char> live(la.cout, 1);
+    int n_live = la.cout;
+    for (size_t j = k + 2; j < net->ops.size() && n_live > 0 && !other; ++j) {
       const Op& o = net->ops[j];
-      if (o.in == a.out) { other = true; break; }
-      // only a write of every channel op k wrote ends its live range; after a partial one a
-      // later reader could still see channels the fused launch never writes
-      const int wc = o.type == 0 ? net->layers[o.layer].cout : o.C;
-      if (o.out == a.out && o.out_coff == 0 && wc >= la.cout) break;
+      if (o.in == a.out) {
+        const int rc = o.type == 0 ? net->layers[o.layer].cin_phys : o.C;
+        for (int ch = std::max(0, o.in_coff); ch < std::min(la.cout, o.in_coff + rc); ++ch) other |= live[ch] != 0;
+      }
+      if (o.out == a.out) {
+        const int wc = o.type == 0 ? net->layers[o.layer].cout : o.C;
+        for (int ch = std::max(0, o.out_coff); ch < std::min(la.cout, o.out_coff + wc); ++ch)
+          if (live[ch]) { live[ch] = 0; --n_live; }
+      }
     }
     if (other) continue;
     a.fuse67 = true;
@@ -977,6 +985,13 @@ static bool rgb_kernel_enabled() {
   return !(e && e[0] == '0');
 }
 
+// conv1_1 -> conv1_2 -> the pool's pair-max in one launch (conv_c12.hip); ISLPOSE_C12=0: the two
+// convs as their own launches (A/B; read per run)
+static bool c12_enabled() {
+  const char* e = getenv("ISLPOSE_C12");
+  return !(e && e[0] == '0');
+}
+
 // ISLPOSE_FUSED_POOL=0: the plain conv + maxpool2 path (A/B; read per run, so a test
 // can compare both in one process)
 static bool fused_pool_enabled() {
@@ -1217,6 +1232,47 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
       continue;
     }
 
+    // conv1_1 (rgb kernel) -> conv1_2 -> pool: both convs in one launch writing the pool's
+    // pair-max buffer, where conv1_1's output feeds conv1_2 only (conv_c12.hip)
+    if (net->algo == ISL_ALGO_X3 && op.type == 0 && vin_buf < 0 && fuse_pools && c12_enabled() &&
+        k + 2 < net->ops.size() && net->layers[op.layer].d_wrgb && rgb_kernel_enabled()) {
+      const Op& o2 = net->ops[k + 1];
+      const Op& pl = net->ops[k + 2];
+      bool only = o2.type == 0 && o2.in == op.out && o2.in_coff == 0 && op.out_coff == 0 && pl.type == 1 &&
+                  pl.in == o2.out && o2.out_coff == 0 && pl.hbuf >= 0 && net->out0.buf != op.out &&
+                  !(net->n_out > 1 && net->out1.buf == op.out);
+      for (size_t j = k + 2; only && j < net->ops.size(); ++j) {
+        if (net->ops[j].in == op.out) only = false;
+        if (net->ops[j].out == op.out) break;
+      }
+      ConvLaunch L1 = basic_launch(net, op), L2 = only ? basic_launch(net, o2) : ConvLaunch{};
+      if (only) {
+        L1.wx3 = net->layers[op.layer].d_wrgb;
+        const Act& hb = net->act[pl.hbuf];
+        L2.out = hb.base; L2.out_pad = 0; L2.out_cs = hb.cs; L2.out_coff = 0;
+        L2.hpool = 1;
+        only = pl.C == L2.cout && x3_rgb_fits(L1) && x3_hpool_ok(L2) && x3_c12_fits(L1, L2);
+      }
+      if (only) {
+        HIP_OK(launch_conv_x3_c12(L1, L2, s));
+        net->op_variant[k] = x3_variant_code(X3V_C12, 3, 256, 64);
+        net->op_variant[k + 1] = -2;   // ran inside op k
+        if (tr) {
+          const ConvLayer& c1 = net->layers[op.layer];
+          const ConvLayer& c2 = net->layers[o2.layer];
+          tr->kind.push_back(3);
+          tr->flops.push_back(2.0 * L1.H * L1.W * L1.n * 9.0 * ((double)c1.cout * c1.cin + (double)c2.cout * c2.cin));
+          tr->mfma_flops.push_back(conv_x3_c12_mfma_flops(L1));
+          HIP_OK(hipEventRecord(tr->ev[k + 1], s));
+          tr->kind.push_back(0); tr->flops.push_back(0.0); tr->mfma_flops.push_back(0.0);
+          HIP_OK(hipEventRecord(tr->ev[k + 2], s));
+        }
+        fused = true;   // the pool op finds its pair-max buffer written
+        ++k;
+        continue;
+      }
+    }
+
     if (op.type == 1) {
       // deferred: the next conv either stages from the pair-max buffer or runs vpool2 first
       if (fused && pool_input && pool_into_next_conv(net, k)) { vin_buf = (int)k; net->op_variant[k] = -1; }
@@ -1347,7 +1403,7 @@ static const char* const kRunKeySwitches[] = {
     "ISLPOSE_X3_DEEP",   "ISLPOSE_RGB_CONV", "ISLPOSE_FUSED_POOL", "ISLPOSE_POOL_INPUT", "ISLPOSE_CONV_STAGING",
     "ISLPOSE_X3_TILES",  "ISLPOSE_X3_UNION", "ISLPOSE_X3_HALF64",  "ISLPOSE_X3_WIDE7",   "ISLPOSE_X3_ACROSS",
     "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67", "ISLPOSE_X3_G2", "ISLPOSE_X3_PX64", "ISLPOSE_X3_HALFSMALL",
-    "ISLPOSE_X3_WR",     "ISLPOSE_X3_WR_WN",
+    "ISLPOSE_X3_WR",     "ISLPOSE_X3_WR_WN", "ISLPOSE_C12",
 #ifdef ISLPOSE_DEV
     "ISLPOSE_X3_HALFCO", "ISLPOSE_X3_PPS2",  "ISLPOSE_X3_M16",     "ISLPOSE_X3_WINO",    "ISLPOSE_X3_ABL",
 #endif

@@ -179,7 +179,8 @@ def ptr(t) -> ctypes.c_void_p:
 
 
 def decode_variant(code: int) -> dict:
-    """isl_net_op_info's variant code -> dict(var=VAR bits, bpx, bco, ks, rgb, pool_fused)."""
+    """isl_net_op_info's variant code -> dict(var=VAR bits, bpx, bco, ks, rgb, pool_fused, ...):
+    wave_ranges (conv_x3_wr, VAR 8), c12 (conv1_1 -> conv1_2 in one launch, 4)."""
     if code == -1:
         return {"pool_fused": True}
     if code == -2:
@@ -192,7 +193,8 @@ def decode_variant(code: int) -> dict:
             "ks": 2 * ((code >> 29) & 3) + 1, "rgb": bool(code & (1 << 18)),
             "union": bool(code & 512), "ranged": bool(code & 1024), "split": bool(code & 2048),
             "pairs2": bool(code & 4096), "vin": bool(code & 32768), "sib": bool(code & 65536),
-            "fold": bool(code & 8192), "m16": bool(code & 131072), "fold_out": bool(code & (1 << 19))}
+            "fold": bool(code & 8192), "m16": bool(code & 131072), "fold_out": bool(code & (1 << 19)),
+            "wave_ranges": bool(code & 8), "c12": bool(code & 4)}
 
 
 class Net:

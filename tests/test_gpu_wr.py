@@ -110,3 +110,4 @@ def test_wr_7x7_equals_split_reduce(kind, h, w, n, monkeypatch):
     ref = ref if isinstance(ref, tuple) else (ref,)
     for a, r in zip(o1, ref):
         assert _rel(a.cpu().numpy(), r) < TOL
+

@@ -107,14 +107,22 @@ __global__ void __launch_bounds__(NT, 4) conv_x3_c12(C12Args a) {
     s_p[128 + i] = a.act1 == ACT_PRELU ? a.sl1[i] : 0.f;
     s_p[192 + i] = a.act2 == ACT_PRELU ? a.sl2[i] : 0.f;
   }
-  // conv1_2 weight slab of step s (pair s / 3, kernel row s % 3) into buffer b by LDS-DMA
-  auto issue_w = [&](int st, int b) __attribute__((always_inline)) {
+  // conv1_2 weight slab of step s (pair s / 3, kernel row s % 3): register-staged one step ahead
+  // (loads at the step's top, LDS stores at its end), so the load latency hides behind the
+  // step's MFMAs; an LDS-DMA slab would be drained at once (hipcc orders every LDS read after
+  // an LDS-DMA in flight)
+  f16x8 wreg[2];
+  auto load_w = [&](int st) __attribute__((always_inline)) {
     const f16x8* src = a.w2 + (size_t)st * WSL;
-    for (int q = wave; q < WSL / 64; q += NT / 64)
-      __builtin_amdgcn_global_load_lds((const void*)(src + q * 64 + lane),
-                                       (__attribute__((address_space(3))) void*)(&s_w[b][q * 64]), 16, 0, 0);
+    wreg[0] = src[tid];
+    if (tid < WSL - NT) wreg[1] = src[NT + tid];
   };
-  issue_w(0, 0);
+  auto store_w = [&](int b) __attribute__((always_inline)) {
+    s_w[b][tid] = wreg[0];
+    if (tid < WSL - NT) s_w[b][NT + tid] = wreg[1];
+  };
+  load_w(0);
+  store_w(0);
   // the input region every halo pixel's 3 x 3 neighbourhood reads, once for both channel halves
   // (clamped into the padded plane: only out-of-image halo pixels, zeroed below, read the clamps)
   for (int i = tid; i < (TH + 4) * (TW + 4); i += NT) {
@@ -192,7 +200,7 @@ __global__ void __launch_bounds__(NT, 4) conv_x3_c12(C12Args a) {
     // ---- conv1_2 pairs 2 hf, 2 hf + 1 (6 steps of (pair, ky)) from the resident halo
     for (int i = 0; i < 6; ++i) {
       const int st = 6 * hf + i, b = st & 1;
-      if (st + 1 < 12) issue_w(st + 1, b ^ 1);
+      if (st + 1 < 12) load_w(st + 1);
       const int pp = i / 3, ky = i - 3 * pp;
       const f16x8* sw = &s_w[b][h * 64 + l32];
       const f16x8* sx = &s_x[0][2 * pp + h][(wave + ky) * HWD + l32];
@@ -212,7 +220,8 @@ __global__ void __launch_bounds__(NT, 4) conv_x3_c12(C12Args a) {
           acc2[wm] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[wm][1], B[0], acc2[wm], 0, 0, 0);
         }
       }
-      __syncthreads();   // the next slab has landed; this one may be overwritten
+      if (st + 1 < 12) store_w(b ^ 1);   // buffer b ^ 1 was last read in the previous step
+      __syncthreads();   // the next slab is in LDS; this one may be overwritten
     }
   }
   // ---- conv1_2's epilogue with the pair-max of the pool (conv_x3_f16 hpool)

@@ -822,10 +822,12 @@ static int upload_params(isl_net* net) {
   if (!net->d_flag) {
     HIP_OK(hipMalloc(&net->d_flag, sizeof(int)));
     HIP_OK(hipMemset(net->d_flag, 0, sizeof(int)));
+    HIP_OK(hipDeviceSynchronize());   // ordered before the next run on a non-blocking stream
   }
   if (!net->d_trips) {
     HIP_OK(hipMalloc(&net->d_trips, sizeof(unsigned long long)));
     HIP_OK(hipMemset(net->d_trips, 0, sizeof(unsigned long long)));
+    HIP_OK(hipDeviceSynchronize());
   }
   net->packed = true;
   return ISL_OK;
@@ -936,6 +938,10 @@ static int plan(isl_net* net, int n, int h, int w) {
     }
     HIP_OK(hipMalloc(&ar.base, ar.bytes));
     HIP_OK(hipMemset(ar.base, 0, ar.bytes));  // zero rings and gap channels, once
+    // hipMemset runs on the null stream, which the callers' non-blocking streams do not wait
+    // for: a first run on another stream (the pyramid's scales, the hand scales) could otherwise
+    // start writing the arena while the zeroing is still in flight and have its outputs erased
+    HIP_OK(hipDeviceSynchronize());
     net->plans_bytes += ar.bytes;
     it = net->plans.emplace(key, std::move(ar)).first;
   }
@@ -1863,6 +1869,7 @@ int isl_net_check(isl_net* net, int clear) {
   HIP_OK(hipMemcpy(&f, net->d_flag, sizeof(int), hipMemcpyDeviceToHost));
   if (f && clear) {
     HIP_OK(hipMemset(net->d_flag, 0, sizeof(int)));
+    HIP_OK(hipDeviceSynchronize());   // cleared before the next run on a non-blocking stream
     ++net->range_trips_host;   // one trip per cleared flag (a check without clear counts nothing)
   }
   if (f) return fail(ISL_E_RANGE, "an activation left the split-fp16 range (|x| >= 65504); re-run with ISL_ALGO_DIRECT");

@@ -2415,10 +2415,12 @@ hipError_t launch_conv_x3(const ConvLaunch& c0, hipStream_t s) {
   ConvLaunch c = c0;
   const X3Ranges r = x3_ranges(c);
   c.ksplit = r.S;
-  // wave ranges where a layer has at most 4 K ranges: with 8 a block's 8 waves load 2x the
-  // operand bytes per CU of the split-K blocks (no sharing between ranges), and in the net the
-  // c384 / c288 stage layers ran 20-35 % slower on it (profiles/r05/r5c/ops_*.txt)
-  if (r.across_blocks && !c.fold_out && (x3_wr_mode() >= 3 || (x3_wr_mode() >= 1 && r.S <= 4)))
+  // wave ranges where a 1x1 / 3x3 layer has at most 4 K ranges: with 8 a block's 8 waves load 2x
+  // the operand bytes per CU of the split-K blocks (no sharing between ranges), and in the net the
+  // c384 / c288 stage layers ran 20-35 % slower on it (profiles/r05/r5c/ops_*.txt); a 7x7 range
+  // is 98 taps long for one wave (the hand's 184-pixel scale: C3 109.4 -> 107.5 frames/s on it,
+  // profiles/r05/r5n/)
+  if (r.across_blocks && !c.fold_out && (x3_wr_mode() >= 3 || (x3_wr_mode() >= 1 && r.S <= 4 && c.ks <= 3)))
     return launch_x3_wr(c, r.S, s);
   if (x3_wr_mode() == 2 && r.S == 1 && c.ks <= 3 && !c.hpool && !c.vin && !c.fold && !x3_big_tiles(c) &&
       x3_7x7_bpx(c) == 128)

@@ -191,7 +191,7 @@ def test_c3_crop_batch_vs_oracle():
     four scales (reference src/hand.py:25-56 per crop).  Crops 0, 15 and 31: maps within 1e-4 of
     the oracle's net on the oracle's own crop input, peaks bit-exact with the oracle's post on
     those maps; the 7x7 tile size every scale ran (isl_net_op_info) is the grid-quantisation
-    choice for 32 crops (or the wave-range kernel where the K ranges run across blocks)."""
+    choice for 32 crops."""
     from islpose import runtime as rt
     B, H, W = 16, 368, 656
     frames = synth.synth_frames(B, H, W, seed=5)
@@ -214,10 +214,7 @@ def test_c3_crop_batch_vs_oracle():
         want = _x3_7x7_bpx(len(boxes), side)
         var = [rt.decode_variant(v) for name, v in net.op_variants() if name.startswith("Mconv") and "Mconv6" not in name
                and "Mconv7" not in name]
-        # (layers whose canonical K ranges run across blocks with <= 4 ranges take the wave-range
-        # kernel, conv_x3_wr, at its 32-pixel tiles)
-        assert len(var) == 25 and all(d["ks"] == 7 and (d["bpx"] == want or d.get("wave_ranges")) for d in var), \
-            (s, want, var[:2])
+        assert len(var) == 25 and all(d["ks"] == 7 and d["bpx"] == want for d in var), (s, want, var[:2])
     peaks = HandEstimator(net=net).post_crops(boxes, heats)
     fn = cpu_ref.make_net_fn("hand", wh)
     for i in (0, 15, 31):

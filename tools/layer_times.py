@@ -1,8 +1,9 @@
 """Per-layer durations of the last bench step from a rocprofv3 kernel trace.
 
 Kernel launches map onto the netspec convs in order; a fused Mconv6 -> Mconv7 launch
-(conv_x3_f16 with VAR bit 16, csrc/conv_x3.hip) covers two convs and is counted as both
-(its row is labelled "pair"), so the rows stay aligned after the fusion.  Split-K reduces,
+(conv_x3_f16 with VAR bit 16, csrc/conv_x3.hip) and the conv1_1 -> conv1_2 launch
+(conv_x3_c12, csrc/conv_c12.hip) cover two convs each and are counted as both (their rows are
+labelled "pair"), so the rows stay aligned after the fusions.  Split-K reduces,
 pools and the post kernels are listed by name.  TF is the direct-conv count (fp32-eq) per
 second; a row above a third of the FP16 peak (838.9 TF-eq) cannot be real and is flagged.
 """
@@ -31,21 +32,26 @@ def main(path, h=368, w=656, B=32, kind=0, quiet=False):
         n = r["Kernel_Name"]
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         tot += d
-        if "conv_mfma" in n or "wino_f23" in n or "conv_x3_f16" in n or "conv_x3_rgb" in n or "wino_x3" in n:
+        conv_kernels = ("conv_mfma", "wino_f23", "conv_x3_f16", "conv_x3_rgb", "conv_x3_wr", "conv_x3_c12", "wino_x3")
+        if any(k in n for k in conv_kernels):
             targs = re.search(r"conv_x3_f16<([^>]*)>", n)
-            fused = bool(targs) and (int(targs.group(1).split(",")[5]) & 16) != 0
+            # two convs in one launch: the fused 1x1 pair (VAR 16) or conv1_1 -> conv1_2 (conv_c12.hip)
+            fused = (bool(targs) and (int(targs.group(1).split(",")[5]) & 16) != 0) or "conv_x3_c12" in n
             c = convs[ci]
             fl = 2 * c.cout * c.cin * c.k * c.k * h * w * B
             tag = "WX" if "wino_x3" in n else ("W" if "wino" in n else ("X" if "x3" in n else "D"))
-            if fused:   # Mconv6 and Mconv7 in one launch
-                c7 = convs[ci + 1]
-                fl += 2 * c7.cout * c7.cin * c7.k * c7.k * h * w * B
-                key = "%dx%d c%d->%d->%d k1 pair %s" % (h, w, c.cin, c.cout, c7.cout, tag)
+            if "conv_x3_wr" in n:
+                tag += " wave-ranges"
+            if fused:
+                c2 = convs[ci + 1]
+                fl += 2 * c2.cout * c2.cin * c2.k * c2.k * h * w * B
+                key = "%dx%d c%d->%d->%d k%d pair %s" % (h, w, c.cin, c.cout, c2.cout, c2.k, tag)
             else:
                 key = "%dx%d c%d->%d k%d %s" % (h, w, c.cin, c.cout, c.k, tag)
             g = groups.setdefault(key, [0, 0.0, 0.0])
             g[0] += 1; g[1] += d; g[2] += fl
-            if c.name in ("conv1_2", "conv2_2", "conv3_4"):
+            last = convs[ci + 1] if fused else c
+            if last.name in ("conv1_2", "conv2_2", "conv3_4"):
                 h //= 2; w //= 2
             ci += 2 if fused else 1
         else:

@@ -98,7 +98,7 @@ def mfma_busy(sq_dir, stats_csv, sq_out, clock_ghz=None):
         k = n.split("(")[0].replace("void ", "").replace("isl::", "").split("<")[0]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r.get("Dispatch_Id", ""))
-        if "conv_x3" in n:   # the whole conv stage: conv_x3_f16 + conv1_1's conv_x3_rgb
+        if "conv_x3" in n:   # the whole conv stage: conv_x3_f16 + conv_x3_c12 (or conv_x3_rgb)
             acc["conv_stage"][r["Counter_Name"]] += float(r["Counter_Value"])
             disp["conv_stage"].add(r.get("Dispatch_Id", ""))
     json.dump({"note": "raw SQ/GRBM counter sums per kernel class over the profiled bench run",
@@ -112,8 +112,8 @@ def mfma_busy(sq_dir, stats_csv, sq_out, clock_ghz=None):
     cs = acc["conv_stage"]
     stage_wall = sum(float(r["TotalDurationNs"]) for r in stats if "conv_x3" in r["Name"])
     extra = {"conv_stage_mfma_busy_frac": round(cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (cs["GRBM_GUI_ACTIVE"] / 8), 4),
-             "conv_stage_note": "all conv kernels of the net (conv_x3_f16 + conv1_1's conv_x3_rgb, which is bound by "
-                                "its 64-channel output write): MFMA busy / GRBM cycles, as x3_mfma_busy_frac"}
+             "conv_stage_note": "all conv kernels of the net (conv_x3_f16 + the conv1_1->conv1_2 pair's conv_x3_c12 (or conv_x3_rgb when unfused)"
+                                "): MFMA busy / GRBM cycles, as x3_mfma_busy_frac"}
     if clock_ghz:
         extra["conv_stage_mfma_busy_frac_at_stamp_clock"] = round(
             cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (stage_wall * clock_ghz), 4)

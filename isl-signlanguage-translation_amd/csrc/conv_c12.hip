@@ -1,4 +1,4 @@
-// conv1_1 -> conv1_2 (+ the horizontal half of the 2x2 pool) in one launch, on the split-fp16
+// conv1_1 -> conv1_2 -> the 2x2 pool in one launch, on the split-fp16
 // ("x3") matrix-core arithmetic of conv_x3.hip.
 //
 // Replaces model.py:25-45's first two layers of every net (conv1_1 3 -> 64 + ReLU, conv1_2 64 ->
@@ -14,7 +14,8 @@
 //            order, its epilogue (x 2^-s, bias, activation), zero outside the image (conv1_2's
 //            padding ring), then x3_split8's split of every value;
 //   conv1_2: K order (pair, ky, kx), 3 MFMAs per tap (hi*hi, hi*lo, lo*hi) from zero, its
-//            epilogue, the pair-max of the hpool epilogue.
+//            epilogue, then the pool's maxima (pool2: the pooled map; else the hpool pair-max
+//            buffer that vpool2 / the next conv's staging finishes).
 // Channel halves: conv1_1's 64 outputs are staged 32 at a time (chunk pairs 0-1, then 2-3) so
 // the halo buffer is 45 KB and two blocks fit a CU; conv1_2 walks its pairs in order across the
 // two halves, so its K order is unchanged.
@@ -55,8 +56,9 @@ struct C12Args {
   const float* sl2;
   float s2_inv;
   int act2;
-  float* out;                                   // pair-max buffer [n][8 chunks][H][W / 2][8]
-  long long out_fs, out_chs;
+  float* out;                                   // pool2: the pooled buffer [n][8 chunks][H/2 + 2 op][W/2 + 2 op][8];
+  long long out_fs, out_chs;                    // else the pair-max buffer [n][8 chunks][H][W / 2][8]
+  int pool2, out_pad, out_wp;                   // out_wp: padded pooled width W/2 + 2 out_pad
   int H, W, tiles_x, tiles_y, nblocks;
   int* range_flag;
 };
@@ -224,10 +226,15 @@ __global__ void __launch_bounds__(NT, 4) conv_x3_c12(C12Args a) {
       __syncthreads();   // the next slab is in LDS; this one may be overwritten
     }
   }
-  // ---- conv1_2's epilogue with the pair-max of the pool (conv_x3_f16 hpool)
+  // ---- conv1_2's epilogue with the pool (model.py:29 pool1_stage1, 2 x 2 / 2): the pair max of
+  // neighbouring columns by a DPP swap (conv_x3_f16 hpool); pool2: the row pair's max too (rows
+  // y, y + 1 are waves 2i, 2i + 1: the odd wave hands its pair maxima over in LDS) and the pooled
+  // value stored into the padded pooled buffer, so conv2_1 reads a plain input (no row-pair max
+  // in its staging).  max is exact in any order: the bits of maxpool2 / vpool2.
   const int y = y0 + wave, x = x0 + l32;
   const bool ok = y < a.H && x < a.W;
   float* out_f = a.out + (size_t)n * a.out_fs;
+  f32x4 pv[2][4];
 #pragma unroll
   for (int wm = 0; wm < 2; ++wm)
 #pragma unroll
@@ -244,19 +251,56 @@ __global__ void __launch_bounds__(NT, 4) conv_x3_c12(C12Args a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         v[e] = fmaxf(v[e], __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v[e]), 0xB1, 0xF, 0xF, false)));
-      if (ok && !(x & 1))
-        *(f32x4*)(out_f + (size_t)(co >> 3) * a.out_chs + ((size_t)y * (a.W / 2) + (x >> 1)) * 8 + (co & 7)) = v;
+      pv[wm][q] = v;
     }
+  if (!a.pool2) {
+#pragma unroll
+    for (int wm = 0; wm < 2; ++wm)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = wm * 32 + 8 * q + 4 * h;
+        if (ok && !(x & 1))
+          *(f32x4*)(out_f + (size_t)(co >> 3) * a.out_chs + ((size_t)y * (a.W / 2) + (x >> 1)) * 8 + (co & 7)) = pv[wm][q];
+      }
+  } else {
+    // the K loop ended on a barrier: s_x is free.  Slot (row pair, wm, q, h, even lane / 2).
+    f32x4* xch = reinterpret_cast<f32x4*>(&s_x[0][0][0]);
+    auto slot = [&](int wm, int q) { return (((wave >> 1) * 8 + wm * 4 + q) * 2 + h) * 16 + (l32 >> 1); };
+    if (wave & 1) {
+#pragma unroll
+      for (int wm = 0; wm < 2; ++wm)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (!(l32 & 1)) xch[slot(wm, q)] = pv[wm][q];
+    }
+    __syncthreads();
+    if (!(wave & 1) && ok && y + 1 < a.H && !(x & 1)) {
+      float* op = out_f + ((size_t)((y >> 1) + a.out_pad) * a.out_wp + (x >> 1) + a.out_pad) * 8;
+#pragma unroll
+      for (int wm = 0; wm < 2; ++wm)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int co = wm * 32 + 8 * q + 4 * h;
+          const f32x4 u = xch[slot(wm, q)];
+          f32x4 v = pv[wm][q];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], u[e]);
+          *(f32x4*)(op + (size_t)(co >> 3) * a.out_chs + (co & 7)) = v;
+        }
+    }
+  }
   if (bad) atomicOr(a.range_flag, 1);
 }
 
 }  // namespace
 
 bool x3_c12_fits(const ConvLaunch& l1, const ConvLaunch& l2) {
+  // hpool 1: the pair-max buffer (out_pad 0); 2: the pooled buffer, any pad ring
   return l1.ks == 3 && l1.cin_chunks == 1 && l1.cout == 64 && l1.in_pad >= 1 && l1.in_coff == 0 &&
-         l2.ks == 3 && l2.cin_chunks == 8 && l2.cout == 64 && l2.bco == 64 && l2.hpool && !(l2.W & 1) &&
-         l1.H == l2.H && l1.W == l2.W && l1.n == l2.n && l2.out_coff == 0 && l2.out_pad == 0 &&
-         (l2.out_cs & 7) == 0 && l1.wx3 && l2.wx3 && l1.range_flag;
+         l2.ks == 3 && l2.cin_chunks == 8 && l2.cout == 64 && l2.bco == 64 && (l2.hpool == 1 || l2.hpool == 2) &&
+         !(l2.W & 1) && l1.H == l2.H && l1.W == l2.W && l1.n == l2.n && l2.out_coff == 0 &&
+         (l2.hpool == 2 ? l2.out_pad >= 0 : l2.out_pad == 0) && (l2.out_cs & 7) == 0 && l2.out_cs >= 64 && l1.wx3 &&
+         l2.wx3 && l1.range_flag;
 }
 
 hipError_t launch_conv_x3_c12(const ConvLaunch& l1, const ConvLaunch& l2, hipStream_t s) {
@@ -274,7 +318,10 @@ hipError_t launch_conv_x3_c12(const ConvLaunch& l1, const ConvLaunch& l2, hipStr
   a.w2 = (const f16x8*)l2.wx3;
   a.b2 = l2.bias; a.sl2 = l2.slope; a.s2_inv = l2.wscale_inv; a.act2 = l2.act;
   a.out = l2.out;
-  a.out_chs = (long long)l2.H * (l2.W / 2) * 8;
+  a.pool2 = l2.hpool == 2;
+  a.out_pad = a.pool2 ? l2.out_pad : 0;
+  a.out_wp = l2.W / 2 + 2 * a.out_pad;
+  a.out_chs = a.pool2 ? (long long)(l2.H / 2 + 2 * a.out_pad) * a.out_wp * 8 : (long long)l2.H * (l2.W / 2) * 8;
   a.out_fs = a.out_chs * (l2.out_cs / 8);
   a.H = l1.H; a.W = l1.W;
   a.tiles_x = (l1.W + TW - 1) / TW;

@@ -991,11 +991,12 @@ static bool rgb_kernel_enabled() {
   return !(e && e[0] == '0');
 }
 
-// conv1_1 -> conv1_2 -> the pool's pair-max in one launch (conv_c12.hip); ISLPOSE_C12=0: the two
-// convs as their own launches (A/B; read per run)
-static bool c12_enabled() {
+// conv1_1 -> conv1_2 -> the 2x2 pool in one launch (conv_c12.hip) writing the pooled map;
+// ISLPOSE_C12=0: the two convs as their own launches, =2: the fused launch writing the pool's
+// pair-max buffer, finished by the next conv's staging (round-5 form; A/B, read per run)
+static int c12_mode() {
   const char* e = getenv("ISLPOSE_C12");
-  return !(e && e[0] == '0');
+  return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
 }
 
 // ISLPOSE_FUSED_POOL=0: the plain conv + maxpool2 path (A/B; read per run, so a test
@@ -1238,9 +1239,11 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
       continue;
     }
 
-    // conv1_1 (rgb kernel) -> conv1_2 -> pool: both convs in one launch writing the pool's
-    // pair-max buffer, where conv1_1's output feeds conv1_2 only (conv_c12.hip)
-    if (net->algo == ISL_ALGO_X3 && op.type == 0 && vin_buf < 0 && fuse_pools && c12_enabled() &&
+    // conv1_1 (rgb kernel) -> conv1_2 -> pool: both convs and the pool in one launch writing the
+    // pooled map (or, ISLPOSE_C12=2, the pool's pair-max buffer), where conv1_1's output feeds
+    // conv1_2 only (conv_c12.hip)
+    const int c12m = c12_mode();
+    if (net->algo == ISL_ALGO_X3 && op.type == 0 && vin_buf < 0 && fuse_pools && c12m &&
         k + 2 < net->ops.size() && net->layers[op.layer].d_wrgb && rgb_kernel_enabled()) {
       const Op& o2 = net->ops[k + 1];
       const Op& pl = net->ops[k + 2];
@@ -1259,6 +1262,16 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
         L2.hpool = 1;
         only = pl.C == L2.cout && x3_rgb_fits(L1) && x3_hpool_ok(L2) && x3_c12_fits(L1, L2);
       }
+      // the whole pool in the epilogue: the pooled buffer is the floor-mode 2x2 pool of conv1_2's
+      // plane, written from its channel 0
+      const Act& po = net->act[pl.out];
+      bool pool2 = false;
+      if (only && c12m == 1 && pl.out_coff == 0 && po.H == L2.H / 2 && po.W == L2.W / 2 && po.cs >= 64 &&
+          po.n == L2.n) {
+        ConvLaunch P = L2;
+        P.out = po.base; P.out_pad = po.pad; P.out_cs = po.cs; P.hpool = 2;
+        if (x3_c12_fits(L1, P)) { L2 = P; pool2 = true; }
+      }
       if (only) {
         HIP_OK(launch_conv_x3_c12(L1, L2, s));
         net->op_variant[k] = x3_variant_code(X3V_C12, 3, 256, 64);
@@ -1272,6 +1285,15 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
           HIP_OK(hipEventRecord(tr->ev[k + 1], s));
           tr->kind.push_back(0); tr->flops.push_back(0.0); tr->mfma_flops.push_back(0.0);
           HIP_OK(hipEventRecord(tr->ev[k + 2], s));
+          if (pool2) {
+            tr->kind.push_back(0); tr->flops.push_back(0.0); tr->mfma_flops.push_back(0.0);
+            HIP_OK(hipEventRecord(tr->ev[k + 3], s));
+          }
+        }
+        if (pool2) {
+          net->op_variant[k + 2] = -2;   // the pool ran inside op k
+          k += 2;
+          continue;
         }
         fused = true;   // the pool op finds its pair-max buffer written
         ++k;

@@ -180,8 +180,8 @@ def test_fused_pair_default_form_by_grid(net25, monkeypatch, n):
     assert torch.equal(po, pd) and torch.equal(ho, hd)
 
 
-def _c12_run(net, x, on, monkeypatch):
-    monkeypatch.setenv("ISLPOSE_C12", "1" if on else "0")
+def _c12_run(net, x, mode, monkeypatch):
+    monkeypatch.setenv("ISLPOSE_C12", mode)
     out = net.forward(x)
     torch.cuda.synchronize()
     var = net.op_variants()
@@ -189,26 +189,34 @@ def _c12_run(net, x, on, monkeypatch):
 
 
 @pytest.mark.parametrize("kind,n,h,w", [("body25", 2, 368, 656), ("body25", 1, 184, 328), ("body25", 3, 62, 94),
-                                        ("hand", 2, 184, 184), ("hand", 1, 368, 368), ("coco", 1, 184, 200)])
+                                        ("body25", 1, 61, 94), ("hand", 2, 184, 184), ("hand", 1, 368, 368),
+                                        ("coco", 1, 184, 200)])
 def test_c12_conv1_pair_bit_identical(kind, n, h, w, monkeypatch):
-    """conv1_1 -> conv1_2 -> the pool's pair-max in one launch (conv_c12.hip: conv1_1 recomputed
-    on each 8 x 32 tile's halo into LDS; model.py:25-45's first two layers of every net) == the
-    rgb kernel + conv1_2 on the generic loop (ISLPOSE_C12=0) bit for bit, at the bench's size,
-    Mode R, a size with partial row and column tiles, the hand scales and COCO; asserted to run
-    (isl_net_op_info), and within the tolerance of the oracle."""
+    """conv1_1 -> conv1_2 -> pool1 in one launch (conv_c12.hip: conv1_1 recomputed on each 8 x 32
+    tile's halo into LDS, the 2 x 2 pool in the epilogue; model.py:25-45's first layers of every
+    net) == the rgb kernel + conv1_2 on the generic loop + the pool (ISLPOSE_C12=0) == the fused
+    launch writing the pair-max buffer that conv2_1's staging finishes (=2), bit for bit, at the
+    bench's size, Mode R, sizes with partial row and column tiles (an odd height: floor-mode pool),
+    the hand scales and COCO; asserted to run (isl_net_op_info), and within the tolerance of the
+    oracle."""
     code = {"body25": rt.ISL_BODY25, "hand": rt.ISL_HAND, "coco": rt.ISL_COCO}[kind]
     wts = synth.synth_weights(code)
     net = rt.Net(code)
     net.load_weights(wts)
     x = _inputs(n, h, w, seed=h * 3 + w + n)
     xt = torch.from_numpy(x).cuda()
-    o0, v0 = _c12_run(net, xt, False, monkeypatch)
-    o1, v1 = _c12_run(net, xt, True, monkeypatch)
-    d1 = dict((name, rt.decode_variant(v)) for name, v in v1)
-    assert d1["conv1_1"].get("var", 0) & 4 and d1["conv1_2"].get("fused_into_prev"), (d1["conv1_1"], d1["conv1_2"])
+    o0, v0 = _c12_run(net, xt, "0", monkeypatch)
+    o2, v2 = _c12_run(net, xt, "2", monkeypatch)
+    o1, v1 = _c12_run(net, xt, "1", monkeypatch)
+    for v in (v1, v2):
+        d = dict((name, rt.decode_variant(c)) for name, c in v)
+        assert d["conv1_1"].get("var", 0) & 4 and d["conv1_2"].get("fused_into_prev"), (d["conv1_1"], d["conv1_2"])
+    i12 = [name for name, _ in v1].index("conv1_2")
+    assert v1[i12 + 1][0] == "maxpool2" and v1[i12 + 1][1] == -2 and v2[i12 + 1][1] != -2, (v1[i12 + 1], v2[i12 + 1])
+    assert not rt.decode_variant(v1[i12 + 2][1]).get("vin"), v1[i12 + 2]
     assert not any(rt.decode_variant(v).get("var", 0) & 4 and not rt.decode_variant(v).get("rgb") for _, v in v0)
-    for a, b in zip(o0, o1):
-        assert torch.equal(a, b)
+    for a, b, c in zip(o0, o1, o2):
+        assert torch.equal(a, b) and torch.equal(a, c)
     ref = cpu_ref.make_net_fn(kind, wts)(x[:1])
     ref = ref if isinstance(ref, tuple) else (ref,)
     for a, r in zip(o1, ref):

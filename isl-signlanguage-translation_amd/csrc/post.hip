@@ -1254,6 +1254,7 @@ struct GroupArgs {
   int* pair_keep;           // [n][max_pairs]  (-1 rejected, else rank key)
   int* order;               // [n][max_pairs]
   unsigned char* used;      // [n][2][max_peaks]
+  int limb_lds;             // large pair sets ranked in LDS (ISLPOSE_LIMB_LDS=0: the per-thread pair loop)
 };
 
 // One element of the two-stage resize m2(m1(low)) (body.py:68-73 then :74-76 on a frame whose
@@ -1326,8 +1327,15 @@ __device__ __forceinline__ double paf_value(const GroupArgs& a, int f, int c, in
 }
 
 constexpr int LIMB_ITEMS = 2048;   // (pair, point) items scored in parallel (16 KB of LDS)
+constexpr int LIMB_MAXP = 4096;    // large pair sets ranked and matched in LDS (the default max_pairs)
+constexpr int LIMB_MAXPK = 1024;   // ... with at most this many peaks of either part (used flags in LDS)
 // One workgroup per (limb, frame): score every (A, B) pair (body.py:142-164),
 // stable descending sort by rank counting, greedy matching (body.py:166-175).
+// MODE 0: all of it.  Small batches (a frame per call) spread the scoring, the bulk of the work
+// (two nested PAF samples per (pair, point)), over more CUs: MODE 1 blocks (limb, frame, z)
+// score the z-th slice of a limb's pairs into pscore / pkeep, then MODE 2 (one block per limb
+// and frame) ranks and matches them.  The same sums in the same order: the same scores.
+template <int MODE>
 __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
   const int k = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
   char* rec = a.result + (size_t)f * a.lay.record_bytes;
@@ -1343,6 +1351,7 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
   unsigned char* usedA = a.used + slot * 2 * a.max_peaks;
   unsigned char* usedB = usedA + a.max_peaks;
   __shared__ int s_offA, s_offB, s_nkeep;
+  __shared__ double s_item[LIMB_ITEMS];
   if (*status != ISL_OK) return;    // capacity overflow in compaction: host re-runs with larger caps
   const int A = a.model == ISL_BODY25 ? kLimbs25[k][0] : kLimbsCoco[k][0];
   const int B = a.model == ISL_BODY25 ? kLimbs25[k][1] : kLimbsCoco[k][1];
@@ -1350,12 +1359,12 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
   const int my = a.model == ISL_BODY25 ? kMap25[k][1] : kMapCoco[k][1];
   const int nA = n_peaks[A], nB = n_peaks[B];
   if (nA == 0 || nB == 0) {            // special_k
-    if (tid == 0) n_conns[k] = -1;
+    if (MODE != 1 && tid == 0) n_conns[k] = -1;
     return;
   }
   const int np = nA * nB;
   if (np > a.max_pairs) {
-    if (tid == 0) { atomicExch(status, ISL_E_CAPACITY); n_conns[k] = -2; }
+    if (MODE != 1 && tid == 0) { atomicExch(status, ISL_E_CAPACITY); n_conns[k] = -2; }
     return;
   }
   if (tid == 0) {
@@ -1395,15 +1404,53 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
     pscore[p] = score;
     pkeep[p] = (cnt > 8 && score > 0.0) ? 1 : 0;
   };
+  // pairs [q0, q1): their (pair, point) items in chunks of LIMB_ITEMS / 20 pairs, the two PAF
+  // channels of a point on two threads (products added in order after the barrier, as the small
+  // path), each pair's sum in point order into pscore / pkeep
+  auto score_range = [&](int q0, int q1) __attribute__((always_inline)) {
+    constexpr int CP = LIMB_ITEMS / 20;
+    for (int p0 = q0; p0 < q1; p0 += CP) {
+      const int pc = min(CP, q1 - p0);
+      for (int it = tid; it < pc * 20; it += 256) {
+        const int item = it >> 1, ch = it & 1;
+        double ux, uy, nr;
+        int xi, yi;
+        point(p0 + item / 10, item % 10, &ux, &uy, &nr, &xi, &yi);
+        s_item[it] = paf_value(a, f, ch ? my : mx, yi, xi) * (ch ? uy : ux);
+      }
+      __syncthreads();
+      for (int q = tid; q < pc; q += 256) {
+        double sum = 0.0;
+        int cnt = 0;
+        for (int I = 0; I < 10; ++I) {
+          const double v = s_item[(q * 10 + I) * 2] + s_item[(q * 10 + I) * 2 + 1];
+          sum = sum + v;                                                      // builtin sum(), left to right
+          cnt += v > 0.05;
+        }
+        double ux, uy, nr;
+        int xi, yi;
+        point(p0 + q, 0, &ux, &uy, &nr, &xi, &yi);
+        score_of(p0 + q, sum, cnt, nr);
+      }
+      __syncthreads();   // s_item is reused
+    }
+  };
+  if constexpr (MODE == 1) {
+    const int Z = gridDim.z, per = (np + Z - 1) / Z;
+    const int q0 = min(np, (int)blockIdx.z * per), q1 = min(np, q0 + per);
+    score_range(q0, q1);
+    return;
+  }
   if (np * 10 <= LIMB_ITEMS) {
     // every (pair, point) in parallel (the nested two-stage samples are ~80 loads each), then
     // each pair's sum in point order
-    __shared__ double s_item[LIMB_ITEMS];
     // small pair sets (np * 20 <= LIMB_ITEMS: a batch-1 frame's limbs) take the two PAF channels
     // of a point on two threads, so a thread's chain is one sample; the products are added in the
     // same order after the barrier (vx * ux + vy * uy)
     const bool split = np * 20 <= LIMB_ITEMS;
-    if (split) {
+    if (MODE == 2) {
+      // scored by the MODE 1 launch
+    } else if (split) {
       for (int it = tid; it < np * 20; it += 256) {
         const int item = it >> 1, ch = it & 1;
         double ux, uy, nr;
@@ -1433,6 +1480,11 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
     __shared__ unsigned char s_ua[LIMB_ITEMS / 10], s_ub[LIMB_ITEMS / 10];
     __syncthreads();
     for (int p = tid; p < np; p += 256) {
+      if (MODE == 2) {
+        s_ps[p] = pscore[p];
+        s_pk[p] = pkeep[p];
+        continue;
+      }
       double sum = 0.0;
       int cnt = 0;
       for (int I = 0; I < 10; ++I) {
@@ -1482,7 +1534,76 @@ __global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
       n_conns[k] = m;
     }
     return;
-  } else {
+  } else if (a.limb_lds && np <= LIMB_MAXP && nA <= LIMB_MAXPK && nB <= LIMB_MAXPK) {
+    // Large pair sets (crowded or noisy frames: a 1080p frame's limbs reach hundreds of pairs).
+    // The (pair, point) items in chunks of LIMB_ITEMS / 10 pairs, every thread at once, each
+    // pair's sum in point order into pscore / pkeep; the rank sort over LDS tiles of the kept
+    // scores (a thread's pairs counted against each staged score); the order, the sorted scores
+    // and the used flags in LDS for the serial greedy.  Same sums, ranks and matches as the
+    // per-thread pair loop below, which walked dependent global loads in its O(np^2) rank sort
+    // and its greedy (~0.9 ms per 1080p frame).
+    if (MODE == 0) score_range(0, np);
+    __shared__ int s_ord[LIMB_MAXP];
+    __shared__ unsigned char s_uA[LIMB_MAXPK], s_uB[LIMB_MAXPK];
+    constexpr int PJ = LIMB_MAXP / 256;            // pairs per thread (p = tid + 256 j)
+    const int nj = (np + 255) / 256;
+    double sp[PJ];
+    bool kp[PJ];
+    int rk[PJ];
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      const int p = tid + 256 * j;
+      kp[j] = j < nj && p < np && pkeep[p];
+      sp[j] = kp[j] ? pscore[p] : 0.0;
+      rk[j] = 0;
+    }
+    // kept scores are > 0, so a staged -1 (not kept) is never better than a kept pair
+    for (int q0 = 0; q0 < np; q0 += LIMB_ITEMS) {
+      const int qc = min(LIMB_ITEMS, np - q0);
+      for (int i = tid; i < qc; i += 256) s_item[i] = pkeep[q0 + i] ? pscore[q0 + i] : -1.0;
+      __syncthreads();
+      for (int i = 0; i < qc; ++i) {
+        const double v = s_item[i];
+        const int q = q0 + i;
+#pragma unroll
+        for (int j = 0; j < PJ; ++j)
+          if (j < nj) rk[j] += (v > sp[j] || (v == sp[j] && q < tid + 256 * j)) ? 1 : 0;
+      }
+      __syncthreads();
+    }
+    // the order and the sorted scores (ranks < LIMB_ITEMS) for the greedy
+#pragma unroll
+    for (int j = 0; j < PJ; ++j)
+      if (kp[j]) {
+        s_ord[rk[j]] = tid + 256 * j;
+        if (rk[j] < LIMB_ITEMS) s_item[rk[j]] = sp[j];
+        atomicAdd(&s_nkeep, 1);
+      }
+    for (int i = tid; i < nA; i += 256) s_uA[i] = 0;
+    for (int j = tid; j < nB; j += 256) s_uB[j] = 0;
+    __syncthreads();
+    if (tid == 0) {
+      double* cw = conns + (size_t)k * a.max_conns * 5;
+      const int lim = nA < nB ? nA : nB;
+      int m = 0;
+      for (int r = 0; r < s_nkeep && m < lim; ++r) {
+        const int p = s_ord[r];
+        const int i = p / nB, j = p - i * nB;
+        if (s_uA[i] || s_uB[j]) continue;
+        s_uA[i] = s_uB[j] = 1;
+        if (m >= a.max_conns) { atomicExch(status, ISL_E_CAPACITY); break; }
+        double* c = cw + (size_t)m * 5;
+        c[0] = (double)(s_offA + i);
+        c[1] = (double)(s_offB + j);
+        c[2] = r < LIMB_ITEMS ? s_item[r] : pscore[p];
+        c[3] = (double)i;
+        c[4] = (double)j;
+        ++m;
+      }
+      n_conns[k] = m;
+    }
+    return;
+  } else if (MODE == 0) {
     for (int p = tid; p < np; p += 256) {
       double sum = 0.0, nr = 0.0;
       int cnt = 0;
@@ -3277,7 +3398,20 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   ga.pair_keep = (int*)(pairs + slots * caps->max_pairs * 8);
   ga.order = ga.pair_keep + slots * caps->max_pairs;
   ga.used = used;
-  hipLaunchKernelGGL(limb_kernel, dim3(nlimbs, n), dim3(256), 0, s, ga);
+  {   // ISLPOSE_LIMB_LDS=0: large pair sets on the per-thread pair loop (A/B and tests; read per call)
+    const char* e = getenv("ISLPOSE_LIMB_LDS");
+    ga.limb_lds = !(e && e[0] == '0');
+  }
+  // a frame per call: the scoring over Z blocks per limb (MODE 1), then ranks and matches (MODE 2);
+  // ISLPOSE_LIMB_SPLIT=0: one block per limb (A/B; read per call)
+  const char* lse = getenv("ISLPOSE_LIMB_SPLIT");
+  const int lz = (lse && lse[0] == '0') || n * nlimbs >= 128 ? 1 : std::min(16, 256 / (n * nlimbs));
+  if (lz > 1) {
+    hipLaunchKernelGGL(limb_kernel<1>, dim3(nlimbs, n, lz), dim3(256), 0, s, ga);
+    hipLaunchKernelGGL(limb_kernel<2>, dim3(nlimbs, n), dim3(256), 0, s, ga);
+  } else {
+    hipLaunchKernelGGL(limb_kernel<0>, dim3(nlimbs, n), dim3(256), 0, s, ga);
+  }
   PHIP(hipGetLastError());
   const int asm_lds = caps->max_rows <= ASM_LDS_ROWS;
   // (the connection cache takes what is left of 64 KB of dynamic LDS, up to ASM_CONN_CACHE)

@@ -198,6 +198,40 @@ def test_assemble_register_merge_equals_table(est25, estcoco, monkeypatch, kind,
     assert np.array_equal(got[0].candidate, cand) and np.array_equal(got[0].subset, subset)
 
 
+@pytest.mark.parametrize("H,W,scale,persons", [(368, 4096, 1.0, 20), (368, 4096, 1.0, 45), (1080, 1920, 0.5, 16)])
+def test_limb_large_pair_sets(est25, monkeypatch, H, W, scale, persons):
+    """Limbs with more than LIMB_ITEMS / 10 candidate pairs (body.py:142-175; hundreds per limb on
+    crowded or noisy frames, e.g. 1080p frames through the two-stage resize): the chunked scoring
+    with the rank sort and the greedy in LDS (default) == the per-thread pair loop
+    (ISLPOSE_LIMB_LDS=0), with the scoring spread over blocks (small batches, the default) and in
+    the limb's own block (ISLPOSE_LIMB_SPLIT=0) == the oracle, connections included."""
+    geoms = [g[1:] for g in scale_geometry(H, W, (scale,))]
+    nh, nw = geoms[0][0] // 8, geoms[0][1] // 8
+    ms = [synth.designed_pose_maps(nh, nw, persons, seed=500 + persons + i) for i in range(2)]
+    pafs = [torch.from_numpy(np.stack([m[0] for m in ms])).cuda()]
+    heats = [torch.from_numpy(np.stack([m[1] for m in ms])).cuda()]
+    monkeypatch.delenv("ISLPOSE_LIMB_LDS", raising=False)
+    monkeypatch.delenv("ISLPOSE_LIMB_SPLIT", raising=False)
+    got = est25.post_maps(H, W, geoms, pafs, heats)
+    refs = []
+    for lds, split in (("0", "1"), ("1", "0"), ("0", "0")):
+        monkeypatch.setenv("ISLPOSE_LIMB_LDS", lds)
+        monkeypatch.setenv("ISLPOSE_LIMB_SPLIT", split)
+        refs.append(est25.post_maps(H, W, geoms, pafs, heats))
+    for ref in refs:
+        for a, b in zip(got, ref):
+            assert np.array_equal(a.candidate, b.candidate) and np.array_equal(a.subset, b.subset)
+            for x, y in zip(a.connection_all, b.connection_all):
+                assert np.array_equal(np.asarray(x).reshape(-1, 5), np.asarray(y).reshape(-1, 5))
+    heat_avg, paf_avg = cpu_ref.body_maps(np.zeros((H, W, 3), np.uint8), lambda im: (ms[0][0][None], ms[0][1][None]),
+                                          "body25", (scale,))
+    cand, subset, peaks, conn = cpu_ref.body_post(heat_avg, paf_avg, "body25", H)
+    assert max(len(p) for p in peaks) ** 2 > 204     # some limb takes the large-pair path
+    assert np.array_equal(got[0].candidate, cand) and np.array_equal(got[0].subset, subset)
+    for x, y in zip(got[0].connection_all, conn):
+        assert np.array_equal(np.asarray(x).reshape(-1, 5), np.asarray(y).reshape(-1, 5))
+
+
 def test_body_post_golden_bit_exact(est25, estcoco):
     """Designed low-res maps replayed through the GPU post kernels == reference Body.__call__."""
     z, names = _golden_cases()

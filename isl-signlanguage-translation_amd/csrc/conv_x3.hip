@@ -1831,8 +1831,10 @@ static int device_cus() {
 // grid buys more than the second staging of the input costs; with one block per CU (Mode R
 // batch 32) it loses 10-20 % (profiles/r03/halfco_ab/).  Same bits either way.
 // ISLPOSE_X3_HALFCO=0 off, =1 every 128-channel launch of the family (read per launch; A/B).
+static bool x3_small7(const ConvLaunch& c);
 static bool x3_halfco(const ConvLaunch& c) {
   if (c.ks > 7 || c.fold) return false;
+  if (c.ks == 7) return c.ksplit > 1 && c.ws && x3_small7(c);
 #ifdef ISLPOSE_DEV
   // development build only (A/B of profiles/r03/halfco_ab/): =0 off, =1 every 128-channel
   // launch of the family (measured slower at one block per CU, so not in the product)
@@ -1841,6 +1843,20 @@ static bool x3_halfco(const ConvLaunch& c) {
   if (e && e[0] == '1') return true;
 #endif
   return c.ks <= 3 && c.ksplit > 1 && c.ws;
+}
+
+// Small 7x7 grids (a frame's hand crops per call: one or two crops at the 46^2 - 92^2 hand
+// scales, or the 23^2 scale's across-block K ranges), under one 128-pixel block per CU: the
+// 128-channel tiles run as two 64-channel blocks on 64-pixel tiles (VAR 256, 4 waves of 32co x
+// 32px, two blocks per CU): 4x the blocks, each output the same MFMA sequence (same ranges, same
+// K order), so the same bits as the batched crops.  ISLPOSE_X3_SMALL7=0 off (A/B; per launch).
+static bool x3_small7(const ConvLaunch& c) {
+  if (c.ks != 7 || c.bco != 128 || c.fold || c.vin || c.hpool) return false;
+  const char* e = getenv("ISLPOSE_X3_SMALL7");
+  if (e && e[0] == '0') return false;
+  const int tpx = tile_pixels(c, 128, x3_segmax(128));
+  const long long blocks = (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * std::max(1, c.ksplit);
+  return blocks < device_cus();
 }
 
 // Small grids (the 128-pixel family) with two K groups per block (VAR 32, 16 waves: the first
@@ -2152,6 +2168,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
     // of 64co x 32px on 128 pixels (one block per CU either way: the 56 KiB weight
     // slabs; 8 waves measured 2-6 % over 4 waves of 64co x 64px / x 128px)
     if (c.ksplit <= 1 && c.bco == 128) {
+      if (x3_small7(c)) return launch_t<KS, 2, 2, 1, 1, 256, 4>(c, s);       // 64co x 64px blocks
       if (x3_wide7_384(c)) return launch_t<KS, 2, 6, 2, 2, 65536, 1>(c, s);   // 12 waves, 384 px
       if (x3_wide7(c)) return launch_t<KS, 2, 4, 2, 2, 0, 1>(c, s);
       return launch_t<KS, 2, 4, 2, 1, 0, 1>(c, s);

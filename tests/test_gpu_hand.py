@@ -145,6 +145,29 @@ def test_hand_net_split_k(hest):
         assert d < 1e-5, d
 
 
+@pytest.mark.parametrize("side", [184, 368, 552, 736])
+def test_small7_half_channel_bit_identical(hest, side, monkeypatch):
+    """A frame's single hand crop (the per-frame call of the reference scripts): the 7x7 stage
+    layers' grids are under one 128-pixel block per CU, so they run as 64-channel blocks on
+    64-pixel tiles (conv_x3.hip x3_small7, VAR 256; the 23^2 scale with its across-block K
+    ranges) == the 128-pixel blocks (ISLPOSE_X3_SMALL7=0) bit for bit, and the crop alone ==
+    the crop inside a batch of 8."""
+    from islpose import runtime as rt
+    x = torch.from_numpy(np.ascontiguousarray(
+        np.transpose(synth.synth_frames(8, side, side, seed=side + 1).astype(np.float32), (0, 3, 1, 2)) / 256 - 0.5)).cuda()
+    monkeypatch.delenv("ISLPOSE_X3_SMALL7", raising=False)
+    h1 = hest.net.forward(x[:1]).clone()
+    var = [rt.decode_variant(v) for name, v in hest.net.op_variants()
+           if name.startswith("Mconv") and "Mconv6" not in name and "Mconv7" not in name]
+    assert len(var) == 25 and all(d["ks"] == 7 and d["var"] & 256 and d["bpx"] == 64 for d in var), var[:2]
+    h8 = hest.net.forward(x).clone()
+    monkeypatch.setenv("ISLPOSE_X3_SMALL7", "0")
+    h0 = hest.net.forward(x[:1]).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(h1, h0)
+    assert torch.equal(h1[0], h8[0])
+
+
 def test_arena_bounded_over_crop_counts():
     """estimate_crops with a different crop count per batch keeps one arena
     per hand scale, sized by the largest count seen -- not one per (count, scale)."""

@@ -113,7 +113,7 @@ class ISLSignPos(object):
         if self._pinned_ev is not None:
             self._pinned_ev.synchronize()          # the previous upload has left the buffer
         host = buf[:src.size].view(src.shape)
-        np.copyto(host.numpy(), src)
+        host.copy_(torch.from_numpy(src))          # (torch's copy runs on the host's threads)
         t = host.to(dev, non_blocking=True)
         self._pinned_ev = torch.cuda.Event()
         self._pinned_ev.record(torch.cuda.current_stream(dev))

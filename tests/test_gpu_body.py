@@ -466,7 +466,7 @@ def test_timed_config_forward_vs_oracle(net25, w25):
         assert var[k].get("union") and var[k]["bpx"] == 512, (k, var[k])
     for k in ("conv3_1", "conv4_1"):
         assert var[k].get("vin"), (k, var[k])
-    assert var["conv2_1"].get("union") and not var["conv2_1"].get("vin"), var["conv2_1"]   # pool1 in conv_c12
+    assert var["conv2_1"]["bpx"] == 512 and not var["conv2_1"].get("vin"), var["conv2_1"]   # pool1 in conv_c12
     assert var["conv4_1"].get("union"), var["conv4_1"]
     m6 = [k for k in var if k.startswith("Mconv6")]
     assert len(m6) == 6 and all(var[k].get("fused67") and var[k]["bco"] in (256, 512) for k in m6), m6

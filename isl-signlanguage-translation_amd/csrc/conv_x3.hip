@@ -1850,13 +1850,27 @@ static bool x3_halfco(const ConvLaunch& c) {
 // 128-channel tiles run as two 64-channel blocks on 64-pixel tiles (VAR 256, 4 waves of 32co x
 // 32px, two blocks per CU): 4x the blocks, each output the same MFMA sequence (same ranges, same
 // K order), so the same bits as the batched crops.  ISLPOSE_X3_SMALL7=0 off (A/B; per launch).
+static int x3_small7_mode() {
+  const char* e = getenv("ISLPOSE_X3_SMALL7");
+  return e ? atoi(e) : 2;
+}
 static bool x3_small7(const ConvLaunch& c) {
   if (c.ks != 7 || c.bco != 128 || c.fold || c.vin || c.hpool) return false;
-  const char* e = getenv("ISLPOSE_X3_SMALL7");
-  if (e && e[0] == '0') return false;
+  if (x3_small7_mode() == 0) return false;
   const int tpx = tile_pixels(c, 128, x3_segmax(128));
   const long long blocks = (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * std::max(1, c.ksplit);
   return blocks < device_cus();
+}
+// ... with the operands two K steps ahead (VAR 128: a ring of three 28 KiB weight slabs, one
+// block per CU) where the 64-pixel grid still fits one block per CU: the 46^2 / 69^2 scales
+// of one crop 55 -> 48 us per layer; past one round (92^2: 266 blocks) the two resident
+// blocks of the plain loop win (profiles/r05/r5s7b/).  ISLPOSE_X3_SMALL7=1: never, 3: always.
+static bool x3_small7_deep(const ConvLaunch& c) {
+  const int m = x3_small7_mode();
+  if (m < 2) return false;
+  if (m >= 3) return true;
+  const int tpx = tile_pixels(c, 64, x3_segmax(64));
+  return (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * 2 * std::max(1, c.ksplit) <= device_cus();
 }
 
 // Small grids (the 128-pixel family) with two K groups per block (VAR 32, 16 waves: the first
@@ -2168,7 +2182,10 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
     // of 64co x 32px on 128 pixels (one block per CU either way: the 56 KiB weight
     // slabs; 8 waves measured 2-6 % over 4 waves of 64co x 64px / x 128px)
     if (c.ksplit <= 1 && c.bco == 128) {
-      if (x3_small7(c)) return launch_t<KS, 2, 2, 1, 1, 256, 4>(c, s);       // 64co x 64px blocks
+      if (x3_small7(c)) {   // 64co x 64px blocks (=2: the steps' operands two steps ahead)
+        if (x3_small7_deep(c)) return launch_t<KS, 2, 2, 1, 1, 256 | 128, 1>(c, s);
+        return launch_t<KS, 2, 2, 1, 1, 256, 4>(c, s);
+      }
       if (x3_wide7_384(c)) return launch_t<KS, 2, 6, 2, 2, 65536, 1>(c, s);   // 12 waves, 384 px
       if (x3_wide7(c)) return launch_t<KS, 2, 4, 2, 2, 0, 1>(c, s);
       return launch_t<KS, 2, 4, 2, 1, 0, 1>(c, s);
@@ -2245,6 +2262,9 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
       }
 #endif
       if (c.bco == 128 && x3_halfco(c)) {   // two blocks of 4 waves (64co x 32px) per 128-channel tile
+        if constexpr (KS == 7) {
+          if (split && x3_small7_deep(c)) return launch_t<KS, 2, 2, 1, 1, 2048 | 256 | 128, 1>(c, s);
+        }
         if (split && x3_px64_mode() >= 2) return launch_t<KS, 2, 2, 1, 1, 2048 | 256, 4>(c, s);
         if (split) return launch_t<KS, 1, 4, 2, 1, 2048 | 256, 4>(c, s);
 #ifdef ISLPOSE_DEV

@@ -149,9 +149,10 @@ def test_hand_net_split_k(hest):
 def test_small7_half_channel_bit_identical(hest, side, monkeypatch):
     """A frame's single hand crop (the per-frame call of the reference scripts): the 7x7 stage
     layers' grids are under one 128-pixel block per CU, so they run as 64-channel blocks on
-    64-pixel tiles (conv_x3.hip x3_small7, VAR 256; the 23^2 scale with its across-block K
-    ranges) == the 128-pixel blocks (ISLPOSE_X3_SMALL7=0) bit for bit, and the crop alone ==
-    the crop inside a batch of 8."""
+    64-pixel tiles with their operands two steps ahead (conv_x3.hip x3_small7, VAR 256 | 128;
+    the 23^2 scale with its across-block K ranges) == the same blocks one step ahead
+    (ISLPOSE_X3_SMALL7=1) == the 128-pixel blocks (=0) bit for bit, and the crop alone == the
+    crop inside a batch of 8.  (92^2: 266 blocks, past one round: one step ahead.)"""
     from islpose import runtime as rt
     x = torch.from_numpy(np.ascontiguousarray(
         np.transpose(synth.synth_frames(8, side, side, seed=side + 1).astype(np.float32), (0, 3, 1, 2)) / 256 - 0.5)).cuda()
@@ -160,11 +161,15 @@ def test_small7_half_channel_bit_identical(hest, side, monkeypatch):
     var = [rt.decode_variant(v) for name, v in hest.net.op_variants()
            if name.startswith("Mconv") and "Mconv6" not in name and "Mconv7" not in name]
     assert len(var) == 25 and all(d["ks"] == 7 and d["var"] & 256 and d["bpx"] == 64 for d in var), var[:2]
+    # operands two steps ahead where the 64-pixel grid fits one block per CU (x3_small7_deep)
+    assert all(bool(d["var"] & 128) == (side != 736) for d in var), var[:2]
     h8 = hest.net.forward(x).clone()
+    monkeypatch.setenv("ISLPOSE_X3_SMALL7", "1")
+    hs = hest.net.forward(x[:1]).clone()
     monkeypatch.setenv("ISLPOSE_X3_SMALL7", "0")
     h0 = hest.net.forward(x[:1]).clone()
     torch.cuda.synchronize()
-    assert torch.equal(h1, h0)
+    assert torch.equal(h1, h0) and torch.equal(h1, hs)
     assert torch.equal(h1[0], h8[0])
 
 

@@ -1,6 +1,6 @@
 # Round profile at HEAD: the bench line (with the CPU baseline), kernel trace + FETCH / WRITE /
 # SQ passes of Mode N (profiles/conv_traffic.json, post_traffic.json), a kernel trace of Mode R
-# batch 32, the per-layer table.  usage: bash tools/profile_r4.sh <tag>  (gpurun_out/<tag>)
+# batch 32, the per-layer table.  usage: bash tools/profile_round5.sh <tag>  (gpurun_out/<tag>)
 export TMPDIR=/tmp
 T=${1:-r5p}; O=gpurun_out/$T; mkdir -p $O
 B="python3 bench.py --no-cpu --no-mode-r --e2e-steps 0 --steps 3 --warmup 1"

@@ -110,6 +110,10 @@ struct X3Args {
   float wscale7_inv;
   int cout7, act7;
   int bco_pack;                 // conv_x3_wr: output channels per tile of the weight packing (c.bco)
+  // tail tiles (x3_tail_plan): blocks [0, nb_full) take each frame's first full_tiles tiles of tpx
+  // pixels, blocks [nb_full, nblocks) the frame's rest in tail_tiles tiles of ttpx pixels (0: one
+  // tiling of px_tiles tiles)
+  int nb_full, full_tiles, tail_tiles, ttpx;
 };
 
 // u / d for 0 <= u < 2^20, d >= 1, through the fp32 reciprocal r = 1/d: (u + 0.5) / d sits
@@ -235,8 +239,13 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
   // XCD-aware tile order (conv.hip): co-tiles of a pixel tile, then neighbouring
   // pixel tiles, on one XCD / L2.
   int bid = blockIdx.x;
+  // tail tiles: the full tiles' blocks are dispatched first (whole rounds of one block per CU),
+  // then the tails', each class spread over the XCDs on its own
+  const bool tail = a.nb_full > 0 && bid >= a.nb_full;
   {
-    const int nb = a.nblocks, q = nb >> 3, r = nb & 7, xcd = bid & 7, k = bid >> 3;
+    const int b0 = tail ? a.nb_full : 0;
+    const int nb = a.nb_full > 0 ? (tail ? a.nblocks - a.nb_full : a.nb_full) : a.nblocks;
+    const int lb = bid - b0, q = nb >> 3, r = nb & 7, xcd = lb & 7, k = lb >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
   }
   int ks_i = 0;
@@ -246,12 +255,13 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
   }
   const int co_t = bid % a.co_tiles;
   const int rest = bid / a.co_tiles;
-  const int pt = rest % a.px_tiles;
-  const int n = rest / a.px_tiles;
+  const int ntile = tail ? a.tail_tiles : a.nb_full > 0 ? a.full_tiles : a.px_tiles;
+  const int pt = rest % ntile;
+  const int n = rest / ntile;
 
   const int HW = a.H * a.W;
-  const int m0 = pt * a.tpx;                    // tpx = BPX unless the image is very narrow
-  const int mlast = min(m0 + a.tpx, HW) - 1;
+  const int m0 = tail ? a.full_tiles * a.tpx + pt * a.ttpx : pt * a.tpx;   // tpx = BPX unless the image is very narrow
+  const int mlast = min(m0 + (tail ? a.ttpx : a.tpx), HW) - 1;
   const int Wi = a.W + 2 * a.in_pad;
   const float inv_wi = 1.f / (float)Wi;          // VIN: x3_div
   const int ya = m0 / a.W, xa = m0 - ya * a.W;
@@ -289,7 +299,13 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
 
   // one tap (kx) of a K step: WM x WN accumulator tiles x 3 MFMAs from the weight
   // slab sw and the input run sx (both already offset to this lane's fragments)
+  // big tiles (the tail-tile families): a wave whose pixel granules all lie past the tile (tail and
+  // last tiles) skips its MFMAs -- the live waves of a tile of 128 k pixels stay spread evenly over
+  // the SIMDs.  (The 128-pixel family keeps its loops branch-free.)
+  constexpr bool SKIP_DEAD = BPX >= 256 && !FUSE67 && !M16;
+  const bool wave_live = !SKIP_DEAD || m0 + (wave_u / WAVES_M) * WN * 32 <= mlast;   // (uniform)
   auto tap = [&](const f16x8* sw, const f16x8* sx, int sx_plane, int kx) __attribute__((always_inline)) {
+    if (SKIP_DEAD && !wave_live) return;
     f16x8 A[WM][2], B[WN][2];
 #pragma unroll
     for (int hl = 0; hl < 2; ++hl) {
@@ -1696,6 +1712,41 @@ __global__ void __launch_bounds__(512) conv_x3_wr(X3Args a) {
   if (bad) atomicOr(a.range_flag, 1);
 }
 
+// Tail tiles.  A chip-filling grid of full tiles takes ceil(blocks / CUs) rounds of one block per
+// CU, its last round often part-empty (Mode N's 92x164 layers: 1920 blocks, 7.5 rounds -> 8; the
+// layer time follows the rounds, tools/round_probe.py).  Where it pays by the estimate below, each
+// frame's first full_tiles tiles fill whole rounds and the rest of its pixels run as tail tiles of
+// ttpx pixels (a multiple of 128, so that the MFMA-skipping waves past the tile stay spread over
+// the SIMDs), dispatched after them; a tail block costs ~0.3 + 0.7 ttpx / tpx of a full one (its
+// weight slabs, staging and barriers stay).  Every output keeps its MFMA sequence: same bits.
+// ISLPOSE_X3_TAIL=0: one tiling (A/B; read per launch).
+static int device_cus();
+static void x3_tail_plan(int n, int HW, X3Args& a) {
+  a.nb_full = a.full_tiles = a.tail_tiles = a.ttpx = 0;
+  const char* e = getenv("ISLPOSE_X3_TAIL");
+  if (e && e[0] == '0') return;
+  const long long cus = device_cus(), per = (long long)n * a.co_tiles;
+  const long long R0 = (per * a.px_tiles + cus - 1) / cus;
+  const int full_max = HW / a.tpx;
+  const long long Rf = per * full_max / cus;        // whole rounds the full tiles can fill
+  if (Rf < 1 || R0 < 2) return;
+  const int F = (int)(Rf * cus / per);
+  const long long NF = per * F;
+  if (F < 1 || NF % 8) return;                      // (each class is spread over the 8 XCDs)
+  const int rem = HW - F * a.tpx;
+  double best = (double)R0 - 0.25;
+  for (int t = 128; t < a.tpx; t += 128) {
+    const int TT = (rem + t - 1) / t;
+    const long long NT = per * TT;
+    const double est = (double)NF / cus + (double)((NT + cus - 1) / cus) * (0.3 + 0.7 * t / a.tpx);
+    if (est < best && NF + NT <= 0x7fffffff) {
+      best = est;
+      a.nb_full = (int)NF; a.full_tiles = F; a.tail_tiles = TT; a.ttpx = t;
+      a.nblocks = (int)(NF + NT);
+    }
+  }
+}
+
 template <int KS, int WAVES_M, int WAVES_N, int WM, int WN, int VAR, int OCC>
 static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   constexpr int BCO = WAVES_M * WM * 32;
@@ -1784,6 +1835,7 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   const long long nb = (long long)c.n * a.px_tiles * a.co_tiles * (SPLIT ? a.ksplit : 1);
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
+  if constexpr (!SPLIT && !RANGED && !(VAR & 16) && BPX >= 256) x3_tail_plan(c.n, c.H * c.W, a);
   hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN, VAR, OCC>), dim3(a.nblocks),
                      dim3(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1)), 0, s, a);
   if constexpr (SPLIT) {

@@ -221,3 +221,29 @@ def test_c12_conv1_pair_bit_identical(kind, n, h, w, monkeypatch):
     ref = ref if isinstance(ref, tuple) else (ref,)
     for a, r in zip(o1, ref):
         assert _rel(a[:1].cpu().numpy(), r) < TOL
+
+
+@pytest.mark.parametrize("kind,n,h,w", [("body25", 32, 368, 656), ("hand", 32, 368, 368), ("hand", 32, 736, 736)])
+def test_tail_tiles_bit_identical(kind, n, h, w, monkeypatch):
+    """Tail tiles (conv_x3.hip x3_tail_plan: whole rounds of full 512-pixel tiles, then each
+    frame's remaining pixels as tail tiles whose dead waves skip their MFMAs -- Mode N's 92x164
+    layers, the hand's VGG layers at the C3 scales) == one tiling (ISLPOSE_X3_TAIL=0) bit for
+    bit, and within the tolerance of the oracle on a frame."""
+    code = {"body25": rt.ISL_BODY25, "hand": rt.ISL_HAND}[kind]
+    wts = synth.synth_weights(code)
+    net = rt.Net(code)
+    net.load_weights(wts)
+    x = _inputs(n, h, w, seed=h + n)
+    xt = torch.from_numpy(x).cuda()
+    outs = []
+    for m in ("0", "1"):
+        monkeypatch.setenv("ISLPOSE_X3_TAIL", m)
+        o = net.forward(xt)
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (o if isinstance(o, tuple) else (o,))])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    ref = cpu_ref.make_net_fn(kind, wts)(x[n - 1:n])
+    ref = ref if isinstance(ref, tuple) else (ref,)
+    for a, r in zip(outs[1], ref):
+        assert _rel(a[n - 1:n].cpu().numpy(), r) < TOL

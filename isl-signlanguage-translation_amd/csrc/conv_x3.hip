@@ -1717,8 +1717,10 @@ __global__ void __launch_bounds__(512) conv_x3_wr(X3Args a) {
 // layer time follows the rounds, tools/round_probe.py).  Where it pays by the estimate below, each
 // frame's first full_tiles tiles fill whole rounds and the rest of its pixels run as tail tiles of
 // ttpx pixels (a multiple of 128, so that the MFMA-skipping waves past the tile stay spread over
-// the SIMDs), dispatched after them; a tail block costs ~0.3 + 0.7 ttpx / tpx of a full one (its
-// weight slabs, staging and barriers stay).  Every output keeps its MFMA sequence: same bits.
+// the SIMDs), dispatched after them.  The plan prices a tail block at 0.3 + 0.7 ttpx / tpx of a
+// full one; measured, a 256-pixel tail of the 512-pixel row union costs ~0.85 (its weight slabs,
+// staging and barriers stay: profiles/r05/r5tl), so only clear wins are taken (>= 0.25 round by
+// the estimate).  Every output keeps its MFMA sequence: same bits.
 // ISLPOSE_X3_TAIL=0: one tiling (A/B; read per launch).
 static int device_cus();
 static void x3_tail_plan(int n, int HW, X3Args& a) {

@@ -1075,6 +1075,13 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
     // wave's Mconv7 sums into LDS, then the waves' sums added in wave order and stored.
     static_assert(KS == 1 && WM == 2 && WN == 2 && !SPLIT && !RANGED && !UNION && !DEEP && !VIN && !HALFCO,
                   "fused 1x1 pair: generic loop, 64co x 64px waves");
+#ifdef ISLPOSE_DEV
+    // ablations (tools/archive/cb_f67.sh): 64 no epilogue, 32 Mconv7 filters not loaded
+    if (a.abl & 64) return;
+    const bool abl_f7 = (a.abl & 32) != 0;
+#else
+    constexpr bool abl_f7 = false;
+#endif
     constexpr int RPX = WAVES_N * 32;            // pixels of one pass
     float* eb = (float*)smem;                    // [BCO] bias6, [BCO] slope6, [64] bias7, [64] slope7
     float* red = eb + 2 * BCO + 128;             // [WAVES_M][RPX][F7_ROWS]
@@ -1137,7 +1144,7 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
           for (int kq = 0; kq < 2; ++kq) {
             const int kb = (wave_m * WM + wm) * 2 + kq;
             const f16x8* wp = a.wpk7 + ((size_t)(t * KB + kb) * 2) * 64 + lane;
-            const f16x8 Ah = wp[0], Al = wp[64];
+            const f16x8 Ah = abl_f7 ? Bh[wm][kq] : wp[0], Al = abl_f7 ? Bl[wm][kq] : wp[64];
             d = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ah, Bh[wm][kq], d, 0, 0, 0);
             d = __builtin_amdgcn_mfma_f32_32x32x16_f16(Ah, Bl[wm][kq], d, 0, 0, 0);
             d = __builtin_amdgcn_mfma_f32_32x32x16_f16(Al, Bh[wm][kq], d, 0, 0, 0);

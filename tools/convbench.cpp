@@ -64,6 +64,7 @@ int main(int argc, char** argv) {
   float* wu = wb ? dev_random<float>((size_t)(cout / wb) * chunks * 16 * 2 * wb * 4, -0.05f, 0.05f, 4) : nullptr;
   const int wxt = (cout + 63) / 64;
   _Float16* wux = dev_random<_Float16>((size_t)wxt * pairs * 16 * 4 * 64 * 8, -8192.f, 8192.f, 7);
+  _Float16* f7w = dev_random<_Float16>((size_t)2 * ((cout + 15) / 16) * 2 * 64 * 8, -8192.f, 8192.f, 8);
   float* bias = dev_random<float>(co_tiles * 256 + 256, -0.05f, 0.05f, 5);
   float* slope = dev_random<float>(co_tiles * 256 + 256, 0.05f, 0.25f, 6);
   int* flag;
@@ -131,6 +132,13 @@ int main(int argc, char** argv) {
           c.bco = bco; c.wpk = wd;
           return launch_conv_x3(c, 0);
         }
+        // x3f: the fused 1x1 pair (cout = Mconv6 channels; CONVBENCH_F7 Mconv7 outputs, default 52)
+        if (a == "x3f" && ks == 1) {
+          c.cout7 = getenv("CONVBENCH_F7") ? atoi(getenv("CONVBENCH_F7")) : 52;
+          c.wx3f7 = f7w; c.bias7 = bias; c.slope7 = slope; c.act7 = ACT_PRELU; c.wscale7_inv = 1.f / 16384.f;
+          c.out_cs = 64; c.bco = cout; c.wpk = wd;
+          return launch_conv_x3(c, 0);
+        }
         if (a == "direct") { c.bco = bco; c.wpk = wd; return launch_conv(c, 0); }
         if (a == "wino" && wb && ks == 3) { c.bco = wb; c.wpk = wu; return launch_wino(c, 0); }
         if (a == "wx3" && ks == 3) { c.wx3 = wux; return launch_wino_x3(c, 0); }
@@ -163,7 +171,7 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
       }
       const double us = ms * 1e3 / iters;
-      const double fac = (a == "x3" || a == "x3m" || a == "x3h" || a == "x3p" || a == "x3d") ? 3.0 : a == "wx3" ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
+      const double fac = (a == "x3" || a == "x3f" || a == "x3m" || a == "x3h" || a == "x3p" || a == "x3d") ? 3.0 : a == "wx3" ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
       printf("  round %d %-7s %9.1f us  fp32-equiv %7.1f TF  alg-MFMA %7.1f TF\n", r, a.c_str(), us,
              flops / us / 1e6, fac * flops / us / 1e6);
     }

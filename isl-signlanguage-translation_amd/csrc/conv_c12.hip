@@ -79,12 +79,16 @@ __device__ __forceinline__ void split4(const f32x4& a, f16x4& hi, f16x4& lo) {
   }
 }
 
+// RR: both layers ReLU (the VGG conv1 pair of every net), a compile-time activation: the
+// run-time test per value made a scalar branch chain of both epilogues
+template <bool RR>
 __device__ __forceinline__ float act_f(float v, int act, float slope) {
-  if (act == ACT_RELU) return v > 0.f ? v : 0.f;
+  if (RR || act == ACT_RELU) return v > 0.f ? v : 0.f;
   if (act == ACT_PRELU) return v >= 0.f ? v : v * slope;
   return v;
 }
 
+template <bool RR>
 __global__ void __launch_bounds__(NT, 4) conv_x3_c12(C12Args a) {
   __shared__ f16x8 s_x[2][4][HPS];              // conv1_1 output half: [hi|lo][chunk of the half][halo px]
   __shared__ f16x8 s_w[2][WSL];                 // conv1_2 weight slabs, double-buffered
@@ -188,7 +192,7 @@ __global__ void __launch_bounds__(NT, 4) conv_x3_c12(C12Args a) {
         for (int e = 0; e < 4; ++e) {
           const int co = 32 * hf + 8 * c + 4 * h + e;
           float t = acc1[4 * c + e] * a.s1_inv + s_p[co];
-          t = act_f(t, a.act1, s_p[128 + co]);
+          t = act_f<RR>(t, a.act1, s_p[128 + co]);
           bad |= inimg && !(__builtin_fabsf(t) < 65504.f);
           v[e] = inimg ? t : 0.f;
         }
@@ -244,7 +248,7 @@ __global__ void __launch_bounds__(NT, 4) conv_x3_c12(C12Args a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float t = acc2[wm][4 * q + e] * a.s2_inv + s_p[64 + co + e];
-        t = act_f(t, a.act2, s_p[192 + co + e]);
+        t = act_f<RR>(t, a.act2, s_p[192 + co + e]);
         bad |= ok && !(__builtin_fabsf(t) < 65504.f);
         v[e] = t;
       }
@@ -330,7 +334,8 @@ hipError_t launch_conv_x3_c12(const ConvLaunch& l1, const ConvLaunch& l2, hipStr
   const long long nb = (long long)l1.n * a.tiles_x * a.tiles_y;
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3_c12: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
-  hipLaunchKernelGGL(conv_x3_c12, dim3(a.nblocks), dim3(NT), 0, s, a);
+  if (a.act1 == ACT_RELU && a.act2 == ACT_RELU) hipLaunchKernelGGL(conv_x3_c12<true>, dim3(a.nblocks), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(conv_x3_c12<false>, dim3(a.nblocks), dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 

@@ -1118,13 +1118,22 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
           const int col = (wave_m * WM + wm) * 32 + 4 * h + 8 * q;
           const f32x4 b = *(const f32x4*)(eb + col);
           const f32x4 sl = *(const f32x4*)(eb + BCO + col);
+          // (the activation chosen once per 4 registers: a test per register made a scalar branch
+          // chain of the whole split)
+          f32x4 x;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = acc[wm][wn][4 * q + e] * a.wscale_inv + b[e];
+          if (a.act == ACT_RELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = x[e] > 0.f ? x[e] : 0.f;
+          } else if (a.act == ACT_PRELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = x[e] >= 0.f ? x[e] : x[e] * sl[e];
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            float x = acc[wm][wn][4 * q + e] * a.wscale_inv + b[e];
-            if (a.act == ACT_RELU) x = x > 0.f ? x : 0.f;
-            else if (a.act == ACT_PRELU) x = x >= 0.f ? x : x * sl[e];
-            bad |= live && !(__builtin_fabsf(x) < 65504.f);
-            v[4 * q + e] = x;
+            bad |= live && !(__builtin_fabsf(x[e]) < 65504.f);
+            v[4 * q + e] = x[e];
           }
         }
 #pragma unroll
@@ -1176,13 +1185,16 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
         const int co = 8 * c8;
         float o[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float x = (e < 4 ? s0[e] : s1[e - 4]) * a.wscale7_inv + bias7[co + e];
-          if (a.act7 == ACT_RELU) x = x > 0.f ? x : 0.f;
-          else if (a.act7 == ACT_PRELU) x = x >= 0.f ? x : x * slope7[co + e];
-          bad |= co + e < a.cout7 && !(__builtin_fabsf(x) < 65504.f);
-          o[e] = x;
+        for (int e = 0; e < 8; ++e) o[e] = (e < 4 ? s0[e] : s1[e - 4]) * a.wscale7_inv + bias7[co + e];
+        if (a.act7 == ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = o[e] > 0.f ? o[e] : 0.f;
+        } else if (a.act7 == ACT_PRELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = o[e] >= 0.f ? o[e] : o[e] * slope7[co + e];
         }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bad |= co + e < a.cout7 && !(__builtin_fabsf(o[e]) < 65504.f);
         const int y = m / a.W, x = m - y * a.W;
         float* oc = out_f + (size_t)(co >> 3) * a.out_chs + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8;
         if (co + 7 < a.cout7) {

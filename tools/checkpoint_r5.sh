@@ -18,7 +18,7 @@ import json
 d=json.load(open('$O/bench.json')); r=d['mode_r']
 print('N', d['value'], d['roofline']['frac'], 'post', d['post']['ms_per_step'], 'R32', r['batch32']['frames_per_s'], r['batch32']['roofline']['frac'], 'post', r['batch32']['post_ms_per_step'], 'R1', r['batch1']['frames_per_s'], 'cpu', d['cpu_baseline']['value'])
 for c in ('c3', 'c4', 'c5', 'frame'):
-    try: print(c, json.load(open('$O/' + c + '.json'))['frames_per_s'])
+    try: j = json.load(open('$O/' + c + '.json')); print(c, j.get('frames_per_s', j.get('overlap_frames_per_s')))
     except Exception as e: print(c, 'n/a', e)
 "
 echo "pytest rc=$rc bench rc=$rb"

@@ -1335,8 +1335,11 @@ constexpr int LIMB_MAXPK = 1024;   // ... with at most this many peaks of either
 // (two nested PAF samples per (pair, point)), over more CUs: MODE 1 blocks (limb, frame, z)
 // score the z-th slice of a limb's pairs into pscore / pkeep, then MODE 2 (one block per limb
 // and frame) ranks and matches them.  The same sums in the same order: the same scores.
+// (3 waves per SIMD: the inlined nested samples took 212 VGPRs, 2 waves per SIMD, and a batch-32
+// grid of 832 blocks ran in two rounds; at 168 VGPRs the spills sit in the large-set path:
+// Mode R batch 32 44.6 -> 38.8 us, profiles/r05/r5lb)
 template <int MODE>
-__global__ void __launch_bounds__(256) limb_kernel(GroupArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) limb_kernel(GroupArgs a) {
   const int k = blockIdx.x, f = blockIdx.y, tid = threadIdx.x;
   char* rec = a.result + (size_t)f * a.lay.record_bytes;
   int* status = (int*)(rec + a.lay.status);

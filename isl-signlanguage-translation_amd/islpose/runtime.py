@@ -302,8 +302,9 @@ class Net:
         return scope()
 
     def range_ok(self, clear: bool = True) -> bool:
-        """Device-synchronising check of the split-fp16 range flag (isl_net_check):
-        False if any conv output since the last clear reached |x| >= 65504."""
+        """Synchronous check of the split-fp16 range flag (isl_net_check; it waits for the
+        streams this net's runs were queued on, not the whole device): False if any conv
+        output since the last clear reached |x| >= 65504."""
         rc = lib().isl_net_check(self.h, 1 if clear else 0)
         if rc == ISL_E_RANGE:
             return False

@@ -102,7 +102,8 @@ class ISLSignPos(object):
         body = self._estimators()[0]
         dev = torch.device("cuda:%d" % body.device)
         if isinstance(img, torch.Tensor) and img.is_cuda:
-            return img.to(dev).contiguous()[None]
+            # any dtype, as the host path's np.ascontiguousarray(..., dtype=np.uint8)
+            return img.to(dev).to(torch.uint8).contiguous()[None]
         a = _as_numpy(img)
         flip = a.ndim == 3 and a.shape[2] == 3 and a.strides[2] < 0 and a[:, :, ::-1].flags.c_contiguous
         src = np.ascontiguousarray(a[:, :, ::-1] if flip else a, dtype=np.uint8)

@@ -696,3 +696,41 @@ def test_x3_g2_two_k_groups_bit_identical(net25, w25, n, monkeypatch):
     assert torch.equal(paf0, paf1) and torch.equal(heat0, heat1)
     rp, rh = cpu_ref.make_net_fn("body25", w25)(x[:1])
     assert _rel(paf1[:1].cpu().numpy(), rp) < TOL and _rel(heat1[:1].cpu().numpy(), rh) < TOL
+
+
+def _forward_async(net, x, stream):
+    """isl_net_forward on `stream` without the synchronous range check (Net.forward's), so the
+    host enqueues and returns at once."""
+    n, _, h, w = x.shape
+    o0 = torch.empty((n, 52, h // 8, w // 8), device=x.device)
+    o1 = torch.empty((n, 26, h // 8, w // 8), device=x.device)
+    rt.check(rt.lib().isl_net_forward(net.h, rt.ptr(x), n, h, w, rt.ptr(o0), rt.ptr(o1), rt.stream_handle(stream)),
+             "isl_net_forward")
+    return o0, o1
+
+
+def test_first_arena_on_nonblocking_stream_while_another_is_busy(w25):
+    """VERDICT r05 #4 (order, don't drain): a new arena is zeroed with hipMemsetAsync on the
+    caller's stream instead of a null-stream memset plus a device-wide drain.  While one
+    non-blocking stream is busy with a batch-8 368x656 forward, a second non-blocking stream
+    runs the first forward of two new sizes (new arenas: their rings and gap channels must be
+    zero before any conv reads them); each equals the same forward run alone, bit for bit.
+    The synchronous range check then waits on the two streams' events only."""
+    net = rt.Net(rt.ISL_BODY25)
+    net.load_weights(w25)
+    ref = rt.Net(rt.ISL_BODY25)
+    ref.load_weights(w25)
+    xa = torch.from_numpy(_inputs(8, 368, 656, seed=3)).cuda()
+    xb = torch.from_numpy(_inputs(2, 200, 264, seed=4)).cuda()
+    xc = torch.from_numpy(_inputs(3, 96, 136, seed=5)).cuda()
+    torch.cuda.synchronize()
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    pa, ha = _forward_async(net, xa, sa)        # long: ~6 ms of convs on sa
+    pb, hb = _forward_async(net, xb, sb)        # new arenas, first runs, on sb
+    pc, hc = _forward_async(net, xc, sb)
+    assert net.range_ok()                       # waits for sa's and sb's events, not the device
+    torch.cuda.synchronize()
+    for x, p, hh in ((xb, pb, hb), (xc, pc, hc), (xa, pa, ha)):
+        rp, rh = ref.forward(x)
+        torch.cuda.synchronize()
+        assert torch.equal(p, rp) and torch.equal(hh, rh)

@@ -55,7 +55,7 @@ def main(path, h=368, w=656, B=32, kind=0, quiet=False):
                 h //= 2; w //= 2
             ci += 2 if fused else 1
         else:
-            g = groups.setdefault(n.split("(")[0][:40], [0, 0.0, 0.0])
+            g = groups.setdefault(n.replace("(anonymous namespace)::", "").split("(")[0][:40], [0, 0.0, 0.0])
             g[0] += 1; g[1] += d
     for k, (cnt, d, fl) in sorted(groups.items(), key=lambda t: -t[1][1]):
         tf = fl / d / 1e6 if fl else 0.0

@@ -10,7 +10,7 @@ import csv
 
 
 def cls(name):
-    return name.split("(")[0].replace("void ", "").replace("isl::", "").split("<")[0]
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("isl::", "").split("<")[0]
 
 
 def main():

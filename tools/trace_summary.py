@@ -13,7 +13,7 @@ import os
 
 
 def cls(name):
-    return name.split("(")[0].replace("void ", "").replace("isl::", "").split("<")[0]
+    return name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("isl::", "").split("<")[0]
 
 
 def main():

@@ -8,7 +8,7 @@ OUT      := $(PKG)/islpose/libislpose.so
 # operation order bit-for-bit, which forbids fused multiply-adds.
 HIPFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -ffp-contract=off -Iinclude -I$(CSRC) \
             -Wall -Wno-unused-function -Wno-unused-variable -Wno-unused-lambda-capture
-SRCS     := $(CSRC)/conv.hip $(CSRC)/conv_x3.hip $(CSRC)/conv_c12.hip $(CSRC)/wino.hip $(CSRC)/ops.hip $(CSRC)/post.hip $(CSRC)/sign.hip $(CSRC)/runtime.cpp
+SRCS     := $(CSRC)/conv.hip $(CSRC)/conv_x3.hip $(CSRC)/conv_c12.hip $(CSRC)/wino_f16.hip $(CSRC)/wino.hip $(CSRC)/ops.hip $(CSRC)/post.hip $(CSRC)/sign.hip $(CSRC)/runtime.cpp
 OBJS     := $(patsubst $(CSRC)/%,build/%.o,$(SRCS))
 # development objects (tools/convbench): the product sources plus the rejected split-fp16
 # Winograd kernel and the s_memtime stamp variant, compiled with -DISLPOSE_DEV

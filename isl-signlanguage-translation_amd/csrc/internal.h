@@ -136,6 +136,7 @@ double conv_x3_mfma_flops(const ConvLaunch& c);
 constexpr int X3V_RGB = 1 << 18;
 constexpr int X3V_FOLD_OUT = 1 << 19;   // a split-K producer whose reduce was folded into its consumers
 constexpr int X3V_C12 = 4;              // conv1_1 -> conv1_2 -> pair-max in one launch (conv_c12.hip)
+constexpr int X3V_W2 = 64;              // split-fp16 Winograd F(2x2, 3x3) (wino_f16.hip)
 
 constexpr int x3_variant_code(int var, int ks, int bpx, int bco) {
   return (var & 0xfffff) | ((bpx / 32) << 20) | ((bco / 32) << 25) | ((ks / 2) << 29);
@@ -160,6 +161,12 @@ bool x3_fold_ok(const ConvLaunch& c);
 hipError_t launch_wino_x3(const ConvLaunch& c, hipStream_t s);
 double wino_x3_mfma_flops(const ConvLaunch& c);
 constexpr int WINO_X3_BCO = 64;
+// Split-fp16 Winograd F(2x2, 3x3) on 64-channel x 64-tile blocks (wino_f16.hip): 3x3 layers with
+// cout % 64 == 0, no fused pool / pooled input / fold, >= 32 tiles per row, > 1024 pixels per
+// frame; c.wx3 holds the pack_wino_f16 filters and c.wscale_inv their 2^-s.
+bool wino_f16_fits(const ConvLaunch& c);
+hipError_t launch_wino_f16(const ConvLaunch& c, hipStream_t s);
+double wino_f16_mfma_flops(const ConvLaunch& c);
 // FLOPs the matrix cores execute for one launch (tile padding included)
 double conv_mfma_flops(const ConvLaunch& c);
 double wino_mfma_flops(const ConvLaunch& c);

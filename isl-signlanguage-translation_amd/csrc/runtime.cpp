@@ -66,6 +66,8 @@ struct ConvLayer {
   float x3_inv = 1.f;            // 2^-s of the split weights
   void* d_wux3 = nullptr;        // split-fp16 Winograd filters (wino_x3.hip), 3x3 only
   float wx3_inv = 1.f;
+  void* d_ww = nullptr;          // split-fp16 Winograd filters of wino_f16.hip (3x3, cout % 64 == 0)
+  float ww_inv = 1.f;            // their 2^-s
   // the fused 1x1 pair (conv_x3 VAR 16): fuse6 marks the first layer (Mconv6), packed once
   // more for one tile of all its channels (d_wx3f, when bco < cout); fuse7 the second, packed
   // in the fused K order (d_wx3f7, pack_x3_f7)
@@ -551,6 +553,57 @@ static std::vector<_Float16> pack_x3(const ConvLayer& c, int bco, float* inv_sca
   return out;
 }
 
+// Split-fp16 Winograd filters for wino_f16.hip: U = G g G^T per (co, physical ci) in double,
+// scaled by a per-layer 2^s (max|U| * 2^s in [2^13, 2^14), as pack_x3), rounded to fp32 and
+// split hi + lo; layout [co_block 64][pair][xi 16][co tile i 2][hi|lo][h][32][8] -- one wave's
+// filters of a K step are 4 contiguous 1 KiB pieces (i, hi|lo), lane = h * 32 + co.
+static std::vector<_Float16> pack_wino_f16(const ConvLayer& c, float* inv_scale) {
+  const int chunks = c.cin_phys / 8, pairs = (chunks + 1) / 2, cob = c.cout / 64;
+  std::vector<int> p2l(pairs * 16, -1);
+  for (const Seg& sg : c.cmap)
+    for (int i = 0; i < sg.len; ++i) p2l[sg.phys + i] = sg.logical + i;
+  static const double G[4][3] = {{1, 0, 0}, {0.5, 0.5, 0.5}, {0.5, -0.5, 0.5}, {0, 0, 1}};
+  std::vector<double> U((size_t)c.cout * pairs * 16 * 16, 0.0);   // [co][pc][xi]
+  double mx = 0.0;
+  for (int co = 0; co < c.cout; ++co)
+    for (int pc = 0; pc < pairs * 16; ++pc) {
+      const int lci = p2l[pc];
+      if (lci < 0) continue;
+      const float* g = &c.w[((size_t)co * c.cin + lci) * 9];
+      double t[4][3];
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 3; ++j) t[i][j] = G[i][0] * g[0 * 3 + j] + G[i][1] * g[1 * 3 + j] + G[i][2] * g[2 * 3 + j];
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+          const double u = t[i][0] * G[j][0] + t[i][1] * G[j][1] + t[i][2] * G[j][2];
+          U[((size_t)co * pairs * 16 + pc) * 16 + 4 * i + j] = u;
+          mx = std::max(mx, std::fabs(u));
+        }
+    }
+  int e = 0;
+  if (mx > 0.0) {
+    std::frexp(mx, &e);
+    e = 14 - e;
+  }
+  const double scale = std::ldexp(1.0, e);
+  *inv_scale = std::ldexp(1.f, -e);
+  std::vector<_Float16> out((size_t)cob * pairs * 16 * 2 * 2 * 2 * 32 * 8, (_Float16)0.f);
+  for (int co = 0; co < c.cout; ++co)
+    for (int pc = 0; pc < pairs * 16; ++pc) {
+      if (p2l[pc] < 0) continue;
+      const int cb = co / 64, i = (co % 64) / 32, r = co % 32, pr = pc / 16, h = (pc % 16) / 8, k = pc % 8;
+      for (int xi = 0; xi < 16; ++xi) {
+        const float w = (float)(U[((size_t)co * pairs * 16 + pc) * 16 + xi] * scale);
+        const _Float16 hi = (_Float16)w;
+        const _Float16 lo = (_Float16)(w - (float)hi);
+        const size_t base = ((((size_t)cb * pairs + pr) * 16 + xi) * 2 + i) * 2;
+        out[(((base + 0) * 2 + h) * 32 + r) * 8 + k] = hi;
+        out[(((base + 1) * 2 + h) * 32 + r) * 8 + k] = lo;
+      }
+    }
+  return out;
+}
+
 // conv1_1 filters for conv_x3_rgb: K = 9 ky + 3 kx + c (27 real, padded to 32),
 // k = 16 kk + 8 h + j, layout [kk][hi|lo][h][64][8]; the same 2^s as pack_x3.
 static bool rgb_layer(const ConvLayer& c) {
@@ -818,6 +871,11 @@ static int upload_params(isl_net* net) {
       HIP_OK(hipMemcpy(c.d_wux3, up.data(), up.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     }
 #endif
+    if (c.k == 3 && c.cout % 64 == 0 && !rgb_layer(c)) {
+      std::vector<_Float16> up = pack_wino_f16(c, &c.ww_inv);
+      if (!c.d_ww) HIP_OK(hipMalloc(&c.d_ww, up.size() * sizeof(_Float16)));
+      HIP_OK(hipMemcpy(c.d_ww, up.data(), up.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    }
     if (c.wbco) {
       std::vector<float> up = pack_wino(c);
       if (!c.d_wu) HIP_OK(hipMalloc(&c.d_wu, up.size() * sizeof(float)));
@@ -1003,6 +1061,14 @@ static bool x3_wino_enabled() {
   return on;
 }
 #endif
+
+// 3x3 layers on chip-filling grids through the split-fp16 Winograd F(2x2, 3x3) kernel
+// (wino_f16.hip: 2.25x fewer MFMAs, fp32-accurate like conv_x3) where wino_f16_fits;
+// ISLPOSE_X3_W2=0: conv_x3 everywhere (A/B; read per launch)
+static bool w2_enabled() {
+  const char* e = getenv("ISLPOSE_X3_W2");
+  return !(e && e[0] == '0');
+}
 
 // ISLPOSE_RGB_CONV=0: conv1_1 on the generic split-fp16 kernel (A/B; read per launch)
 static bool rgb_kernel_enabled() {
@@ -1387,6 +1453,26 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
         L.hpool = 1;
         fused = true;
       }
+      // the Winograd kernel: plain 3x3 launches (no pool on either side, no fold, no K ranges)
+      if (!perm && w2_enabled() && c.d_ww && !L.vin && !L.hpool && far.fold_ws_off[k] < 0 &&
+          far.fold_tab_off[k] < 0 && x3_split_ranges(L, nullptr) <= 1) {
+        ConvLaunch Lw = L;
+        Lw.wx3 = c.d_ww;
+        Lw.wscale_inv = c.ww_inv;
+        if (wino_f16_fits(Lw)) {
+          HIP_OK(launch_wino_f16(Lw, s));
+          kind = 3;
+          mf = wino_f16_mfma_flops(Lw);
+          net->op_variant[k] = x3_variant_code(X3V_W2, 3, 128, 64);
+          if (tr) {
+            tr->kind.push_back(kind);
+            tr->flops.push_back(2.0 * c.cout * c.cin * c.k * c.k * (double)in.H * in.W * in.n);
+            tr->mfma_flops.push_back(mf);
+            HIP_OK(hipEventRecord(tr->ev[k + 1], s));
+          }
+          continue;
+        }
+      }
       const size_t need = x3_splitk_ws_floats(L);
       isl_net::Arena& ar = *net->cur;
       if (need > ar.ks_floats) {
@@ -1451,6 +1537,7 @@ static const char* const kRunKeySwitches[] = {
     "ISLPOSE_X3_TILES",  "ISLPOSE_X3_UNION", "ISLPOSE_X3_HALF64",  "ISLPOSE_X3_WIDE7",   "ISLPOSE_X3_ACROSS",
     "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67", "ISLPOSE_X3_G2", "ISLPOSE_X3_PX64", "ISLPOSE_X3_HALFSMALL",
     "ISLPOSE_X3_WR",     "ISLPOSE_X3_WR_WN", "ISLPOSE_C12",        "ISLPOSE_X3_TAIL",    "ISLPOSE_X3_SMALL7",
+    "ISLPOSE_X3_W2",
 #ifdef ISLPOSE_DEV
     "ISLPOSE_X3_HALFCO", "ISLPOSE_X3_PPS2",  "ISLPOSE_X3_M16",     "ISLPOSE_X3_WINO",    "ISLPOSE_X3_ABL",
 #endif
@@ -1680,6 +1767,7 @@ int isl_net_destroy(isl_net* net) {
     if (c.d_wx3w) (void)hipFree(c.d_wx3w);
     if (c.d_wrgb) (void)hipFree(c.d_wrgb);
     if (c.d_wux3) (void)hipFree(c.d_wux3);
+    if (c.d_ww) (void)hipFree(c.d_ww);
     if (c.d_wx3f) (void)hipFree(c.d_wx3f);
     if (c.d_wx3f7) (void)hipFree(c.d_wx3f7);
     if (c.d_wx3p) (void)hipFree(c.d_wx3p);

@@ -1,0 +1,413 @@
+// 3x3 convolution (stride 1, pad 1) as Winograd F(2x2, 3x3) on the gfx950 FP16 matrix
+// cores with split-fp16 (x3) products: the fp32-accurate arithmetic of conv_x3.hip on the
+// 16 Winograd GEMMs, for the 3x3 layers of src/model.py:25-64 (make_layers /
+// make_layers_Mconv) on chip-filling grids.
+//
+//   U = G g G^T   per (co, ci), host, double, x 2^s, split hi + lo     (pack_wino_f16)
+//   V = B^T d B   per (tile, ci), in the kernel from the staged input, fp32, then split
+//   M[xi] = sum_ci U[xi][co][ci] V[xi][ci][tile]   16 GEMMs, 3 fp16 MFMAs per product
+//   Y = A^T M A   the 2x2 outputs of a tile, x 2^-s + bias, activation, range check
+//
+// 16 products per 2x2 outputs instead of 36: 2.25x fewer MFMAs than conv_x3_f16.  The
+// transforms are exact-coefficient (0, +-1 for B and A; G's 1/2 in double on the host), so
+// the accuracy class is that of conv_x3 (rel err ~1e-6 vs the fp64 forward).
+//
+// Round 1's split-fp16 Winograd (wino_x3.hip, development build) lost 1.3-1.8x: 4 waves
+// of 64 channels computed all 16 V values of a tile per thread (184 VALU per (tile, channel),
+// redone for every 64-channel block) into a single-buffered 128 KB step.  This kernel is built
+// the other way round, so that no operand of the K loop is shared through LDS except the raw
+// input:
+//
+//   * Block = 16 waves, wave w owns xi = w (one GEMM) for 64 output channels x 64 tiles
+//     (2 x 2 accumulator tiles of 32 x 32, 64 registers).  U[xi] of the block is used by
+//     that wave alone, so its A fragments go straight from L2 into registers (4 x 16 B per
+//     lane and K step, loaded one step ahead) -- no LDS, no barrier for the filters.
+//   * V[xi] is also used by that wave alone: the wave builds its B fragments itself from
+//     the staged fp32 input, 4 pixels per (tile, channel) -- V[r][c] = (d[ra][ca] +
+//     sc d[ra][cb]) + sr (d[rb][ca] + sc d[rb][cb]), B^T's rows having two nonzeros each --
+//     3 fma + the split per value, 24 VALU per 8 values of a fragment.
+//   * The raw input of a K step (a chunk pair) arrives by LDS-DMA, double-buffered, one
+//     barrier per step.  The block's 64 tiles are consecutive in "band order" (a band = two
+//     tile rows, walked column-pair by column-pair), so they touch at most two bands and the
+//     staged run is 6 rows x (64 + 4) columns whatever the image width (26 KB per step).
+//     Layout [chunk half h][channel quad q][row 6][column parity][34] x 16 B: the lanes of
+//     a wave (consecutive band slots) read conflict-free ds_read_b128s (lane pairs 2k, 2k+1
+//     differ by two rows = 32 banks, lane pairs by 16 B).
+//   * Epilogue: the 16 waves' M tiles meet in LDS (two rounds of 32 channels, 128 KB), one
+//     thread per (4 channels, tile) sums them in a fixed order into the 2x2 outputs.
+//
+// Per K step and CU (16 waves of 12 MFMAs): 1536 MFMA cycles against ~1000 LDS cycles
+// (16 ds_read_b128 per wave), ~770 VALU cycles per SIMD and 64 KB of filters + 26 KB of
+// input from L2.  Eligible launches (wino_f16_fits): 3x3, cout % 64 == 0, no fused pool or
+// pooled-input staging, at least 32 tiles per row and > 1024 pixels per frame (no
+// canonical K ranges: those layers keep conv_x3's batch-invariant sums).
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#include "internal.h"
+
+namespace isl {
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct W2Args {
+  const float* in;
+  float* out;
+  const f16x8* upk;             // [co_block][pair][xi][i 2][hi|lo][h][32] x 8 fp16 (pack_wino_f16)
+  const float* bias;
+  const float* slope;
+  int* range_flag;
+  long long in_fs, in_chs, out_fs, out_chs;   // frame / chunk strides (floats)
+  float wscale_inv;             // 2^-s
+  int in_pad, out_pad, H, W, TH, TW, pairs, cin_chunks, co_blocks, bpf, act, nblocks;
+};
+
+constexpr int RS = 34;                  // 16-byte units per staged (row, column parity): 68 columns
+constexpr int QS = 6 * 2 * RS;          // per (chunk half, channel quad): 6 rows x 2 parities
+constexpr int HS = 13 * 64;             // per chunk half: 2 quads (816 units) in 13 whole DMA pieces
+constexpr int BUF = 32 * 64;            // 2048 units (32 KiB): 32 DMA pieces of 64 units, 2 per wave
+
+// v = hi + lo for 4 fp32 values into slots 4q .. 4q+3 of the fp16 fragments: the same bits as
+// hi = (f16)v; lo = (f16)(v - (f32)hi) (conv_x3's x3_split8)
+template <int Q>
+__device__ __forceinline__ void split4(const f32x4& v, f16x8& hi, f16x8& lo) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const f32x2 x = f32x2{v[2 * k], v[2 * k + 1]};
+    const f16x2 hh = __builtin_convertvector(x, f16x2);
+    const f32x2 hf = __builtin_convertvector(hh, f32x2);
+    const f32x2 r = x - hf;
+    const f16x2 ll = __builtin_convertvector(r, f16x2);
+    hi[4 * Q + 2 * k] = hh.x;
+    hi[4 * Q + 2 * k + 1] = hh.y;
+    lo[4 * Q + 2 * k] = ll.x;
+    lo[4 * Q + 2 * k + 1] = ll.y;
+  }
+}
+
+__global__ void __launch_bounds__(1024, 1) wino_f16(W2Args a) {
+  __shared__ f32x4 smem[8192];   // 128 KiB: the K loop's raw and filter buffers, then the M exchange
+
+  // XCD-aware order (conv_x3): the channel blocks of a tile block, then neighbouring tile
+  // blocks, on one XCD, so the staged input is read from one L2
+  int bid = blockIdx.x;
+  {
+    const int nb = a.nblocks, q = nb >> 3, r = nb & 7, xcd = bid & 7, k = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+  }
+  const int co_b = bid % a.co_blocks;
+  const int rest = bid / a.co_blocks;
+  const int fb = rest % a.bpf;
+  const int n = rest / a.bpf;
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int xi = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // the block's 64 band slots s0 .. s0 + 63: band b = tile rows 2b, 2b + 1; slot u of a band =
+  // tile (2b + (u & 1), u >> 1).  They lie in band ba and, past its end, in band bb = ba + 1
+  // (TW >= 32); segment 0 = band ba's columns from txlo0, segment 1 = band bb's from 0
+  const int BW = 2 * a.TW, s0 = fb * 64;
+  const int ba = s0 / BW, bb = (s0 + 63) / BW;
+  const bool two = bb > ba;
+  const int txlo0 = (s0 - ba * BW) >> 1;
+  const int txhi0 = two ? a.TW - 1 : (s0 + 63 - ba * BW) >> 1;
+  const int w0 = 2 * (txhi0 - txlo0 + 1) + 2;                    // staged columns of segment 0
+  const int w1 = two ? 2 * (((s0 + 63 - bb * BW) >> 1) + 1) + 2 : 0;
+  const int Hp = a.H + 2 * a.in_pad, Wp = a.W + 2 * a.in_pad;
+  const float* in_f = a.in + (size_t)n * a.in_fs;
+
+  // Roles (whole loops per role, so that hipcc's wait-count pass never sees an LDS-DMA and a
+  // register load of the same wave in flight together -- it would drain the DMA in front of the
+  // MFMAs): the 8 even waves ("DMA waves", d = xi / 2) stage the raw input of the next pair
+  // (4 pieces each) and their own filters of the next pair (4 pieces) by LDS-DMA and read their
+  // A fragments from LDS; the 8 odd waves load their A fragments into registers one step ahead.
+  const bool dma_role = (xi & 1) == 0;
+  const int d = xi >> 1;
+  // Raw pieces of a DMA wave: p = d + 8 e, 64 units each.  Piece p stages chunk half hp = p / 13
+  // of the pair (13 pieces = 832 units per half: [q][row 6][parity][34] + 16 spare); pieces
+  // 26 .. 31 are spare (they reload pixel 0 into the buffer's tail).  Lane unit -> (q, row,
+  // parity, half column) -> the padded input pixel; rows / columns past the buffer, which only
+  // feed discarded outputs, are clamped.  The chunk is wave-uniform: a uniform base plus a
+  // 32-bit lane offset.
+  int doff[4], dch[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int p = d + 8 * e;
+    const int hp = p < 26 ? p / 13 : 0;
+    const int w = (p - 13 * hp) * 64 + lane;             // unit within the half's region
+    int t = w / RS;
+    const int hc = w - t * RS;
+    const int par = t & 1;
+    t >>= 1;
+    const int row = t % 6;
+    const int qq = t / 6;
+    const int v = 2 * hc + par;
+    const bool s1 = v >= w0;
+    const int vl = s1 ? v - w0 : v;
+    const bool ok = p < 26 && qq < 2 && vl < (s1 ? w1 : w0);
+    const int band = s1 ? bb : ba, txlo = s1 ? 0 : txlo0;
+    const int rp = min(4 * band - 1 + row + a.in_pad, Hp - 1);
+    const int cp = min(2 * txlo - 1 + vl + a.in_pad, Wp - 1);
+    doff[e] = ok ? (rp * Wp + cp) * 8 + qq * 4 : 0;
+    dch[e] = __builtin_amdgcn_readfirstlane(hp);
+  }
+
+  // this wave's transform: V[r][c] = (d[ra][ca] + sc d[ra][cb]) + sr (d[rb][ca] + sc d[rb][cb])
+  // (B^T rows: d0 - d2, d1 + d2, d2 - d1, d1 - d3); the 4 pixels' unit offsets are wave-uniform
+  const int wr = xi >> 2, wc = xi & 3;
+  const int ra = wr == 0 ? 0 : wr == 2 ? 2 : 1, rb = wr == 3 ? 3 : wr == 2 ? 1 : 2;
+  const int ca = wc == 0 ? 0 : wc == 2 ? 2 : 1, cb = wc == 3 ? 3 : wc == 2 ? 1 : 2;
+  const float sr = wr == 1 ? 1.f : -1.f, sc = wc == 1 ? 1.f : -1.f;
+  const int toff0 = (ra * 2 + (ca & 1)) * RS + (ca >> 1), toff1 = (ra * 2 + (cb & 1)) * RS + (cb >> 1);
+  const int toff2 = (rb * 2 + (ca & 1)) * RS + (ca >> 1), toff3 = (rb * 2 + (cb & 1)) * RS + (cb >> 1);
+  // per tile tile j the lane's unit base in a raw buffer (chunk half h, quad 0, row 2 typ, parity 0)
+  int tb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int s = s0 + 32 * j + l32;
+    const int band = s / BW, u = s - band * BW, tx = u >> 1, typ = u & 1;
+    const int hc0 = band > ba ? (w0 >> 1) + tx : tx - txlo0;
+    tb[j] = h * HS + 2 * typ * 2 * RS + hc0;
+  }
+
+  f16x8 A[2][2];
+  // U[co_b][pair k][xi][i][hi|lo][h][32 co] of this wave: 4 pieces of 64 x 16 B (lane = h * 32 + co)
+  auto ubase = [&](int k) __attribute__((always_inline)) {
+    return a.upk + ((size_t)(co_b * a.pairs + k) * 16 + xi) * 256;
+  };
+  // LDS: raw buffers [2][BUF]; the DMA waves' filter buffers [2][8 waves][4 pieces][64] after them
+  f32x4* const ubuf = smem + 2 * BUF;
+  auto load_a = [&](int k) __attribute__((always_inline)) {   // register role
+    const f16x8* ub = ubase(k);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) A[i][hl] = ub[(i * 2 + hl) * 64 + lane];
+  };
+  auto read_a = [&](int buf) __attribute__((always_inline)) {   // DMA role
+    const f16x8* su = (const f16x8*)(ubuf + (buf * 8 + d) * 256);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int hl = 0; hl < 2; ++hl) A[i][hl] = su[(i * 2 + hl) * 64 + lane];
+  };
+  auto dma = [&](int k, int buf) __attribute__((always_inline)) {   // DMA role
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ch = min(2 * k + dch[e], a.cin_chunks - 1);   // a missing odd chunk: zero filters
+      const float* src = in_f + (size_t)ch * a.in_chs;
+      __builtin_amdgcn_global_load_lds((const void*)(src + doff[e]),
+                                       (__attribute__((address_space(3))) void*)(smem + buf * BUF + (d + 8 * e) * 64),
+                                       16, 0, 0);
+    }
+    const f16x8* ub = ubase(k);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      __builtin_amdgcn_global_load_lds((const void*)(ub + e * 64 + lane),
+                                       (__attribute__((address_space(3))) void*)(ubuf + ((buf * 8 + d) * 4 + e) * 64),
+                                       16, 0, 0);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float vmax = 0.f;   // max |V|: the split needs |V| < 65504 (range guard)
+
+  // per tile tile j: the B fragments (the transform) from raw buffer bo and the 6 MFMAs
+  auto compute = [&](int bo) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int b = tb[j] + bo;
+      asm volatile("" : "+v"(b));   // the 4 pixel addresses are formed per step (not held across it)
+      f16x8 Bh, Bl;
+      auto quad = [&](auto qc) __attribute__((always_inline)) {
+        constexpr int Q = decltype(qc)::value;
+        const f32x4 d0 = smem[b + toff0 + Q * QS], d1 = smem[b + toff1 + Q * QS];
+        const f32x4 d2 = smem[b + toff2 + Q * QS], d3 = smem[b + toff3 + Q * QS];
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t0 = __builtin_fmaf(sc, d1[e], d0[e]);
+          const float t1 = __builtin_fmaf(sc, d3[e], d2[e]);
+          v[e] = __builtin_fmaf(sr, t1, t0);
+        }
+        vmax = __builtin_fmaxf(vmax, __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(v[0]), __builtin_fabsf(v[1])),
+                                                     __builtin_fmaxf(__builtin_fabsf(v[2]), __builtin_fabsf(v[3]))));
+        split4<Q>(v, Bh, Bl);
+      };
+      quad(std::integral_constant<int, 0>{});
+      quad(std::integral_constant<int, 1>{});
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[i][0], Bh, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[i][0], Bl, acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[i][1], Bh, acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  // K loop, one step per chunk pair k (raw buffer k & 1), one barrier per step.  DMA waves: the
+  // next pair's input and filters by DMA, this pair's A from LDS, compute, then wait for their
+  // DMA and meet; register waves: compute, then the next pair's A into registers (in flight
+  // across the barrier).  Loads past the last pair repeat it (uniform wait counts).
+  auto run = [&](auto role) __attribute__((always_inline)) {
+    constexpr bool DMA = decltype(role)::value;
+    if constexpr (DMA) {
+      dma(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      load_a(0);
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    for (int k = 0; k < a.pairs; ++k) {
+      const int buf = k & 1;
+      if constexpr (DMA) {
+        dma(min(k + 1, a.pairs - 1), buf ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+        read_a(buf);
+      }
+      compute(buf * BUF);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (DMA) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      } else {
+        load_a(min(k + 1, a.pairs - 1));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if (dma_role) run(std::true_type{});
+  else run(std::false_type{});
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: M tiles through LDS, per round i (32 channels) [xi][j][q][h][32] x f32x4 (128 KB);
+  // thread (j, q, h, tile) of the first 512 sums its 4 channels' 16 values in a fixed order
+  bool bad = !(vmax < 65504.f);
+  f32x4* xm = smem;
+  const int Wo = a.W + 2 * a.out_pad;
+  float* out_f = a.out + (size_t)n * a.out_fs;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        xm[(((xi * 2 + j) * 4 + q) * 2 + h) * 32 + l32] =
+            f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+    __syncthreads();
+    if (tid < 512) {
+      const int rn = tid & 31, rh = (tid >> 5) & 1, rq = (tid >> 6) & 3, rj = tid >> 8;
+      const f32x4* mp = xm + ((rj * 4 + rq) * 2 + rh) * 32 + rn;   // + xi * 8 KiB (512 units)
+      // Y = A^T M A: rows R0[c] = M0c + M1c + M2c, R1[c] = M1c - M2c - M3c; then the columns
+      f32x4 R0[4], R1[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const f32x4 m0 = mp[(0 + c) * 512], m1 = mp[(4 + c) * 512], m2 = mp[(8 + c) * 512], m3 = mp[(12 + c) * 512];
+        R0[c] = (m0 + m1) + m2;
+        R1[c] = (m1 - m2) - m3;
+      }
+      f32x4 Y[2][2];
+      Y[0][0] = (R0[0] + R0[1]) + R0[2];
+      Y[0][1] = (R0[1] - R0[2]) - R0[3];
+      Y[1][0] = (R1[0] + R1[1]) + R1[2];
+      Y[1][1] = (R1[1] - R1[2]) - R1[3];
+      const int co = co_b * 64 + i * 32 + 8 * rq + 4 * rh;
+      const f32x4 b = *(const f32x4*)(a.bias + co);
+      const f32x4 sl = a.act == ACT_PRELU ? *(const f32x4*)(a.slope + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int s = s0 + 32 * rj + rn, band = s / BW, u = s - band * BW, tx = u >> 1, ty = 2 * band + (u & 1);
+      if (ty < a.TH) {
+        float* oc = out_f + (size_t)(co >> 3) * a.out_chs + (co & 7);
+#pragma unroll
+        for (int yy = 0; yy < 2; ++yy)
+#pragma unroll
+          for (int xx = 0; xx < 2; ++xx) {
+            const int y = 2 * ty + yy, x = 2 * tx + xx;
+            if (y >= a.H || x >= a.W) continue;
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = Y[yy][xx][e] * a.wscale_inv + b[e];
+            if (a.act == ACT_RELU) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+            } else if (a.act == ACT_PRELU) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bad |= !(__builtin_fabsf(v[e]) < 65504.f);
+            *(f32x4*)(oc + (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8) = v;
+          }
+      }
+    }
+    __syncthreads();
+  }
+  if (bad) atomicOr(a.range_flag, 1);
+}
+
+int g_wino_blocks(const ConvLaunch& c, int* bpf) {
+  const int TH = (c.H + 1) / 2, TW = (c.W + 1) / 2, nbands = (TH + 1) / 2;
+  *bpf = (nbands * 2 * TW + 63) / 64;
+  return c.n * *bpf * (c.cout / 64);
+}
+
+}  // namespace
+
+bool wino_f16_fits(const ConvLaunch& c) {
+  return c.ks == 3 && c.in_pad >= 1 && c.cout % 64 == 0 && c.cout > 0 && !c.hpool && !c.vin && !c.fold &&
+         c.cout7 == 0 && (c.W + 1) / 2 >= 32 && (long long)c.H * c.W > 1024 &&
+         !((c.in_cs | c.in_coff | c.out_cs | c.out_coff) & 7) && (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8 < (1ll << 30);
+}
+
+hipError_t launch_wino_f16(const ConvLaunch& c, hipStream_t s) {
+  if (!wino_f16_fits(c)) { set_error("wino_f16: launch not eligible"); return hipErrorInvalidValue; }
+  if (!c.wx3 || !c.range_flag) { set_error("wino_f16: split filters / range flag missing"); return hipErrorInvalidValue; }
+  W2Args a{};
+  a.in_chs = (long long)(c.H + 2 * c.in_pad) * (c.W + 2 * c.in_pad) * 8;
+  a.out_chs = (long long)(c.H + 2 * c.out_pad) * (c.W + 2 * c.out_pad) * 8;
+  a.in_fs = a.in_chs * (c.in_cs / 8);
+  a.out_fs = a.out_chs * (c.out_cs / 8);
+  a.in = c.in + (c.in_coff / 8) * a.in_chs;
+  a.out = c.out + (c.out_coff / 8) * a.out_chs;
+  a.upk = (const f16x8*)c.wx3;
+  a.bias = c.bias;
+  a.slope = c.slope;
+  a.range_flag = c.range_flag;
+  a.wscale_inv = c.wscale_inv;
+  a.in_pad = c.in_pad;
+  a.out_pad = c.out_pad;
+  a.H = c.H;
+  a.W = c.W;
+  a.TH = (c.H + 1) / 2;
+  a.TW = (c.W + 1) / 2;
+  a.pairs = (c.cin_chunks + 1) / 2;
+  a.cin_chunks = c.cin_chunks;
+  a.co_blocks = c.cout / 64;
+  a.act = c.act;
+  const long long nb = g_wino_blocks(c, &a.bpf);
+  if (nb <= 0 || nb > 0x7fffffff) { set_error("wino_f16: bad grid"); return hipErrorInvalidValue; }
+  a.nblocks = (int)nb;
+  hipLaunchKernelGGL(wino_f16, dim3(a.nblocks), dim3(1024), 0, s, a);
+  return hipGetLastError();
+}
+
+double wino_f16_mfma_flops(const ConvLaunch& c) {
+  int bpf = 0;
+  const double nb = g_wino_blocks(c, &bpf);
+  return nb * 16.0 * 64 * 64 * 16.0 * ((c.cin_chunks + 1) / 2) * 2 * 3;
+}
+
+}  // namespace isl

@@ -180,7 +180,8 @@ def ptr(t) -> ctypes.c_void_p:
 
 def decode_variant(code: int) -> dict:
     """isl_net_op_info's variant code -> dict(var=VAR bits, bpx, bco, ks, rgb, pool_fused, ...):
-    wave_ranges (conv_x3_wr, VAR 8), c12 (conv1_1 -> conv1_2 in one launch, 4)."""
+    wave_ranges (conv_x3_wr, VAR 8), c12 (conv1_1 -> conv1_2 in one launch, 4), wino2 (the
+    split-fp16 Winograd kernel wino_f16, 64)."""
     if code == -1:
         return {"pool_fused": True}
     if code == -2:
@@ -194,7 +195,7 @@ def decode_variant(code: int) -> dict:
             "union": bool(code & 512), "ranged": bool(code & 1024), "split": bool(code & 2048),
             "pairs2": bool(code & 4096), "vin": bool(code & 32768), "sib": bool(code & 65536),
             "fold": bool(code & 8192), "m16": bool(code & 131072), "fold_out": bool(code & (1 << 19)),
-            "wave_ranges": bool(code & 8), "c12": bool(code & 4)}
+            "wave_ranges": bool(code & 8), "c12": bool(code & 4), "wino2": bool(code & 64)}
 
 
 class Net:

@@ -45,10 +45,12 @@ PEAK_HBM_GBPS = 8000.0             # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 MFMA_LOOP_CEILING_TF = 1549.0      # measured: bare x3 3x3 step loop, 32x32x16, all CUs (profiles/r02/mfma_shape/)
 KIND = {0: "maxpool2_kernel", 1: "conv_mfma_f32 (direct fp32)", 2: "wino_f23_mfma (Winograd F(2x2,3x3) fp32)",
         3: "conv_x3_f16 (split-fp16 x3, fp32-accurate)",
-        4: "wino_x3_f16 (Winograd F(2x2,3x3), split-fp16 x3, fp32-accurate)"}
+        4: "wino_x3_f16 (Winograd F(2x2,3x3), split-fp16 x3, fp32-accurate)",
+        5: "wino_f16 (Winograd F(2x2,3x3), split-fp16 x3, fp32-accurate)"}
 # MFMA FLOPs the algorithm of each kind needs per direct-conv FLOP (2*Cout*Cin*k*k*H*W), tile padding excluded
-ALG_FACTOR = {1: 1.0, 2: 16.0 / 36.0, 3: 3.0, 4: 3.0 * 16.0 / 36.0}
-KIND_PEAK = {1: PEAK_FP32_MFMA_TFLOPS, 2: PEAK_FP32_MFMA_TFLOPS, 3: PEAK_FP16_MFMA_TFLOPS, 4: PEAK_FP16_MFMA_TFLOPS}
+ALG_FACTOR = {1: 1.0, 2: 16.0 / 36.0, 3: 3.0, 4: 3.0 * 16.0 / 36.0, 5: 3.0 * 16.0 / 36.0}
+KIND_PEAK = {1: PEAK_FP32_MFMA_TFLOPS, 2: PEAK_FP32_MFMA_TFLOPS, 3: PEAK_FP16_MFMA_TFLOPS, 4: PEAK_FP16_MFMA_TFLOPS,
+             5: PEAK_FP16_MFMA_TFLOPS}
 
 
 def parse(argv=None):
@@ -480,9 +482,9 @@ def roofline_of(ops):
     fp32_equiv = dk["flops"] / sec / 1e12                      # direct-conv FLOPs per second
     achieved = ALG_FACTOR.get(dom, 1.0) * dk["flops"] / sec / 1e12   # MFMA work the algorithm needs, no padding
     executed = dk["mfma_flops"] / sec / 1e12                   # what the matrix cores ran (tile padding included)
-    conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3, 4))
-    conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3, 4))
-    key = {1: "direct", 2: "wino", 3: "x3", 4: "wino_x3"}.get(dom, "x3")
+    conv_ms = sum(v["ms"] for k, v in kinds.items() if k in (1, 2, 3, 4, 5))
+    conv_flops = sum(v["flops"] for k, v in kinds.items() if k in (1, 2, 3, 4, 5))
+    key = {1: "direct", 2: "wino", 3: "x3", 4: "wino_x3", 5: "w2"}.get(dom, "x3")
     traffic = mfma_busy = clk = busy_s = clk_s = stage_busy = stage_busy_s = src = None
     prof = os.path.join(REPO, "profiles", "conv_traffic.json")
     if os.path.exists(prof):

@@ -1461,7 +1461,7 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
         Lw.wscale_inv = c.ww_inv;
         if (wino_f16_fits(Lw)) {
           HIP_OK(launch_wino_f16(Lw, s));
-          kind = 3;
+          kind = 5;   // (isl_net_timing's op kinds: 1 fp32 direct, 2 fp32 Winograd, 3 split-fp16 direct, 5 wino_f16)
           mf = wino_f16_mfma_flops(Lw);
           net->op_variant[k] = x3_variant_code(X3V_W2, 3, 128, 64);
           if (tr) {

@@ -91,6 +91,10 @@ __device__ __forceinline__ void split4(const f32x4& v, f16x8& hi, f16x8& lo) {
   }
 }
 
+// ABL (development build only, tools/convbench "w2" with ISLPOSE_W2_ABL): timing ablations --
+// 1 no MFMAs, 2 no transform (no raw LDS reads, no VALU; constant B), 4 no filter loads, 8 no
+// raw-input DMA, 16 no epilogue.  Wrong results; libislpose.so has ABL = 0 only.
+template <int ABL>
 __global__ void __launch_bounds__(1024, 1) wino_f16(W2Args a) {
   __shared__ f32x4 smem[8192];   // 128 KiB: the K loop's raw and filter buffers, then the M exchange
 
@@ -184,6 +188,11 @@ __global__ void __launch_bounds__(1024, 1) wino_f16(W2Args a) {
   // LDS: raw buffers [2][BUF]; the DMA waves' filter buffers [2][8 waves][4 pieces][64] after them
   f32x4* const ubuf = smem + 2 * BUF;
   auto load_a = [&](int k) __attribute__((always_inline)) {   // register role
+    if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) A[i][0] = A[i][1] = f16x8{1, 1, 1, 1, 1, 1, 1, 1};
+      return;
+    }
     const f16x8* ub = ubase(k);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -200,6 +209,7 @@ __global__ void __launch_bounds__(1024, 1) wino_f16(W2Args a) {
   auto dma = [&](int k, int buf) __attribute__((always_inline)) {   // DMA role
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
+      if constexpr ((ABL & 8) != 0) break;
       const int ch = min(2 * k + dch[e], a.cin_chunks - 1);   // a missing odd chunk: zero filters
       const float* src = in_f + (size_t)ch * a.in_chs;
       __builtin_amdgcn_global_load_lds((const void*)(src + doff[e]),
@@ -209,6 +219,7 @@ __global__ void __launch_bounds__(1024, 1) wino_f16(W2Args a) {
     const f16x8* ub = ubase(k);
 #pragma unroll
     for (int e = 0; e < 4; ++e)
+      if constexpr ((ABL & 4) == 0)
       __builtin_amdgcn_global_load_lds((const void*)(ub + e * 64 + lane),
                                        (__attribute__((address_space(3))) void*)(ubuf + ((buf * 8 + d) * 4 + e) * 64),
                                        16, 0, 0);
@@ -230,6 +241,10 @@ __global__ void __launch_bounds__(1024, 1) wino_f16(W2Args a) {
       int b = tb[j] + bo;
       asm volatile("" : "+v"(b));   // the 4 pixel addresses are formed per step (not held across it)
       f16x8 Bh, Bl;
+      if constexpr ((ABL & 2) != 0) {
+        Bh = f16x8{1, 1, 1, 1, 1, 1, 1, 1};
+        Bl = Bh;
+      }
       auto quad = [&](auto qc) __attribute__((always_inline)) {
         constexpr int Q = decltype(qc)::value;
         const f32x4 d0 = smem[b + toff0 + Q * QS], d1 = smem[b + toff1 + Q * QS];
@@ -245,10 +260,13 @@ __global__ void __launch_bounds__(1024, 1) wino_f16(W2Args a) {
                                                      __builtin_fmaxf(__builtin_fabsf(v[2]), __builtin_fabsf(v[3]))));
         split4<Q>(v, Bh, Bl);
       };
-      quad(std::integral_constant<int, 0>{});
-      quad(std::integral_constant<int, 1>{});
+      if constexpr ((ABL & 2) == 0) {
+        quad(std::integral_constant<int, 0>{});
+        quad(std::integral_constant<int, 1>{});
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
+        if constexpr ((ABL & 1) != 0) continue;
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[i][0], Bh, acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[i][0], Bl, acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[i][1], Bh, acc[i][j], 0, 0, 0);
@@ -294,6 +312,7 @@ __global__ void __launch_bounds__(1024, 1) wino_f16(W2Args a) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
+  if constexpr ((ABL & 16) != 0) return;
   // epilogue: M tiles through LDS, per round i (32 channels) [xi][j][q][h][32] x f32x4 (128 KB);
   // thread (j, q, h, tile) of the first 512 sums its 4 channels' 16 values in a fixed order
   bool bad = !(vmax < 65504.f);
@@ -400,7 +419,16 @@ hipError_t launch_wino_f16(const ConvLaunch& c, hipStream_t s) {
   const long long nb = g_wino_blocks(c, &a.bpf);
   if (nb <= 0 || nb > 0x7fffffff) { set_error("wino_f16: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
-  hipLaunchKernelGGL(wino_f16, dim3(a.nblocks), dim3(1024), 0, s, a);
+#ifdef ISLPOSE_DEV
+  const int abl = getenv("ISLPOSE_W2_ABL") ? atoi(getenv("ISLPOSE_W2_ABL")) : 0;
+  switch (abl) {
+#define W2ABL(k) case k: hipLaunchKernelGGL(wino_f16<k>, dim3(a.nblocks), dim3(1024), 0, s, a); return hipGetLastError();
+    W2ABL(1) W2ABL(2) W2ABL(3) W2ABL(4) W2ABL(6) W2ABL(8) W2ABL(12) W2ABL(14) W2ABL(16) W2ABL(31)
+#undef W2ABL
+    default: break;
+  }
+#endif
+  hipLaunchKernelGGL(wino_f16<0>, dim3(a.nblocks), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 

@@ -64,6 +64,9 @@ int main(int argc, char** argv) {
   float* wu = wb ? dev_random<float>((size_t)(cout / wb) * chunks * 16 * 2 * wb * 4, -0.05f, 0.05f, 4) : nullptr;
   const int wxt = (cout + 63) / 64;
   _Float16* wux = dev_random<_Float16>((size_t)wxt * pairs * 16 * 4 * 64 * 8, -8192.f, 8192.f, 7);
+  // split-fp16 Winograd filters of wino_f16 (w2): [cout/64][pair][16][2][2][2][32][8]
+  _Float16* ww = cout % 64 == 0 ? dev_random<_Float16>((size_t)(cout / 64) * pairs * 16 * 8 * 32 * 8, -8192.f, 8192.f, 9)
+                                : nullptr;
   _Float16* f7w = dev_random<_Float16>((size_t)2 * ((cout + 15) / 16) * 2 * 64 * 8, -8192.f, 8192.f, 8);
   float* bias = dev_random<float>(co_tiles * 256 + 256, -0.05f, 0.05f, 5);
   float* slope = dev_random<float>(co_tiles * 256 + 256, 0.05f, 0.25f, 6);
@@ -142,6 +145,8 @@ int main(int argc, char** argv) {
         if (a == "direct") { c.bco = bco; c.wpk = wd; return launch_conv(c, 0); }
         if (a == "wino" && wb && ks == 3) { c.bco = wb; c.wpk = wu; return launch_wino(c, 0); }
         if (a == "wx3" && ks == 3) { c.wx3 = wux; return launch_wino_x3(c, 0); }
+        // w2: the split-fp16 Winograd kernel wino_f16 (ISLPOSE_W2_ABL: its timing ablations)
+        if (a == "w2" && ww && wino_f16_fits(c)) { c.wx3 = ww; return launch_wino_f16(c, 0); }
         return hipErrorNotSupported;
       };
       if (launch() != hipSuccess) continue;
@@ -171,7 +176,7 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, e0, e1));
       }
       const double us = ms * 1e3 / iters;
-      const double fac = (a == "x3" || a == "x3f" || a == "x3m" || a == "x3h" || a == "x3p" || a == "x3d") ? 3.0 : a == "wx3" ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
+      const double fac = (a == "x3" || a == "x3f" || a == "x3m" || a == "x3h" || a == "x3p" || a == "x3d") ? 3.0 : (a == "wx3" || a == "w2") ? 3.0 * 16 / 36 : a == "wino" ? 16.0 / 36 : 1.0;
       printf("  round %d %-7s %9.1f us  fp32-equiv %7.1f TF  alg-MFMA %7.1f TF\n", r, a.c_str(), us,
              flops / us / 1e6, fac * flops / us / 1e6);
     }

@@ -89,6 +89,10 @@ def parse(argv=None):
                         "(BodyEstimator.launch(post_stream=...)); measured +0.8 %% Mode N, +0-5 %% Mode R, "
                         "+5 %% at batch 1, but the post then slows the concurrent convs (Mode N frac 0.446 -> "
                         "0.439, Mode R 0.34 -> 0.29), so off by default (profiles/r03/post_overlap/)")
+    p.add_argument("--frame-count", type=int, default=64,
+                   help="the unchanged scripts' per-frame path (ISLSignPos.call on sequential 1080x1920 frames, "
+                        "extract_features_mp.py:125-130) timed over this many frames after the headline, reported "
+                        "as the 'frame' sub-object (rank 0; 0 = skip)")
     p.add_argument("--no-mode-r", dest="mode_r", action="store_false",
                    help="skip the Mode R sub-measurement (net 184x328 at batch 32 and batch 1)")
     p.add_argument("--pg-timeout", type=float, default=120.0,
@@ -456,10 +460,26 @@ def gpu_main(args, rank, local, world):
         "e2e": e2e,
         "cpu_baseline": None,
     }
+    if args.frame_count > 0:
+        out["frame"] = frame_leg(args)
     if not args.no_cpu and args.cpu_frames > 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(args, mult, nh, nw)
     print(json.dumps(out))
     sys.stdout.flush()
+
+
+def frame_leg(args):
+    """The unchanged reference scripts' per-frame path: ISLSignPos.call on
+    sequential 1080x1920 frames (extract_features_mp.py:125-130), body and hand ms per frame
+    and the conv launches per frame -- tools/bench_configs.py's FRAME leg, run in this
+    invocation after the headline (rank 0)."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import bench_configs
+    ns = argparse.Namespace(frame_count=args.frame_count)
+    try:
+        return bench_configs.frame(ns)
+    except Exception as e:   # never lose the headline line to the sub-measurement
+        return {"error": "%s: %s" % (type(e).__name__, e)}
 
 
 def roofline_of(ops):

@@ -183,7 +183,7 @@ def c5(args):
 def frame(args):
     """ISLSignPos.call per frame, 1080x1920 RGB frames flipped to BGR as a view (the script's
     frame[:, :, ::-1]); every call returns to the host (numpy results), as in the script."""
-    from islpose import synth
+    from islpose import runtime as rt, synth
     from islpose.body import BodyEstimator
     from src import util
     from src.body import Body
@@ -214,7 +214,18 @@ def frame(args):
         (c, sb), = body.estimate(isl._upload(f))
         widths += [w for _, _, w, _ in util.handDetect(c, sb, f)]
     db = time.perf_counter() - t0
+    # conv launches per frame: the body net (one run) and the hand net (one run per scale of the
+    # frame's crop batch), from the op variants of their last runs; a split-K layer adds its reduce
+    hand = isl._estimators()[1]
+
+    def launches(net):
+        codes = [v for _, v in net.op_variants()]
+        return sum(1 for v in codes if v not in (-1, -2)) + sum(1 for v in codes if rt.decode_variant(v).get("split"))
+    body_launches = launches(body.net)
+    hand_launches = launches(hand.net) if crops else 0   # (the last scale the hand net ran)
     return {"config": "FRAME ISLSignPos.call per 1080x1920 frame (extract_features_mp.py:130 pattern)",
+            "body_conv_launches_per_frame": body_launches,
+            "hand_conv_launches_last_scale": hand_launches,
             "frames": T, "frames_per_s": round(T / dt, 2), "ms_per_frame": round(dt / T * 1e3, 3),
             "body_ms_per_frame": round(db / T * 1e3, 3), "hand_ms_per_frame": round((dt - db) / T * 1e3, 3),
             "hand_crops_per_frame": round(crops / T, 2),

@@ -55,6 +55,7 @@ typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 struct W2Args {
   const float* in;
@@ -73,22 +74,17 @@ constexpr int QS = 6 * 2 * RS;          // per (chunk half, channel quad): 6 row
 constexpr int HS = 13 * 64;             // per chunk half: 2 quads (816 units) in 13 whole DMA pieces
 constexpr int BUF = 32 * 64;            // 2048 units (32 KiB): 32 DMA pieces of 64 units, 2 per wave
 
-// v = hi + lo for 4 fp32 values into slots 4q .. 4q+3 of the fp16 fragments: the same bits as
-// hi = (f16)v; lo = (f16)(v - (f32)hi) (conv_x3's x3_split8)
-template <int Q>
-__device__ __forceinline__ void split4(const f32x4& v, f16x8& hi, f16x8& lo) {
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const f32x2 x = f32x2{v[2 * k], v[2 * k + 1]};
-    const f16x2 hh = __builtin_convertvector(x, f16x2);
-    const f32x2 hf = __builtin_convertvector(hh, f32x2);
-    const f32x2 r = x - hf;
-    const f16x2 ll = __builtin_convertvector(r, f16x2);
-    hi[4 * Q + 2 * k] = hh.x;
-    hi[4 * Q + 2 * k + 1] = hh.y;
-    lo[4 * Q + 2 * k] = ll.x;
-    lo[4 * Q + 2 * k + 1] = ll.y;
-  }
+// v = hi + lo for 4 fp32 values as dwords of 2 fp16 each (h01 = hi of v.x, v.y; ...): hi by the
+// packed RNE conversion, lo = (f16)(v - (f32)hi) in one v_fma_mix per value (-1 * hi + v: the
+// difference is exact in fp32, Sterbenz), written straight into its half of the dword -- the bits of
+// conv_x3's x3_split8 in 1.5 instead of 3 VALU per value and no repacking moves.
+__device__ __forceinline__ void split_dw(const f32x4& v, unsigned& h01, unsigned& h23, unsigned& l01, unsigned& l23) {
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h01) : "v"(v.x), "v"(v.y));
+  asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(h23) : "v"(v.z), "v"(v.w));
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l01) : "v"(h01), "v"(v.x));
+  asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l01) : "v"(h01), "v"(v.y));
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l23) : "v"(h23), "v"(v.z));
+  asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l23) : "v"(h23), "v"(v.w));
 }
 
 // ABL (development build only, tools/convbench "w2" with ISLPOSE_W2_ABL): timing ablations --
@@ -168,16 +164,17 @@ __global__ void __launch_bounds__(512, 1) wino_f16(W2Args a) {
   // This wave's two GEMMs: xi0 = 4 r + 2 cp, xi1 = xi0 + 1 (one row r of V, a column pair).
   // V[r][c] = (d[ra][ca] + sc d[ra][cb]) + sr (d[rb][ca] + sc d[rb][cb]); B^T rows: d0 - d2,
   // d1 + d2, d2 - d1, d1 - d3.  The row combination t[col] = d[ra][col] + sr d[rb][col] is
-  // shared by the pair: columns {0, 1, 2} for c = 0, 1 (t0 - t2, t1 + t2), {1, 2, 3} for
-  // c = 2, 3 (t2 - t1, t1 - t3): 6 pixels per (tile, channel) for the two values.
+  // shared by the pair, over three column slots X, Y, Z: V(xi0) = tX - tY, V(xi1) = tY + sz tZ
+  // (cp 0: columns 0, 2, 1, sz = +1 -- d0 - d2, d2 + d1; cp 1: columns 2, 1, 3, sz = -1 --
+  // d2 - d1, d1 - d3): 6 pixels, 3 + 2 fma per channel for the two values, no selects.
   const int wr = w >> 1, cpr = w & 1;
   const int ra = wr == 0 ? 0 : wr == 2 ? 2 : 1, rb = wr == 3 ? 3 : wr == 2 ? 1 : 2;
-  const float sr = wr == 1 ? 1.f : -1.f;
-  // the three columns (cpr = 0: 0, 1, 2; cpr = 1: 1, 2, 3): unit offsets of (row, column)
-  const int cl = cpr;                                     // first column of the three
+  const float sr = wr == 1 ? 1.f : -1.f, sz = cpr ? -1.f : 1.f;
+  const f32x4 srv = f32x4{sr, sr, sr, sr}, szv = f32x4{sz, sz, sz, sz};
+  const int cX = cpr ? 2 : 0, cY = cpr ? 1 : 2, cZ = cpr ? 3 : 1;
   auto toff = [&](int row, int col) { return (row * 2 + (col & 1)) * RS + (col >> 1); };
-  const int to_a0 = toff(ra, cl), to_a1 = toff(ra, cl + 1), to_a2 = toff(ra, cl + 2);
-  const int to_b0 = toff(rb, cl), to_b1 = toff(rb, cl + 1), to_b2 = toff(rb, cl + 2);
+  const int to_aX = toff(ra, cX), to_aY = toff(ra, cY), to_aZ = toff(ra, cZ);
+  const int to_bX = toff(rb, cX), to_bY = toff(rb, cY), to_bZ = toff(rb, cZ);
   // per tile tile j the lane's unit base in a raw buffer (chunk half h, quad 0, row 2 typ, parity 0)
   int tb[2];
 #pragma unroll
@@ -233,7 +230,9 @@ __global__ void __launch_bounds__(512, 1) wino_f16(W2Args a) {
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[x][i][j][r] = 0.f;
-  float vmax = 0.f;   // max |V|: the split needs |V| < 65504 (range guard)
+  // Range: a V value with |V| >= 65520 splits to an infinite hi, which makes every output it feeds
+  // inf or NaN (a zero filter gives NaN too), so the epilogue's output check raises the range flag
+  // (the host then recomputes on the fp32 kernels); |V| in [65504, 65520) splits exactly.
 
   // per tile tile j: both GEMMs' B fragments (the transform) from ring slot sl, then 12 MFMAs
   auto compute = [&](const f16x8 (&A)[2][2][2], int sl) __attribute__((always_inline)) {
@@ -241,38 +240,37 @@ __global__ void __launch_bounds__(512, 1) wino_f16(W2Args a) {
     for (int j = 0; j < 2; ++j) {
       int b = tb[j] + sl * BUF;
       asm volatile("" : "+v"(b));   // the pixel addresses are formed per step (not held across it)
-      f16x8 Bh[2], Bl[2];
+      // B fragments as dwords (2 fp16 each): [xi][hi|lo] x 4 dwords, quad Q in dwords 2Q, 2Q + 1
+      unsigned Bd[2][2][4];
       if constexpr ((ABL & 2) != 0) {
-        Bh[0] = Bh[1] = Bl[0] = Bl[1] = f16x8{1, 1, 1, 1, 1, 1, 1, 1};
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int hl = 0; hl < 2; ++hl)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) Bd[x][hl][d] = 0x3c003c00u;
       } else {
         auto quad = [&](auto qc) __attribute__((always_inline)) {
           constexpr int Q = decltype(qc)::value;
-          const f32x4 a0 = smem[b + to_a0 + Q * QS], a1 = smem[b + to_a1 + Q * QS], a2 = smem[b + to_a2 + Q * QS];
-          const f32x4 b0 = smem[b + to_b0 + Q * QS], b1 = smem[b + to_b1 + Q * QS], b2 = smem[b + to_b2 + Q * QS];
-          f32x4 v0, v1;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float t0 = __builtin_fmaf(sr, b0[e], a0[e]);
-            const float t1 = __builtin_fmaf(sr, b1[e], a1[e]);
-            const float t2 = __builtin_fmaf(sr, b2[e], a2[e]);
-            // cpr 0: V(c=0) = t0 - t2, V(c=1) = t1 + t2; cpr 1: V(c=2) = t1 - t0 (cols 2, 1), V(c=3) = t0 - t2 (cols 1, 3)
-            if (cpr == 0) {
-              v0[e] = t0 - t2;
-              v1[e] = t1 + t2;
-            } else {
-              v0[e] = t1 - t0;
-              v1[e] = t0 - t2;
-            }
-          }
-          vmax = __builtin_fmaxf(vmax, __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(v0[0]), __builtin_fabsf(v0[1])),
-                                                       __builtin_fmaxf(__builtin_fabsf(v0[2]), __builtin_fabsf(v0[3]))));
-          vmax = __builtin_fmaxf(vmax, __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(v1[0]), __builtin_fabsf(v1[1])),
-                                                       __builtin_fmaxf(__builtin_fabsf(v1[2]), __builtin_fabsf(v1[3]))));
-          split4<Q>(v0, Bh[0], Bl[0]);
-          split4<Q>(v1, Bh[1], Bl[1]);
+          const f32x4 aX = smem[b + to_aX + Q * QS], aY = smem[b + to_aY + Q * QS], aZ = smem[b + to_aZ + Q * QS];
+          const f32x4 bX = smem[b + to_bX + Q * QS], bY = smem[b + to_bY + Q * QS], bZ = smem[b + to_bZ + Q * QS];
+          // (vector forms: each f32x4 op becomes two v_pk_*_f32 on the registers ds_read_b128 filled)
+          const f32x4 tX = __builtin_elementwise_fma(srv, bX, aX);
+          const f32x4 tY = __builtin_elementwise_fma(srv, bY, aY);
+          const f32x4 tZ = __builtin_elementwise_fma(srv, bZ, aZ);
+          const f32x4 v0 = tX - tY;
+          const f32x4 v1 = __builtin_elementwise_fma(szv, tZ, tY);
+          split_dw(v0, Bd[0][0][2 * Q], Bd[0][0][2 * Q + 1], Bd[0][1][2 * Q], Bd[0][1][2 * Q + 1]);
+          split_dw(v1, Bd[1][0][2 * Q], Bd[1][0][2 * Q + 1], Bd[1][1][2 * Q], Bd[1][1][2 * Q + 1]);
         };
         quad(std::integral_constant<int, 0>{});
         quad(std::integral_constant<int, 1>{});
+      }
+      f16x8 Bh[2], Bl[2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        Bh[x] = __builtin_bit_cast(f16x8, u32x4{Bd[x][0][0], Bd[x][0][1], Bd[x][0][2], Bd[x][0][3]});
+        Bl[x] = __builtin_bit_cast(f16x8, u32x4{Bd[x][1][0], Bd[x][1][1], Bd[x][1][2], Bd[x][1][3]});
       }
 #pragma unroll
       for (int x = 0; x < 2; ++x)
@@ -319,10 +317,18 @@ __global__ void __launch_bounds__(512, 1) wino_f16(W2Args a) {
     step(k, AS[0], AS[1]);
     if (k + 1 < a.pairs) step(k + 1, AS[1], AS[0]);
   }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // every filter register the asm loads wrote stays allocated until the loads have landed (the
+  // last step's loads are never used: without this their registers could be reused while in flight)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)"
+               : "+v"(AS[0][0][0][0]), "+v"(AS[0][0][0][1]), "+v"(AS[0][0][1][0]), "+v"(AS[0][0][1][1]),
+                 "+v"(AS[0][1][0][0]), "+v"(AS[0][1][0][1]), "+v"(AS[0][1][1][0]), "+v"(AS[0][1][1][1]),
+                 "+v"(AS[1][0][0][0]), "+v"(AS[1][0][0][1]), "+v"(AS[1][0][1][0]), "+v"(AS[1][0][1][1]),
+                 "+v"(AS[1][1][0][0]), "+v"(AS[1][1][0][1]), "+v"(AS[1][1][1][0]), "+v"(AS[1][1][1][1])
+               :
+               : "memory");
   __syncthreads();
 
-  bool bad = !(vmax < 65504.f);
+  bool bad = false;
   if constexpr ((ABL & 16) != 0) {
     // keep the accumulators live: one value per lane
     float sum = 0.f;

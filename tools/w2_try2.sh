@@ -9,7 +9,7 @@ if [ $rc -ne 0 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
 run() { echo "== $*" >> $O/abl.txt; timeout -k 10 120 "$@" >> $O/abl.txt 2>&1; }
 for shape in "3 128 128 46 82 32" "3 384 128 46 82 32" "3 256 256 92 164 32" "3 512 512 46 82 32"; do
   run tools/convbench $shape 10 x3,w2 2 || exit 1
-  for k in 16 3 1 2 4 8 31; do
+  for k in 16 2 1 3 31; do
     ISLPOSE_W2_ABL=$k run tools/convbench $shape 10 w2 1 || exit 1
   done
 done

@@ -230,6 +230,11 @@ struct isl_net {
     void* tab = nullptr;
     size_t tab_bytes = 0;
     std::vector<char> tab_host;   // what `tab` holds (upload_tab skips an identical table)
+    // pinned staging of the table upload (a pageable hipMemcpyAsync may block the host until
+    // the stream reaches it) and the event behind the copy out of it
+    void* tab_pin = nullptr;
+    size_t tab_pin_bytes = 0;
+    hipEvent_t tab_ev = nullptr;
     float* ks = nullptr;
     size_t ks_floats = 0;
     // split-K fold plan for the current batch size (plan_fold): per op, the offset of a
@@ -976,6 +981,11 @@ static void drop_arena(isl_net* net, std::map<long long, isl_net::Arena>::iterat
   // hipFree waits for queued work that may still use the arena
   (void)hipFree(it->second.base);
   if (it->second.tab) (void)hipFree(it->second.tab);
+  if (it->second.tab_ev) {
+    (void)hipEventSynchronize(it->second.tab_ev);
+    (void)hipEventDestroy(it->second.tab_ev);
+  }
+  if (it->second.tab_pin) (void)hipHostFree(it->second.tab_pin);
   if (it->second.ks) (void)hipFree(it->second.ks);
   if (it->second.fold_mem) (void)hipFree(it->second.fold_mem);
   if (it->second.fold_tab) (void)hipFree(it->second.fold_tab);
@@ -1065,9 +1075,17 @@ static bool x3_wino_enabled() {
 // 3x3 layers on chip-filling grids through the split-fp16 Winograd F(2x2, 3x3) kernel
 // (wino_f16.hip: 2.25x fewer MFMAs, fp32-accurate like conv_x3) where wino_f16_fits;
 // ISLPOSE_X3_W2=0: conv_x3 everywhere (A/B; read per launch)
-static bool w2_enabled() {
+// Default: layers with >= 256 input channels (32 chunks) -- measured faster than conv_x3 there
+// (46x82 c384->128 1.06-1.16x, 92x164 c256->256 1.04-1.12x, 46x82 c512->512 1.05-1.17x in
+// tools/convbench, profiles/r06/w2c/), slower on c128->128 (K = 128: 0.85-0.9x).
+// ISLPOSE_X3_W2=0 never, =1 every eligible launch (A/B, tests), default 2 = the K rule.
+static int w2_mode() {
   const char* e = getenv("ISLPOSE_X3_W2");
-  return !(e && e[0] == '0');
+  return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 2;
+}
+static bool w2_enabled(const ConvLaunch& c) {
+  const int m = w2_mode();
+  return m == 1 || (m == 2 && c.cin_chunks >= 32);
 }
 
 // ISLPOSE_RGB_CONV=0: conv1_1 on the generic split-fp16 kernel (A/B; read per launch)
@@ -1454,7 +1472,7 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
         fused = true;
       }
       // the Winograd kernel: plain 3x3 launches (no pool on either side, no fold, no K ranges)
-      if (!perm && w2_enabled() && c.d_ww && !L.vin && !L.hpool && far.fold_ws_off[k] < 0 &&
+      if (!perm && w2_enabled(L) && c.d_ww && !L.vin && !L.hpool && far.fold_ws_off[k] < 0 &&
           far.fold_tab_off[k] < 0 && x3_split_ranges(L, nullptr) <= 1) {
         ConvLaunch Lw = L;
         Lw.wx3 = c.d_ww;
@@ -1784,6 +1802,11 @@ int isl_net_destroy(isl_net* net) {
   drop_all_graphs(net);
   if (net->cap_stream) (void)hipStreamDestroy(net->cap_stream);
   for (auto& kv : net->plans) {
+    if (kv.second.tab_ev) {
+      (void)hipEventSynchronize(kv.second.tab_ev);
+      (void)hipEventDestroy(kv.second.tab_ev);
+    }
+    if (kv.second.tab_pin) (void)hipHostFree(kv.second.tab_pin);
     if (kv.second.tab) (void)hipFree(kv.second.tab);
     if (kv.second.ks) (void)hipFree(kv.second.ks);
     if (kv.second.fold_mem) (void)hipFree(kv.second.fold_mem);
@@ -1885,7 +1908,21 @@ static int upload_tab(isl_net* net, hipStream_t s) {
     HIP_OK(hipMalloc(&ar.tab, bytes));
     ar.tab_bytes = bytes;
   }
-  HIP_OK(hipMemcpyAsync(ar.tab, net->h_tab.data(), bytes, hipMemcpyHostToDevice, s));
+  // through a pinned staging buffer, so the call never waits for the stream (the hand scales'
+  // crop tables change every frame, and each scale's stream must not block the host enqueue of
+  // the next): the previous copy out of the staging buffer has long completed, normally
+  if (ar.tab_ev) HIP_OK(hipEventSynchronize(ar.tab_ev));
+  if (bytes > ar.tab_pin_bytes) {
+    if (ar.tab_pin) HIP_OK(hipHostFree(ar.tab_pin));
+    ar.tab_pin = nullptr;
+    ar.tab_pin_bytes = 0;
+    HIP_OK(hipHostMalloc(&ar.tab_pin, bytes, hipHostMallocDefault));
+    ar.tab_pin_bytes = bytes;
+  }
+  memcpy(ar.tab_pin, net->h_tab.data(), bytes);
+  HIP_OK(hipMemcpyAsync(ar.tab, ar.tab_pin, bytes, hipMemcpyHostToDevice, s));
+  if (!ar.tab_ev) HIP_OK(hipEventCreateWithFlags(&ar.tab_ev, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(ar.tab_ev, s));
   ar.tab_host = net->h_tab;
   net->d_tab = ar.tab;
   return ISL_OK;

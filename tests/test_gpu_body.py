@@ -462,12 +462,19 @@ def test_timed_config_forward_vs_oracle(net25, w25):
     var = {name: rt.decode_variant(v) for name, v in net25.op_variants()}
     stage3 = [k for k in var if k.startswith("Mconv") and k[5] in "12345"]
     assert len(stage3) == 90
+    # the first conv of blocks 2-5 of the 128-wide stages reads 384 channels: the split-fp16
+    # Winograd kernel (wino_f16, the default for >= 256 input channels); the rest the row union
+    w2 = [k for k in stage3 if var[k].get("wino2")]
+    assert sorted(w2) == sorted(k for k in stage3 if k[5] in "2345" and k.endswith("_0") and "stage0" not in k), w2
     for k in stage3:
-        assert var[k].get("union") and var[k]["bpx"] == 512, (k, var[k])
+        if k not in w2:
+            assert var[k].get("union") and var[k]["bpx"] == 512, (k, var[k])
+    for k in ("conv3_2", "conv3_3", "conv4_2", "conv4_3_CPM", "conv4_4_CPM"):
+        assert var[k].get("wino2"), (k, var[k])
     for k in ("conv3_1", "conv4_1"):
         assert var[k].get("vin"), (k, var[k])
     assert var["conv2_1"]["bpx"] == 512 and not var["conv2_1"].get("vin"), var["conv2_1"]   # pool1 in conv_c12
-    assert var["conv4_1"].get("union"), var["conv4_1"]
+    assert var["conv4_1"].get("union"), var["conv4_1"]   # (pooled input: not eligible for wino_f16)
     m6 = [k for k in var if k.startswith("Mconv6")]
     assert len(m6) == 6 and all(var[k].get("fused67") and var[k]["bco"] in (256, 512) for k in m6), m6
     assert all(var[k].get("fused_into_prev") for k in var if k.startswith("Mconv7"))

@@ -28,6 +28,13 @@ def w25():
     return synth.synth_weights(rt.ISL_BODY25)
 
 
+@pytest.fixture(autouse=True)
+def _w2_everywhere(monkeypatch):
+    """Every eligible launch on the Winograd kernel (the default takes layers with >= 256 input
+    channels only), so the parity checks cover the 128-channel stage layers too."""
+    monkeypatch.setenv("ISLPOSE_X3_W2", "1")
+
+
 @pytest.fixture(scope="module")
 def net25(w25):
     n = rt.Net(rt.ISL_BODY25)
@@ -82,7 +89,7 @@ def test_wino2_hand_736_vs_x3():
         out0 = net.forward(xt)
         torch.cuda.synchronize()
     finally:
-        del os.environ["ISLPOSE_X3_W2"]
+        os.environ["ISLPOSE_X3_W2"] = "1"
     assert _rel(out.cpu().numpy(), out0.cpu().numpy()) < 2e-5
     ref = cpu_ref.make_net_fn("hand", w)(x)
     assert _rel(out.cpu().numpy(), ref) < TOL
@@ -111,3 +118,16 @@ def test_wino2_deterministic_and_batch_position(net25):
     p1, h1 = net25.forward(xt[2:3].contiguous())
     torch.cuda.synchronize()
     assert torch.equal(p3[2:3], p1) and torch.equal(h3[2:3], h1)
+
+
+def test_wino2_default_rule(net25, monkeypatch):
+    """The default (ISLPOSE_X3_W2 unset): the Winograd kernel on the eligible layers with >= 256
+    input channels (the 384-channel stage inputs, conv3_2/3_3, conv4_2 .. conv4_4), conv_x3 on
+    the 128-channel stage layers, where it is faster."""
+    monkeypatch.delenv("ISLPOSE_X3_W2", raising=False)
+    xt = torch.from_numpy(_inputs(1, 368, 656, seed=5)).cuda()
+    net25.forward(xt)
+    torch.cuda.synchronize()
+    used = set(_w2_layers(net25))
+    assert {"conv3_2", "conv3_3", "conv4_2", "conv4_3_CPM", "conv4_4_CPM"} <= used, used
+    assert "Mconv2_stage1_L2_0" in used and "Mconv2_stage1_L2_1" not in used, used

@@ -1471,8 +1471,12 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
         L.hpool = 1;
         fused = true;
       }
-      // the Winograd kernel: plain 3x3 launches (no pool on either side, no fold, no K ranges)
-      if (!perm && w2_enabled(L) && c.d_ww && !L.vin && !L.hpool && far.fold_ws_off[k] < 0 &&
+      // the Winograd kernel: plain 3x3 launches -- no pool on either side (decided from the graph,
+      // not from whether the pool is fused, so the pool switches never change a conv's arithmetic),
+      // no fold, no K ranges
+      const bool pool_side = (k > 0 && net->ops[k - 1].type == 1 && net->ops[k - 1].out == op.in) ||
+                             (k + 1 < net->ops.size() && net->ops[k + 1].type == 1 && net->ops[k + 1].in == op.out);
+      if (!perm && !pool_side && w2_enabled(L) && c.d_ww && !L.vin && !L.hpool && far.fold_ws_off[k] < 0 &&
           far.fold_tab_off[k] < 0 && x3_split_ranges(L, nullptr) <= 1) {
         ConvLaunch Lw = L;
         Lw.wx3 = c.d_ww;

@@ -482,6 +482,27 @@ def frame_leg(args):
         return {"error": "%s: %s" % (type(e).__name__, e)}
 
 
+def conv_stage(kinds, runs):
+    """All split-fp16 conv launches (kinds 3 + 5): executed MFMA TF/s and frac, the direct-conv
+    equivalent (3 x 2*Cout*Cin*k*k*H*W) TF/s and frac, and each algorithm's share."""
+    ks = [k for k in kinds if k in (3, 5)]
+    if not ks:
+        return None
+    ms = sum(kinds[k]["ms"] for k in ks)
+    sec = ms * 1e-3
+    executed = sum(kinds[k]["mfma_flops"] for k in ks) / sec / 1e12
+    alg = sum(ALG_FACTOR[k] * kinds[k]["flops"] for k in ks) / sec / 1e12
+    deq = 3.0 * sum(kinds[k]["flops"] for k in ks) / sec / 1e12
+    return {"ms_per_step": round(ms / runs, 3), "launches_per_step": sum(kinds[k]["launches"] for k in ks) // runs,
+            "executed_mfma_tflops": round(executed, 2), "executed_frac": round(executed / PEAK_FP16_MFMA_TFLOPS, 4),
+            "algorithmic_mfma_tflops": round(alg, 2), "algorithmic_frac": round(alg / PEAK_FP16_MFMA_TFLOPS, 4),
+            "direct_equiv_tflops": round(deq, 2), "direct_equiv_frac": round(deq / PEAK_FP16_MFMA_TFLOPS, 4),
+            "basis": "executed = MFMA FLOPs the kernels ran (tile padding included); algorithmic = split-fp16 "
+                     "direct x3 / Winograd 3 x 16/36 of the direct count; direct_equiv = 3 x the direct-conv count "
+                     "for every layer (the rate the round-5 frac measured), all over the summed conv launch time",
+            "share_ms": {KIND[k]: round(kinds[k]["ms"] / runs, 3) for k in ks}}
+
+
 def roofline_of(ops):
     """Roofline fields of the dominant kernel class from per-op HIP-event timings (summed
     over lanes and recorded runs): achieved = the MFMA FLOPs its algorithm needs / summed
@@ -531,6 +552,10 @@ def roofline_of(ops):
             "algorithmic_gflop_per_launch": round(dk["flops"] / dk["launches"] / 1e9, 3),
             "all_convs_tflops": round(conv_flops / (conv_ms * 1e-3) / 1e12, 2),
             "ms_per_step_by_kind": {KIND[k]: round(v["ms"] / runs, 3) for k, v in kinds.items()},
+            # every conv of the step together (split-fp16 direct + Winograd): the MFMA work the
+            # matrix cores executed and the direct-conv-equivalent rate (3 x the direct count, the
+            # work the x3 direct form would need: comparable across rounds), side by side
+            "conv_stage": conv_stage(kinds, runs),
             # PMC (profiles/conv_traffic.json, from tools/profile_round.sh): MFMA pipe busy
             # fraction of the dominant kernel's wall cycles, and the DVFS clock it ran at; the
             # conv stage adds conv1_1's write-bound conv_x3_rgb

@@ -77,8 +77,8 @@ class BodyEstimator:
             # one stream per net size: two scales that pad to the same size share one arena,
             # preprocess table and split-K workspace, so they run in order on one stream
             streams = rt.size_streams(self, frames.device, [(g[1], g[2]) for g in sg])
+            rt.fork_streams(cur, streams)
             for st, (m, nh, nw, vh, vw) in zip(streams, sg):
-                st.wait_stream(cur)
                 with torch.cuda.stream(st):
                     gh, gw = self.net.preprocess(frames, m)
                     assert (gh, gw) == (nh, nw)
@@ -88,10 +88,10 @@ class BodyEstimator:
                 frames.record_stream(st)
                 paf.record_stream(cur)
                 heat.record_stream(cur)
-                cur.wait_stream(st)
                 geoms.append((nh, nw, vh, vw))
                 pafs.append(paf)
                 heats.append(heat)
+            rt.join_streams(cur, streams)
             return geoms, pafs, heats
         for (m, nh, nw, vh, vw) in scale_geometry(H, W, self.scale_search):
             gh, gw = self.net.preprocess(frames, m)

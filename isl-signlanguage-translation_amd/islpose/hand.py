@@ -39,8 +39,9 @@ class HandEstimator:
         cur = torch.cuda.current_stream(crops.device)
         # the scales side by side on their own streams, as run_crops (one per net size)
         sg = scale_geometry(h, w, self.scale_search)
-        for st, (m, nh, nw, vh, vw) in zip(rt.size_streams(self, crops.device, [(g[1], g[2]) for g in sg]), sg):
-            st.wait_stream(cur)
+        streams = rt.size_streams(self, crops.device, [(g[1], g[2]) for g in sg])
+        rt.fork_streams(cur, streams)
+        for st, (m, nh, nw, vh, vw) in zip(streams, sg):
             with torch.cuda.stream(st):
                 gh, gw = self.net.preprocess(crops, m)
                 assert (gh, gw) == (nh, nw)
@@ -48,9 +49,9 @@ class HandEstimator:
                 self.net.run(heat)
             crops.record_stream(st)
             heat.record_stream(cur)
-            cur.wait_stream(st)
             geoms.append((nh, nw, vh, vw))
             heats.append(heat)
+        rt.join_streams(cur, streams)
         return geoms, heats
 
     def post_maps(self, h, w, geoms, heats, out=None):
@@ -100,16 +101,17 @@ class HandEstimator:
         heats = []
         # one stream per net size (scales that pad to one size share its arena)
         keys = [rt.crop_net_size(crops[0][4], crops[0][3], s * BOXSIZE) for s in self.scale_search]
-        for st, s in zip(rt.size_streams(self, frames_t.device, keys), self.scale_search):
-            st.wait_stream(cur)
+        streams = rt.size_streams(self, frames_t.device, keys)
+        rt.fork_streams(cur, streams)
+        for st, s in zip(streams, self.scale_search):
             with torch.cuda.stream(st):
                 gh, gw = self.net.preprocess_crops(frames_t, crops, s * BOXSIZE)
                 heat = torch.empty((len(crops), 22, gh // 8, gw // 8), device=frames_t.device)
                 self.net.run(heat)
             frames_t.record_stream(st)
             heat.record_stream(cur)
-            cur.wait_stream(st)
             heats.append(heat)
+        rt.join_streams(cur, streams)
         return heats
 
     def launch_crops(self, frames_t, boxes):

@@ -166,6 +166,20 @@ def size_streams(owner, device, keys):
     return [ss[lane[k]] for k in keys]
 
 
+def fork_streams(cur, streams):
+    """Every distinct stream of `streams` waits for the work queued so far on `cur`.  All
+    forks come before any join: a stream forked after `cur` joined an earlier one would wait
+    for that one's whole chain, and the scales would run one after another."""
+    for st in dict.fromkeys(streams):
+        st.wait_stream(cur)
+
+
+def join_streams(cur, streams):
+    """`cur` waits for everything queued on `streams` (after fork_streams and the launches)."""
+    for st in dict.fromkeys(streams):
+        cur.wait_stream(st)
+
+
 def crop_net_size(crop_h: int, crop_w: int, scale_times_box: float):
     """Padded net size isl_net_preprocess_crops gives a crop (runtime.cpp: fx = fy =
     scale_times_box / h, cvRound, then padRightDownCorner to a multiple of 8)."""

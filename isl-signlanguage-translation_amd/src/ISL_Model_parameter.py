@@ -33,6 +33,11 @@ from islpose.hand import HandEstimator
 
 from . import util
 
+# the per-frame calls replay each net's conv chain as a HIP graph (bit-identical to the eager
+# launches, tests/test_gpu_wino2.py, test_gpu_body.py): one host call per run instead of
+# ~150 kernel launches, so the four hand scales' streams start together
+GRAPH_REPLAY = True
+
 
 def _as_numpy(img):
     return img.cpu().numpy() if isinstance(img, torch.Tensor) else np.asarray(img)
@@ -63,8 +68,10 @@ class ISLSignPos(object):
         bnet, hnet = self.pt_body.native(dev), self.pt_hand.native(dev)
         if self._body is None or self._body.net is not bnet:
             self._body = BodyEstimator(model_type="body25", device=dev, scale_search=(0.5,), net=bnet)
+            bnet.set_graph(GRAPH_REPLAY)
         if self._hand is None or self._hand.net is not hnet:
             self._hand = HandEstimator(device=dev, net=hnet)
+            hnet.set_graph(GRAPH_REPLAY)
         return self._body, self._hand
 
     def state_key(self):
@@ -91,15 +98,16 @@ class ISLSignPos(object):
         frame goes to the GPU once (_upload) and every hand crop of it runs as one batch per
         scale (HandEstimator.estimate_crops) instead of one 4-scale chain per crop in turn; the
         results equal the reference's per-crop handpos (tests/test_gpu_configs.py)."""
-        return self.call_batch(self._upload(oriImg))[0]
+        ests = self._estimators()   # (once per call: it checks both modules' parameters)
+        return self.call_batch(self._upload(oriImg, ests), ests)[0]
 
-    def _upload(self, img):
+    def _upload(self, img, ests=None):
         """One host frame [H, W, 3] -> cuda uint8 [1, H, W, 3] BGR.  The scripts pass
         frame[:, :, ::-1] of a decoded RGB frame (extract_features_mp.py:130): that view is
         uploaded as the contiguous RGB buffer it reverses and flipped on the GPU, not copied
         into a contiguous BGR array on the host first; the copy goes through a reused pinned
         buffer (one memcpy, then a DMA) instead of a pageable upload."""
-        body = self._estimators()[0]
+        body = (ests or self._estimators())[0]
         dev = torch.device("cuda:%d" % body.device)
         if isinstance(img, torch.Tensor) and img.is_cuda:
             # any dtype, as the host path's np.ascontiguousarray(..., dtype=np.uint8) (ADVICE r05)
@@ -115,6 +123,8 @@ class ISLSignPos(object):
             self._pinned_ev.synchronize()          # the previous upload has left the buffer
         host = buf[:src.size].view(src.shape)
         host.copy_(torch.from_numpy(src))          # (torch's copy runs on the host's threads)
+        # (in row bands, each band's DMA beside the next band's copy: measured level, 268 vs
+        # 287 us for 1 / 4 bands of a 1080p frame, tools/upload_micro.py -- the copy is 16 us)
         t = host.to(dev, non_blocking=True)
         self._pinned_ev = torch.cuda.Event()
         self._pinned_ev.record(torch.cuda.current_stream(dev))
@@ -122,11 +132,11 @@ class ISLSignPos(object):
 
     __call__ = call
 
-    def call_batch(self, frames):
+    def call_batch(self, frames, ests=None):
         """frames uint8 [n, H, W, 3] -> [(candidate, subset, all_hand_peaks)] * n, equal to
         call() per frame.  The body runs as one batch; every hand crop of the batch
         (util.handDetect boxes, in the reference's order) runs as one batch per scale."""
-        body, hand = self._estimators()
+        body, hand = ests or self._estimators()
         if isinstance(frames, torch.Tensor) and frames.is_cuda:
             # already resident (islpose.pipeline's prefetch: async H2D on a copy stream)
             if frames.dtype != torch.uint8 or frames.ndim != 4 or frames.shape[3] != 3:

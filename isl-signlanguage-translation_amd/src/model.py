@@ -55,6 +55,18 @@ class _NativeNet(nn.Module):
         object.__setattr__(self, "_native_net", None)
         object.__setattr__(self, "_native_key", None)
 
+    def _param_key(self):
+        """(storage, in-place version) of every parameter: load_state_dict / in-place edits bump
+        the versions, a replaced parameter changes its storage.  The modules holding parameters
+        are listed once (re-listed when a top-level child is replaced): walking
+        self.parameters() per call cost ~0.3 ms per net on every per-frame call."""
+        top = tuple(map(id, self._modules.values()))
+        cache = self.__dict__.get("_native_mods")
+        if cache is None or cache[0] != top:
+            cache = (top, [m for m in self.modules() if m._parameters])
+            object.__setattr__(self, "_native_mods", cache)
+        return tuple((p.data_ptr(), p._version) for m in cache[1] for p in m._parameters.values() if p is not None)
+
     def _freeze(self):
         for p in self.parameters():       # model.py:167-168, 298-299, 391-392
             p.requires_grad = False
@@ -69,7 +81,7 @@ class _NativeNet(nn.Module):
             net = rt.Net(self.KIND, device_index)
             object.__setattr__(self, "_native_net", net)
             object.__setattr__(self, "_native_key", None)
-        key = tuple((p.data_ptr(), p._version) for p in self.parameters())
+        key = self._param_key()
         if key != self._native_key:
             net.load_weights(self.caffe_weights())
             object.__setattr__(self, "_native_key", key)

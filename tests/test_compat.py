@@ -1,5 +1,6 @@
 """The drop-in `src` package (CPU side): module seam contract, util helpers vs the
 reference's golden outputs, and loud failure without a GPU."""
+import copy
 import json
 import os
 
@@ -97,3 +98,30 @@ def test_body_constructor_from_weight_file(tmp_path):
     assert isinstance(h.model, handpose_model)
     c = Body({k: torch.from_numpy(v) for k, v in synth.synth_weights(1).items()}, "xyz")   # falls back to COCO
     assert c.njoint == 19 and isinstance(c.model, bodypose_model)
+
+
+@pytest.mark.parametrize("cls", [bodypose_25_model, handpose_model])
+def test_param_key_sees_every_weight_change(cls):
+    """_NativeNet._param_key (what native() compares before re-uploading weights) equals the
+    (storage, version) walk over self.parameters() and changes on an in-place edit,
+    load_state_dict, a replaced parameter and a replaced top-level child."""
+    import torch
+    m = cls()
+    full = lambda: tuple((p.data_ptr(), p._version) for p in m.parameters())  # noqa: E731
+    k0 = m._param_key()
+    assert k0 == full()
+    with torch.no_grad():
+        next(m.parameters()).add_(1.0)
+    k1 = m._param_key()
+    assert k1 != k0 and k1 == full()
+    m.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
+    k2 = m._param_key()
+    assert k2 != k1 and k2 == full()
+    mod = next(x for x in m.modules() if isinstance(x, torch.nn.Conv2d))
+    mod.weight = torch.nn.Parameter(mod.weight.detach().clone())
+    k3 = m._param_key()
+    assert k3 != k2 and k3 == full()
+    name, child = next(iter(m.named_children()))
+    setattr(m, name, copy.deepcopy(child))
+    k4 = m._param_key()
+    assert k4 != k3 and k4 == full()

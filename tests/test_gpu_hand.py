@@ -126,6 +126,29 @@ def test_estimate_crops_matches_per_crop(hest):
     assert hest.estimate_crops(frames, []).shape == (0, 21, 2)
 
 
+def test_run_crops_concurrent_scales_bit_identical(hest):
+    """run_crops forks all four scale streams before joining any, so the scales' nets run
+    side by side on their own arenas; their maps equal each scale run alone on the current
+    stream with the device drained in between, bit for bit (repeated: stream interleavings
+    vary from call to call)."""
+    from islpose.hand import BOXSIZE
+    frames = torch.from_numpy(synth.synth_frames(2, 400, 600, seed=41)).cuda()
+    boxes = [(0, 40, 30, 200), (1, 300, 150, 200)]
+    crops = [(f, x, y, w, w) for f, x, y, w in boxes]
+    alone = []
+    for s in HAND_SCALES:
+        gh, gw = hest.net.preprocess_crops(frames, crops, s * BOXSIZE)
+        heat = torch.empty((len(crops), 22, gh // 8, gw // 8), device="cuda")
+        hest.net.run(heat)
+        torch.cuda.synchronize()
+        alone.append(heat.clone())
+    for _ in range(3):
+        got = hest.run_crops(frames, boxes)
+        torch.cuda.synchronize()
+        for s, a, g in zip(HAND_SCALES, alone, got):
+            assert torch.equal(a, g), s
+
+
 def test_hand_net_split_k(hest):
     """A single crop at the 184/736 px scales (grids far below the CU count) in the
     latency mode (adaptive split-K on top of the canonical ranges): deterministic and

@@ -72,6 +72,51 @@ def main():
     print("frames %d  ms/frame %.3f  crops/frame %.2f" % (T, tot / T * 1e3, crops / T))
     for k, v in ph.items():
         print("  %-12s %7.3f ms" % (k, v / T * 1e3))
+    hand_detail(isl, body, hand, rgb)
+
+
+def hand_detail(isl, body, hand, rgb):
+    """The hand phase of the frames with crops, split: the four scales' nets side by side
+    (run_crops), each scale alone, the post + D2H; eager and graph replay."""
+    from islpose.hand import BOXSIZE
+    jobs = []
+    for i in range(len(rgb)):
+        x = isl._upload(rgb[i][:, :, ::-1])
+        (c, s), = body.estimate(x)
+        boxes = [(0, bx, by, bw) for bx, by, bw, _l in util.handDetect(c, s, x[0])]
+        if boxes:
+            jobs.append((x, boxes))
+    if not jobs:
+        return
+    for graph in ("0", "1"):
+        os.environ["ISLPOSE_NET_GRAPH"] = graph
+        for x, boxes in jobs[:2]:                 # warm-up (graph capture)
+            for _ in range(2):
+                hand.post_crops(boxes, hand.run_crops(x, boxes))
+        torch.cuda.synchronize()
+        tn = tp = 0.0
+        ta = [0.0] * len(hand.scale_search)
+        for x, boxes in jobs:
+            t0 = time.perf_counter()
+            heats = hand.run_crops(x, boxes)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            hand.post_crops(boxes, heats)
+            t2 = time.perf_counter()
+            tn += t1 - t0
+            tp += t2 - t1
+            crops = [(f, bx, by, w, w) for (f, bx, by, w) in boxes]
+            for k, sc in enumerate(hand.scale_search):
+                t3 = time.perf_counter()
+                gh, gw = hand.net.preprocess_crops(x, crops, sc * BOXSIZE)
+                heat = torch.empty((len(crops), 22, gh // 8, gw // 8), device=x.device)
+                hand.net.run(heat)
+                torch.cuda.synchronize()
+                ta[k] += time.perf_counter() - t3
+        J = len(jobs)
+        print("hand frames %d (graph=%s): nets side by side %.3f ms, post+D2H %.3f ms; alone %s (sum %.3f)" % (
+            J, graph, tn / J * 1e3, tp / J * 1e3, " ".join("%.3f" % (v / J * 1e3) for v in ta), sum(ta) / J * 1e3))
+    os.environ.pop("ISLPOSE_NET_GRAPH")
 
 
 if __name__ == "__main__":

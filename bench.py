@@ -385,6 +385,11 @@ def gpu_main(args, rank, local, world):
                 "B": B, "steps": steps, "fps": B * world * steps / float(g[:, 0].max())}
 
     B, S = args.batch, args.streams
+    # one GPU: the per-frame leg first, on a fresh process -- after the batch-32 legs (their
+    # arenas, Mode R's 200 timed batch-1 steps) the same leg read 3-6 % lower (171-177 vs
+    # 182 frames/s alone, profiles/r06/fr6/); the headline's timed steps do not depend on it
+    frame_first = args.frame_count > 0 and world == 1
+    frame = frame_leg(args) if frame_first else None
     m = measure(args.scale, B, args.steps, args.warmup, S, not args.no_op_timing)
     e2e = e2e_rate(args, m["lanes"][0].est, m["frames_h"], m["maps"], dev) if args.e2e_steps > 0 else None
     # Mode R (the reference scripts' net size, scale_search=[0.5], body.py:41): the
@@ -461,7 +466,7 @@ def gpu_main(args, rank, local, world):
         "cpu_baseline": None,
     }
     if args.frame_count > 0:
-        out["frame"] = frame_leg(args)
+        out["frame"] = frame if frame_first else frame_leg(args)
     if not args.no_cpu and args.cpu_frames > 0 and world == 1:
         out["cpu_baseline"] = cpu_baseline(args, mult, nh, nw)
     print(json.dumps(out))

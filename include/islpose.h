@@ -153,6 +153,18 @@ int isl_net_set_split_k(isl_net* net, int mode);
  * eager.  Env ISLPOSE_NET_GRAPH=0|1 turns replay off / on process-wide. */
 int isl_net_set_graph(isl_net* net, int on);
 
+/* A non-blocking stream for one lane of a pyramid's scales (not in the reference: its scales
+ * run one after another on torch's current stream, body.py:47-77 / hand.py:31-50), created
+ * with a priority class: -1 the device's greatest priority, 0 the middle of its range, +1 its
+ * least.  HIP gives a process a few hardware queues per priority (GPU_MAX_HW_QUEUES, 4 by
+ * default) and maps further streams onto them, so two scales on two streams of one priority
+ * may still run one after the other; lanes of different priorities never share a queue, and
+ * the command processor dispatches the high-priority lane (the largest scale, the critical
+ * path) first.  *stream receives a hipStream_t; isl_lane_stream_destroy waits for its work
+ * and frees it. */
+int isl_lane_stream_create(int device, int priority_class, void** stream);
+int isl_lane_stream_destroy(void* stream);
+
 /* Range guard of ISL_ALGO_X3: waits for the device, returns ISL_E_RANGE if any
  * conv output since the last clear left the fp16 split range (the results of
  * those runs are then not fp32-accurate and must be recomputed with

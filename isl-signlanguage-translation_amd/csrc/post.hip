@@ -2412,26 +2412,49 @@ __global__ void __launch_bounds__(256) cc_find_kernel(int h, int w, int rows, in
   }
 }
 
+// Per-block table of component sums (root -> partial sum) in LDS: a thread's run of equal
+// roots is flushed into the table, and the table into the roots' global sums once per block.
+// Flushing runs straight to global memory (round 5) made the random-weight hand maps -- large
+// components interleaved along a thread's 256-pixel stride -- thousands of fp64 atomics on
+// the same few addresses per plane: 625 us of the 1.7 ms post of a 1080 px crop
+// (profiles/r06/fr6/post_trace).  The sums only pick the candidate components (within a
+// relative 1e-9 of the largest, cc_cand_kernel); the winners' exact numpy sums come from
+// cc_scatter / cc_bufsum, so the order of these additions does not reach a result.
+constexpr int CC_HASH = 1024;   // table slots per block (4096 pixels per chunk at most)
+constexpr int CC_PROBE = 8;     // linear probes before a run goes straight to its root
 __global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ planes, int h, int w, int rows,
                                                      int chunks, const int* __restrict__ parent_all,
                                                      double* __restrict__ vals_all, CcStats* __restrict__ stats) {
-  __shared__ int s_cnt, s_root[4];
-  __shared__ double s_sum[4];
+  __shared__ int s_key[CC_HASH];
+  __shared__ double s_val[CC_HASH];
+  __shared__ int s_cnt;
   const int plane = blockIdx.x / chunks, c = blockIdx.x % chunks;
   const int P = h * w, p0 = c * rows * w, p1 = min(P, p0 + rows * w);
   const int* parent = parent_all + (size_t)plane * P;
   const double* map = planes + (size_t)plane * P;
   double* vals = vals_all + (size_t)plane * P;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < CC_HASH; i += 256) {
+    s_key[i] = -1;
+    s_val[i] = 0.0;
+  }
   if (threadIdx.x == 0) s_cnt = 0;
   __syncthreads();
-  // runs of equal roots in registers (flushed on a root change); the last run of every
-  // thread is combined across the wave, then across the block, when the roots agree.
+  auto flush = [&](int r, double a) {
+    const unsigned hsh = ((unsigned)r * 2654435761u) >> 22;   // 10 bits (CC_HASH)
+#pragma unroll 1
+    for (int q = 0; q < CC_PROBE; ++q) {
+      const int slot = (int)((hsh + q) & (CC_HASH - 1));
+      const int old = atomicCAS(&s_key[slot], -1, r);
+      if (old == -1 || old == r) {
+        atomicAdd(&s_val[slot], a);
+        return;
+      }
+    }
+    atomicAdd(&vals[r], a);   // a crowded table: this run goes to its root directly
+  };
   // Block-strided pixels: every load is one coalesced row segment (a contiguous run per
-  // thread made each load touch 64 cache lines)
-  // a chunk is <= CC_CHUNK = 16 x 256 pixels: every parent load of the thread, then every
-  // value load, in flight together (one exposed latency each, not two per pixel)
-  // (one row of a plane wider than CC_CHUNK takes several rounds)
+  // thread made each load touch 64 cache lines); a chunk is <= CC_CHUNK = 16 x 256 pixels:
+  // every parent load of the thread, then every value load, in flight together
   constexpr int PER = CC_CHUNK / 256;
   int cnt = 0, cur = -1;
   double acc = 0.0;
@@ -2450,39 +2473,19 @@ __global__ void __launch_bounds__(256) cc_sum_kernel(const double* __restrict__ 
       if (r[k] < 0) continue;
       ++cnt;
       if (r[k] != cur) {
-        if (cur >= 0) atomicAdd(&vals[cur], acc);
+        if (cur >= 0) flush(cur, acc);
         cur = r[k];
         acc = 0.0;
       }
       acc += v[k];
     }
   }
-  // lanes that met no foreground pixel (cur < 0, acc 0) do not break the agreement:
-  // otherwise a plane that is one giant component with background lanes would flush
-  // every lane's sum into the same root with its own fp64 atomic
-  const unsigned long long act = __ballot(cur >= 0);
-  const int r0 = act ? __shfl(cur, __builtin_ctzll(act), 64) : -1;
-  const bool wave_same = __all(cur < 0 || cur == r0);
-  if (wave_same) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (lane == 0) { s_root[wave] = r0; s_sum[wave] = acc; }   // r0 = -1: nothing to add
-  } else {
-    if (cur >= 0) atomicAdd(&vals[cur], acc);
-    if (lane == 0) s_root[wave] = -2;                       // flushed already
-  }
-  atomicAdd(&s_cnt, cnt);
+  if (cur >= 0) flush(cur, acc);
+  if (cnt) atomicAdd(&s_cnt, cnt);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < 4; ++k) {
-      const int r = s_root[k];
-      if (r < 0) continue;
-      double sum = s_sum[k];
-      while (k + 1 < 4 && s_root[k + 1] == r) sum += s_sum[++k];
-      atomicAdd(&vals[r], sum);
-    }
-    if (s_cnt) atomicAdd(&stats[plane].count, s_cnt);
-  }
+  for (int i = threadIdx.x; i < CC_HASH; i += 256)
+    if (s_key[i] >= 0) atomicAdd(&vals[s_key[i]], s_val[i]);
+  if (threadIdx.x == 0 && s_cnt) atomicAdd(&stats[plane].count, s_cnt);
 }
 
 __global__ void __launch_bounds__(256) cc_stats_kernel(int h, int w, int rows, int chunks,

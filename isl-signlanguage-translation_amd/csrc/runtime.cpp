@@ -2050,6 +2050,34 @@ int isl_net_set_algo(isl_net* net, int algo) {
 
 int isl_net_get_algo(const isl_net* net) { return net ? net->algo : fail(ISL_E_ARG, "net is NULL"); }
 
+int isl_lane_stream_create(int device, int priority_class, void** stream) {
+  if (!stream) return fail(ISL_E_ARG, "stream is NULL");
+  if (priority_class < -1 || priority_class > 1) return fail(ISL_E_ARG, "priority class must be -1, 0 or 1");
+  *stream = nullptr;
+  int cur = 0;
+  HIP_OK(hipGetDevice(&cur));
+  if (device != cur) HIP_OK(hipSetDevice(device));
+  int least = 0, greatest = 0;
+  hipError_t c = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  hipStream_t s = nullptr;
+  if (c == hipSuccess) {
+    // lower numbers are greater priorities: greatest <= mid <= least
+    const int prio = priority_class < 0 ? greatest : priority_class > 0 ? least : greatest + (least - greatest + 1) / 2;
+    c = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio);
+  }
+  if (device != cur) (void)hipSetDevice(cur);
+  if (c != hipSuccess) return fail(ISL_E_HIP, std::string("hipStreamCreateWithPriority: ") + hipGetErrorString(c));
+  *stream = (void*)s;
+  return ISL_OK;
+}
+
+int isl_lane_stream_destroy(void* stream) {
+  if (!stream) return ISL_OK;
+  HIP_OK(hipStreamSynchronize((hipStream_t)stream));
+  HIP_OK(hipStreamDestroy((hipStream_t)stream));
+  return ISL_OK;
+}
+
 int isl_net_set_graph(isl_net* net, int on) {
   if (!net) return fail(ISL_E_ARG, "net is NULL");
   if (on < 0 || on > 1) return fail(ISL_E_ARG, "graph mode must be 0 or 1");

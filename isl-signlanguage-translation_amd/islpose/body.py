@@ -70,15 +70,16 @@ class BodyEstimator:
         geoms, pafs, heats = [], [], []
         multi = len(self.scale_search) > 1 or keep_maps
         if len(self.scale_search) > 1:
-            # pyramid: the scales side by side on their own streams (per-size arenas), as
-            # HandEstimator.run_crops
+            # pyramid: the scales side by side on the lanes of rt.lane_plan (per-size arenas),
+            # as HandEstimator.run_crops; two scales that pad to the same size share one arena,
+            # preprocess table and split-K workspace, so they run in order on one lane
             cur = torch.cuda.current_stream(frames.device)
             sg = scale_geometry(H, W, self.scale_search)
-            # one stream per net size: two scales that pad to the same size share one arena,
-            # preprocess table and split-K workspace, so they run in order on one stream
-            streams = rt.size_streams(self, frames.device, [(g[1], g[2]) for g in sg])
+            streams, order = rt.lane_plan(self, frames.device, [(g[1], g[2]) for g in sg])
             rt.fork_streams(cur, streams)
-            for st, (m, nh, nw, vh, vw) in zip(streams, sg):
+            pafs, heats = [None] * len(sg), [None] * len(sg)
+            for i in order:
+                st, (m, nh, nw, vh, vw) = streams[i], sg[i]
                 with torch.cuda.stream(st):
                     gh, gw = self.net.preprocess(frames, m)
                     assert (gh, gw) == (nh, nw)
@@ -88,9 +89,8 @@ class BodyEstimator:
                 frames.record_stream(st)
                 paf.record_stream(cur)
                 heat.record_stream(cur)
-                geoms.append((nh, nw, vh, vw))
-                pafs.append(paf)
-                heats.append(heat)
+                pafs[i], heats[i] = paf, heat
+            geoms = [(nh, nw, vh, vw) for (m, nh, nw, vh, vw) in sg]
             rt.join_streams(cur, streams)
             return geoms, pafs, heats
         for (m, nh, nw, vh, vw) in scale_geometry(H, W, self.scale_search):

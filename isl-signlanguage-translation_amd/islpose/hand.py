@@ -35,13 +35,14 @@ class HandEstimator:
     def run_scales(self, crops):
         import torch
         n, h, w, _ = crops.shape
-        geoms, heats = [], []
         cur = torch.cuda.current_stream(crops.device)
-        # the scales side by side on their own streams, as run_crops (one per net size)
+        # the scales side by side on the lanes of rt.lane_plan, as run_crops
         sg = scale_geometry(h, w, self.scale_search)
-        streams = rt.size_streams(self, crops.device, [(g[1], g[2]) for g in sg])
+        streams, order = rt.lane_plan(self, crops.device, [(g[1], g[2]) for g in sg])
         rt.fork_streams(cur, streams)
-        for st, (m, nh, nw, vh, vw) in zip(streams, sg):
+        heats = [None] * len(sg)
+        for i in order:
+            st, (m, nh, nw, vh, vw) = streams[i], sg[i]
             with torch.cuda.stream(st):
                 gh, gw = self.net.preprocess(crops, m)
                 assert (gh, gw) == (nh, nw)
@@ -49,9 +50,9 @@ class HandEstimator:
                 self.net.run(heat)
             crops.record_stream(st)
             heat.record_stream(cur)
-            geoms.append((nh, nw, vh, vw))
-            heats.append(heat)
+            heats[i] = heat
         rt.join_streams(cur, streams)
+        geoms = [(nh, nw, vh, vw) for (m, nh, nw, vh, vw) in sg]
         return geoms, heats
 
     def post_maps(self, h, w, geoms, heats, out=None):
@@ -92,25 +93,27 @@ class HandEstimator:
 
     def run_crops(self, frames_t, boxes):
         """The hand net over all crops, one batch per scale -> low-res heat [n,22,h8,w8] per
-        scale.  The scales run side by side, each on its own stream forked from the current
-        one and joined back (every scale has its own arena, table and split-K workspace in
-        the net): the small scales' grids fill the CUs the large ones leave idle."""
+        scale.  The scales run side by side on the streams of rt.lane_plan (three lanes, the
+        largest scales first), forked from the current stream and joined back (every scale
+        has its own arena, table and split-K workspace in the net): the small scales' grids
+        fill the CUs the large ones leave idle."""
         import torch
         crops = [(f, x, y, w, w) for (f, x, y, w) in boxes]
         cur = torch.cuda.current_stream(frames_t.device)
-        heats = []
-        # one stream per net size (scales that pad to one size share its arena)
+        # one lane per net size at most (scales that pad to one size share its arena)
         keys = [rt.crop_net_size(crops[0][4], crops[0][3], s * BOXSIZE) for s in self.scale_search]
-        streams = rt.size_streams(self, frames_t.device, keys)
+        streams, order = rt.lane_plan(self, frames_t.device, keys)
         rt.fork_streams(cur, streams)
-        for st, s in zip(streams, self.scale_search):
+        heats = [None] * len(keys)
+        for i in order:
+            st, s = streams[i], self.scale_search[i]
             with torch.cuda.stream(st):
                 gh, gw = self.net.preprocess_crops(frames_t, crops, s * BOXSIZE)
                 heat = torch.empty((len(crops), 22, gh // 8, gw // 8), device=frames_t.device)
                 self.net.run(heat)
             frames_t.record_stream(st)
             heat.record_stream(cur)
-            heats.append(heat)
+            heats[i] = heat
         rt.join_streams(cur, streams)
         return heats
 

@@ -26,7 +26,7 @@ EXPORTS = ["isl_abi_version", "isl_last_error", "isl_net_create", "isl_net_destr
            "isl_net_set_algo", "isl_net_get_algo", "isl_net_check", "isl_net_preprocess_crops",
            "isl_sign_param_count", "isl_sign_classify", "isl_net_set_split_k", "isl_net_arena_info",
            "isl_debug_np_sum", "isl_hand_post_crops", "isl_net_check_async", "isl_net_range_info",
-           "isl_net_op_info", "isl_net_set_graph"]
+           "isl_net_op_info", "isl_net_set_graph", "isl_lane_stream_create", "isl_lane_stream_destroy"]
 
 
 class IslCaps(ctypes.Structure):
@@ -94,6 +94,8 @@ def lib():
     L.isl_sign_param_count.argtypes = [i32, i32, ctypes.POINTER(i64)]
     L.isl_net_set_split_k.argtypes = [vp, i32]
     L.isl_net_set_graph.argtypes = [vp, i32]
+    L.isl_lane_stream_create.argtypes = [i32, i32, ctypes.POINTER(vp)]
+    L.isl_lane_stream_destroy.argtypes = [vp]
     L.isl_net_arena_info.argtypes = [vp, ctypes.POINTER(i64), ctypes.POINTER(i32)]
     L.isl_sign_classify.argtypes = [vp, i32, i32, i32, vp, i32, vp, vp]
     L.isl_debug_np_sum.argtypes = [vp, i64, vp, vp]
@@ -145,25 +147,65 @@ def flag_slot(owner, ring: int = 4):
     return f
 
 
+_LANES = {}   # device index -> [torch.cuda.ExternalStream], lane k of every estimator
+
+
+def lane_priorities(k):
+    """Priority class of each of k lanes (isl_lane_stream_create): lane 0 (the largest scale,
+    the critical path) high, lane 1 low, the rest normal -- three classes, three queue pools.
+    ISLPOSE_LANE_PRIO=0: every lane normal (A/B)."""
+    if os.environ.get("ISLPOSE_LANE_PRIO", "1") == "0":
+        return [0] * k
+    return [(-1, 1)[j] if j < 2 else 0 for j in range(k)]
+
+
 def scale_streams(owner, device, k):
-    """k HIP streams kept on `owner` (an estimator) for its pyramid scales."""
+    """k non-blocking streams for a pyramid's scales (isl_lane_stream_create with the classes
+    of lane_priorities).  One pool per device, shared by every estimator (work on one stream
+    stays in order) and never destroyed: torch's allocator may still hold events on a stream
+    that a tensor was recorded on.  `owner` is unused (kept for the callers' signature)."""
     import torch
-    ss = getattr(owner, "_scale_streams", None)
-    if ss is None or len(ss) < k:
-        ss = owner._scale_streams = [torch.cuda.Stream(device) for _ in range(k)]
-    return ss[:k]
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    prios = lane_priorities(k)
+    key = (idx, tuple(prios[:3]))
+    pool = _LANES.setdefault(key, [])
+    while len(pool) < k:
+        h = ctypes.c_void_p()
+        check(lib().isl_lane_stream_create(idx, prios[len(pool)], ctypes.byref(h)), "isl_lane_stream_create")
+        pool.append(torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx)))
+    return pool[:k]
 
 
-def size_streams(owner, device, keys):
-    """One stream per distinct key (a net input size) from owner's scale streams, in the
-    order of `keys`: runs that pad to the same net size share the net's arena, preprocess
-    table and split-K workspace for that size, so they must run in order on one stream;
-    runs of different sizes may overlap."""
-    lane = {}
-    for k in keys:
-        lane.setdefault(k, len(lane))
-    ss = scale_streams(owner, device, len(lane))
-    return [ss[lane[k]] for k in keys]
+SCALE_LANES = 4   # streams a pyramid's scales share (lane_plan)
+
+
+def lane_plan(owner, device, keys, lanes=None):
+    """Streams for a pyramid's scales (keys: their net sizes) and the order to enqueue them:
+    the distinct sizes go largest first onto the least loaded of SCALE_LANES streams (load =
+    net area), and the scales are enqueued largest first.  One stream per scale ran the two
+    largest hand scales one after the other (a process has 4 hardware queues, the current
+    stream holds one, so the fourth scale stream shared one with the third): 6.70 ms for one
+    crop's four scales; [736] [552] [368 -> 184] on three lanes: 5.48 ms
+    (tools/hand_conc_events.py, profiles/r06/fr6/lanes.txt).  Scales of one size share a
+    lane, in their order (they share that size's arena)."""
+    lane, order, n = lane_assign(keys, SCALE_LANES if lanes is None else lanes)
+    ss = scale_streams(owner, device, n)
+    return [ss[j] for j in lane], order
+
+
+def lane_assign(keys, lanes):
+    """lane_plan without the streams: (lane index per key, enqueue order, lanes used)."""
+    distinct = list(dict.fromkeys(keys))
+    area = {k: k[0] * k[1] for k in distinct}
+    n = max(1, min(lanes, len(distinct)))
+    load, lane = [0] * n, {}
+    for k in sorted(distinct, key=lambda k: -area[k]):
+        j = min(range(n), key=lambda i: load[i])
+        lane[k] = j
+        load[j] += area[k]
+    order = sorted(range(len(keys)), key=lambda i: (-area[keys[i]], i))
+    return [lane[k] for k in keys], order, n
 
 
 def fork_streams(cur, streams):

@@ -77,3 +77,18 @@ def test_new_entry_points_reject_bad_arguments():
     assert L.isl_net_check_async(body.h, None, None) == rt.ISL_E_ARG
     assert L.isl_debug_np_sum(None, 8, vp(16), None) == rt.ISL_E_ARG
     assert L.isl_debug_np_sum(vp(16), 0, vp(16), None) == rt.ISL_E_ARG
+
+
+def test_lane_assign_hand_and_pyramid_scales():
+    """rt.lane_assign (the streams of a pyramid's scales): the hand's four crop scales
+    (184/368/552/736 px) -> [736] [552] [368 then 184] on three lanes, largest enqueued
+    first; colliding sizes share a lane in their order; fewer sizes than lanes use fewer."""
+    keys = [(184, 184), (368, 368), (552, 552), (736, 736)]
+    lane, order, n = rt.lane_assign(keys, 3)
+    assert n == 3 and order == [3, 2, 1, 0]
+    assert lane[3] != lane[2] and lane[1] == lane[0] and len({lane[3], lane[2], lane[1]}) == 3
+    body = [(192, 336), (192, 336), (368, 656)]      # two scales padding to one size
+    lane, order, n = rt.lane_assign(body, 3)
+    assert n == 2 and lane[0] == lane[1] != lane[2] and order == [2, 0, 1]
+    lane, order, n = rt.lane_assign(keys, 1)
+    assert n == 1 and lane == [0, 0, 0, 0]

@@ -2095,12 +2095,15 @@ bool x3_wide1(const ConvLaunch& c) {
 // weight slab is 56 KiB).  The 256-pixel block does twice the work for ~1.72x the
 // time of a 128-pixel block (half the weight bytes per MFMA), so the choice is per
 // launch, by grid quantisation: rounds of one block per CU, a 256-pixel block costing
-// X3_WIDE7_COST 128-pixel blocks (measured over 92^2 / 69^2 / 46x82 grids at batch
-// 13-64, tools/archive/gpu_wide7.sh).  Both pack the weights for 128-channel tiles.
-constexpr double X3_WIDE7_COST = 1.74;
-// a round of 384-pixel blocks (12 waves, one input buffer): 2.58 rounds of 128 pixels,
-// from the hand's 92^2 layers (tools/archive/gpu_w384.sh, profiles/r02/w384/)
-constexpr double X3_W384_COST = 2.58;
+// X3_WIDE7_COST 128-pixel blocks.  Both pack the weights for 128-channel tiles.
+// Round 6 re-measured the three forms on the hand's batch-32 grids of C3 (op tables,
+// profiles/r06/w7ab/): 69^2 x 32 ran 11.93 / 10.89 / 11.36 ms over its twenty 7x7 stage
+// layers on 128 / 256 / 384 pixels (5 / 3 / 2 rounds), i.e. 1.52 and 2.38 128-pixel rounds
+// per round; with the round-2 costs (1.74, 2.58; tools/archive/gpu_wide7.sh, gpu_w384.sh)
+// the estimate kept 69^2 on 128 pixels.  92^2 (384) and 46^2 (384) choose as before.
+constexpr double X3_WIDE7_COST = 1.52;
+// a round of 384-pixel blocks (12 waves, one input buffer)
+constexpr double X3_W384_COST = 2.38;
 
 static int x3_wide7_mode() {   // ISLPOSE_X3_WIDE7: 0 never, 1 always (A/B), default by the estimate
   static const int m = getenv("ISLPOSE_X3_WIDE7") ? atoi(getenv("ISLPOSE_X3_WIDE7")) : 2;

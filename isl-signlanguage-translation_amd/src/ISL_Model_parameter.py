@@ -22,6 +22,7 @@ Out of scope: the ffmpeg ``Writer`` -- constructing it raises.
 from __future__ import annotations
 
 import collections
+import os
 
 import numpy as np
 import torch
@@ -35,8 +36,10 @@ from . import util
 
 # the per-frame calls replay each net's conv chain as a HIP graph (bit-identical to the eager
 # launches, tests/test_gpu_wino2.py, test_gpu_body.py): one host call per run instead of
-# ~150 kernel launches, so the four hand scales' streams start together
-GRAPH_REPLAY = True
+# ~50-150 kernel launches, so the four hand scales' streams start together.  (body, hand);
+# ISLPOSE_FRAME_GRAPH="10" etc. overrides (A/B)
+_fg = os.environ.get("ISLPOSE_FRAME_GRAPH", "11")
+GRAPH_REPLAY = (_fg[:1] == "1", _fg[1:2] == "1")
 
 
 def _as_numpy(img):
@@ -68,10 +71,10 @@ class ISLSignPos(object):
         bnet, hnet = self.pt_body.native(dev), self.pt_hand.native(dev)
         if self._body is None or self._body.net is not bnet:
             self._body = BodyEstimator(model_type="body25", device=dev, scale_search=(0.5,), net=bnet)
-            bnet.set_graph(GRAPH_REPLAY)
+            bnet.set_graph(GRAPH_REPLAY[0])
         if self._hand is None or self._hand.net is not hnet:
             self._hand = HandEstimator(device=dev, net=hnet)
-            hnet.set_graph(GRAPH_REPLAY)
+            hnet.set_graph(GRAPH_REPLAY[1])
         return self._body, self._hand
 
     def state_key(self):

@@ -218,7 +218,7 @@ def _x3_7x7_bpx(n, side):
     """conv_x3.hip x3_7x7_bpx for the hand's 7x7 stage layers (128 outputs, input ring 3) on
     a side x side level-3 grid at batch n: canonical K ranges (<= 1024 pixels) keep 128-pixel
     tiles, else the tile with the fewest rounds of one block per CU, a round of 256- / 384-
-    pixel blocks costing 1.74 / 2.58 rounds of 128 (ties keep the smaller tile)."""
+    pixel blocks costing 1.52 / 2.38 rounds of 128 (ties keep the smaller tile)."""
     if side * side <= 1024:
         return 128
 
@@ -228,7 +228,7 @@ def _x3_7x7_bpx(n, side):
                 return t
         return 1
     best, best_t = 128, None
-    for bpx, cost in ((128, 1.0), (256, 1.74), (384, 2.58)):
+    for bpx, cost in ((128, 1.0), (256, 1.52), (384, 2.38)):
         blocks = n * -(-side * side // tile_pixels(bpx))
         tt = -(-blocks // 256) * cost
         if best_t is None or tt < best_t:

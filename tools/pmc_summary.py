@@ -101,7 +101,7 @@ def mfma_busy(sq_dir, stats_csv, sq_out, clock_ghz=None):
         k = n.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("isl::", "").split("<")[0]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r.get("Dispatch_Id", ""))
-        if "conv_x3" in n:   # the whole conv stage: conv_x3_f16 + conv_x3_c12 (or conv_x3_rgb)
+        if "conv_x3" in n or "wino_f16" in n:   # the whole conv stage: conv_x3_f16 + conv_x3_c12 + wino_f16
             acc["conv_stage"][r["Counter_Name"]] += float(r["Counter_Value"])
             disp["conv_stage"].add(r.get("Dispatch_Id", ""))
     json.dump({"note": "raw SQ/GRBM counter sums per kernel class over the profiled bench run",
@@ -113,10 +113,13 @@ def mfma_busy(sq_dir, stats_csv, sq_out, clock_ghz=None):
     wall_ns = sum(float(r["TotalDurationNs"]) for r in stats if "conv_x3_f16" in r["Name"])
     active = x["GRBM_GUI_ACTIVE"] / 8
     cs = acc["conv_stage"]
-    stage_wall = sum(float(r["TotalDurationNs"]) for r in stats if "conv_x3" in r["Name"])
+    stage_wall = sum(float(r["TotalDurationNs"]) for r in stats if "conv_x3" in r["Name"] or "wino_f16" in r["Name"])
     extra = {"conv_stage_mfma_busy_frac": round(cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (cs["GRBM_GUI_ACTIVE"] / 8), 4),
              "conv_stage_note": "all conv kernels of the net (conv_x3_f16 + the conv1_1->conv1_2 pair's conv_x3_c12 (or conv_x3_rgb when unfused)"
-                                "): MFMA busy / GRBM cycles, as x3_mfma_busy_frac"}
+                                " + the Winograd wino_f16): MFMA busy / GRBM cycles, as x3_mfma_busy_frac"}
+    wf = acc.get("wino_f16")
+    if wf and wf.get("GRBM_GUI_ACTIVE"):
+        extra["wino_f16_mfma_busy_frac"] = round(wf["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (wf["GRBM_GUI_ACTIVE"] / 8), 4)
     if clock_ghz:
         extra["conv_stage_mfma_busy_frac_at_stamp_clock"] = round(
             cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (stage_wall * clock_ghz), 4)

@@ -93,6 +93,8 @@ def parse(argv=None):
                    help="the unchanged scripts' per-frame path (ISLSignPos.call on sequential 1080x1920 frames, "
                         "extract_features_mp.py:125-130) timed over this many frames after the headline, reported "
                         "as the 'frame' sub-object (rank 0; 0 = skip)")
+    p.add_argument("--frame-repeat", type=int, default=4,
+                   help="frame leg: timed passes over the --frame-count frames (one pass read +-4 %% run to run)")
     p.add_argument("--no-mode-r", dest="mode_r", action="store_false",
                    help="skip the Mode R sub-measurement (net 184x328 at batch 32 and batch 1)")
     p.add_argument("--pg-timeout", type=float, default=120.0,
@@ -480,7 +482,7 @@ def frame_leg(args):
     invocation after the headline (rank 0)."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import bench_configs
-    ns = argparse.Namespace(frame_count=args.frame_count)
+    ns = argparse.Namespace(frame_count=args.frame_count, frame_repeat=args.frame_repeat)
     try:
         return bench_configs.frame(ns)
     except Exception as e:   # never lose the headline line to the sub-measurement

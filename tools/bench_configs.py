@@ -203,11 +203,15 @@ def frame(args):
         isl.call(rgb[i][:, :, ::-1])
     torch.cuda.synchronize()
     crops, widths = 0, []
+    # the T frames REPEAT times over (a pass is ~0.35 s: one pass read +-4 % run to run)
+    R = max(1, getattr(args, "frame_repeat", 1))
     t0 = time.perf_counter()
-    for i in range(T):
-        _, _, hands = isl.call(rgb[i][:, :, ::-1])
-        crops += len(hands)
-    dt = time.perf_counter() - t0
+    for _ in range(R):
+        for i in range(T):
+            _, _, hands = isl.call(rgb[i][:, :, ::-1])
+            crops += len(hands)
+    dt = (time.perf_counter() - t0) / R
+    crops /= R
     t0 = time.perf_counter()
     for i in range(T):
         f = rgb[i][:, :, ::-1]
@@ -226,7 +230,7 @@ def frame(args):
     return {"config": "FRAME ISLSignPos.call per 1080x1920 frame (extract_features_mp.py:130 pattern)",
             "body_conv_launches_per_frame": body_launches,
             "hand_conv_launches_last_scale": hand_launches,
-            "frames": T, "frames_per_s": round(T / dt, 2), "ms_per_frame": round(dt / T * 1e3, 3),
+            "frames": T, "passes": R, "frames_per_s": round(T / dt, 2), "ms_per_frame": round(dt / T * 1e3, 3),
             "body_ms_per_frame": round(db / T * 1e3, 3), "hand_ms_per_frame": round((dt - db) / T * 1e3, 3),
             "hand_crops_per_frame": round(crops / T, 2),
             "crop_width_px": [int(min(widths)), int(max(widths))] if widths else [],
@@ -274,6 +278,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", choices=["c3", "c4", "c5", "c6", "frame", "all"], default="all")
     ap.add_argument("--frame-count", type=int, default=64, help="FRAME: sequential per-frame calls timed")
+    ap.add_argument("--frame-repeat", type=int, default=4, help="FRAME: timed passes over the frames")
     ap.add_argument("--batch", type=int, default=16, help="C3 / C4 frames per step")
     ap.add_argument("--c5-batch", type=int, default=32, help="C5 frames per pipeline batch")
     ap.add_argument("--steps", type=int, default=3)

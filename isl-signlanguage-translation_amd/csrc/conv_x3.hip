@@ -114,6 +114,7 @@ struct X3Args {
   // pixels, blocks [nb_full, nblocks) the frame's rest in tail_tiles tiles of ttpx pixels (0: one
   // tiling of px_tiles tiles)
   int nb_full, full_tiles, tail_tiles, ttpx;
+  int* tile_cnt;                // VAR 2048: the last block of a tile reduces it (ConvLaunch::tile_cnt), or null
 };
 
 // u / d for 0 <= u < 2^20, d >= 1, through the fp32 reciprocal r = 1/d: (u + 0.5) / d sits
@@ -158,6 +159,87 @@ __device__ __forceinline__ void x3_split8(const f32x4& a, const f32x4& b, f16x8&
     hi[2 * k] = h.x; hi[2 * k + 1] = h.y;
     lo[2 * k] = l.x; lo[2 * k + 1] = l.y;
   }
+}
+
+// Split-K reduction: the ranges' sums added in range order (the order of the in-block
+// ranges, so both give the same bits), then the epilogue of conv_x3_f16 (x 2^-s,
+// bias, activation, range check, masked stores).  One thread per (frame, chunk, pixel,
+// 4-channel half): neighbouring lanes read the two halves of a pixel's 32-byte chunk, so a
+// wave's loads and stores are contiguous.  The ranges' loads are all issued before the first
+// add (up to 8 in flight; the batch-1 frames' reduces had waited on one range at a time:
+// 5.0 us per launch at 23x41).
+// x3_canonical_order: ranges [0, h) summed in order, ranges [h, S) in order, then the two
+// halves, h = ceil(S / 2) -- the order of the in-block ranges (one or two K groups)
+template <int S>
+__device__ __forceinline__ f32x4 x3_sum_ranges(const float* p, size_t stride) {
+  f32x4 part[S];
+#pragma unroll
+  for (int k = 0; k < S; ++k) part[k] = __builtin_nontemporal_load((const f32x4*)(p + k * stride));
+  constexpr int H = (S + 1) / 2;
+  f32x4 lo = f32x4{0.f, 0.f, 0.f, 0.f}, hi = lo;   // onto +0, as the in-block sums
+#pragma unroll
+  for (int k = 0; k < H; ++k) lo += part[k];
+  if constexpr (S > H) {
+#pragma unroll
+    for (int k = H; k < S; ++k) hi += part[k];
+    return lo + hi;
+  }
+  return lo;
+}
+
+// one (frame n, chunk cc, pixel m, 4-channel half h) of the reduction
+__device__ __forceinline__ void x3_reduce_item(const X3Args& a, int n, int cc, int m, int h) {
+  const int HW = a.H * a.W, c8 = (a.cout + 7) / 8;
+  const int co = 8 * cc + 4 * h;
+  if (co >= a.cout) return;
+  const size_t plane = (size_t)HW * 8;
+  const float* p = a.ws + ((size_t)n * c8 + cc) * plane + (size_t)m * 8 + 4 * h;
+  const size_t split_stride = (size_t)a.nfr * c8 * plane;
+  // the epilogue's operands requested with the partials, not one round trip after them
+  const f32x4 b = *(const f32x4*)(a.bias + co);
+  const f32x4 sl = a.act == ACT_PRELU ? *(const f32x4*)(a.slope + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 sum;
+  switch (a.ksplit) {   // uniform: one straight-line body per range count (loads in flight together)
+    case 2: sum = x3_sum_ranges<2>(p, split_stride); break;
+    case 3: sum = x3_sum_ranges<3>(p, split_stride); break;
+    case 4: sum = x3_sum_ranges<4>(p, split_stride); break;
+    case 5: sum = x3_sum_ranges<5>(p, split_stride); break;
+    case 6: sum = x3_sum_ranges<6>(p, split_stride); break;
+    case 7: sum = x3_sum_ranges<7>(p, split_stride); break;
+    case 8: sum = x3_sum_ranges<8>(p, split_stride); break;
+    default: {
+      const int hh = (a.ksplit + 1) / 2;
+      f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
+      sum = hi;
+      for (int k = 0; k < hh; ++k) sum += *(const f32x4*)(p + k * split_stride);
+      for (int k = hh; k < a.ksplit; ++k) hi += *(const f32x4*)(p + k * split_stride);
+      if (a.ksplit > hh) sum += hi;
+    }
+  }
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = sum[e] * a.wscale_inv + b[e];
+  if (a.act == ACT_RELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+  } else if (a.act == ACT_PRELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
+  }
+  bool bad = false;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bad |= co + e < a.cout && !(__builtin_fabsf(v[e]) < 65504.f);
+  const int y = m / a.W, x = m - y * a.W, Wo = a.W + 2 * a.out_pad;
+  float* oc = a.out + (size_t)n * a.out_fs + (size_t)cc * a.out_chs +
+              (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8 + 4 * h;
+  if (co + 3 < a.cout) {
+    *(f32x4*)oc = v;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (co + e < a.cout) oc[e] = v[e];
+  }
+  if (bad) atomicOr(a.range_flag, 1);
 }
 
 // input segment capacity in pixels for a BPX-pixel tile (host: tile_pixels)
@@ -1065,6 +1147,33 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
         }
       }
     }
+    if (a.tile_cnt) {
+      // No reduce launch: the last of the tile's ksplit blocks to arrive sums the tile's
+      // partials (x3_reduce_item: x3_splitk_reduce's order and epilogue, the same bits).
+      // Release: this block's partials visible at agent scope (the XCDs' L2s are not
+      // coherent) before its arrival is counted; acquire before the last block reads the
+      // others'.  No block waits on another: the grid drains whatever the arrival order.
+      __shared__ int s_last;
+      __threadfence();
+      __syncthreads();
+      if (tid == 0) {
+        int* cnt = a.tile_cnt + bid;   // (bid: the tile, ranges divided out above)
+        const int old = atomicAdd(cnt, 1);
+        s_last = old == a.ksplit - 1;
+        if (s_last) atomicExch(cnt, 0);   // zero again for the next launch
+      }
+      __syncthreads();
+      if (s_last) {
+        __threadfence();
+        const int c8 = (a.cout + 7) / 8, cc0 = co_t * BCO / 8, cc1 = min(c8, cc0 + BCO / 8);
+        const int npx = mlast - m0 + 1, items = (cc1 - cc0) * npx * 2;
+        for (int it = tid; it < items; it += NT) {
+          const int h = it & 1, q = it >> 1;
+          const int px = q % npx, cc = cc0 + q / npx;
+          x3_reduce_item(a, n, cc, m0 + px, h);
+        }
+      }
+    }
     return;
   }
   if constexpr (FUSE67) {
@@ -1453,32 +1562,6 @@ double conv_x3_rgb_mfma_flops(const ConvLaunch& c) {
   return 3.0 * 2.0 * RGB_BCO * 32.0 * (double)((c.H * c.W + RGB_TILE - 1) / RGB_TILE) * RGB_TILE * c.n;
 }
 
-// Split-K reduction: the ranges' sums added in range order (the order of the in-block
-// ranges, so both give the same bits), then the epilogue of conv_x3_f16 (x 2^-s,
-// bias, activation, range check, masked stores).  One thread per (frame, chunk, pixel,
-// 4-channel half): neighbouring lanes read the two halves of a pixel's 32-byte chunk, so a
-// wave's loads and stores are contiguous.  The ranges' loads are all issued before the first
-// add (up to 8 in flight; the batch-1 frames' reduces had waited on one range at a time:
-// 5.0 us per launch at 23x41).
-// x3_canonical_order: ranges [0, h) summed in order, ranges [h, S) in order, then the two
-// halves, h = ceil(S / 2) -- the order of the in-block ranges (one or two K groups)
-template <int S>
-__device__ __forceinline__ f32x4 x3_sum_ranges(const float* p, size_t stride) {
-  f32x4 part[S];
-#pragma unroll
-  for (int k = 0; k < S; ++k) part[k] = __builtin_nontemporal_load((const f32x4*)(p + k * stride));
-  constexpr int H = (S + 1) / 2;
-  f32x4 lo = f32x4{0.f, 0.f, 0.f, 0.f}, hi = lo;   // onto +0, as the in-block sums
-#pragma unroll
-  for (int k = 0; k < H; ++k) lo += part[k];
-  if constexpr (S > H) {
-#pragma unroll
-    for (int k = H; k < S; ++k) hi += part[k];
-    return lo + hi;
-  }
-  return lo;
-}
-
 __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
   const int HW = a.H * a.W, c8 = (a.cout + 7) / 8;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -1488,56 +1571,7 @@ __global__ void __launch_bounds__(256) x3_splitk_reduce(X3Args a) {
   const int m = (int)(q % HW);
   const long long r = q / HW;
   const int cc = (int)(r % c8), n = (int)(r / c8);
-  const int co = 8 * cc + 4 * h;
-  if (co >= a.cout) return;
-  const size_t plane = (size_t)HW * 8;
-  const float* p = a.ws + ((size_t)n * c8 + cc) * plane + (size_t)m * 8 + 4 * h;
-  const size_t split_stride = (size_t)a.nfr * c8 * plane;
-  // the epilogue's operands requested with the partials, not one round trip after them
-  const f32x4 b = *(const f32x4*)(a.bias + co);
-  const f32x4 sl = a.act == ACT_PRELU ? *(const f32x4*)(a.slope + co) : f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 sum;
-  switch (a.ksplit) {   // uniform: one straight-line body per range count (loads in flight together)
-    case 2: sum = x3_sum_ranges<2>(p, split_stride); break;
-    case 3: sum = x3_sum_ranges<3>(p, split_stride); break;
-    case 4: sum = x3_sum_ranges<4>(p, split_stride); break;
-    case 5: sum = x3_sum_ranges<5>(p, split_stride); break;
-    case 6: sum = x3_sum_ranges<6>(p, split_stride); break;
-    case 7: sum = x3_sum_ranges<7>(p, split_stride); break;
-    case 8: sum = x3_sum_ranges<8>(p, split_stride); break;
-    default: {
-      const int hh = (a.ksplit + 1) / 2;
-      f32x4 hi = f32x4{0.f, 0.f, 0.f, 0.f};
-      sum = hi;
-      for (int k = 0; k < hh; ++k) sum += *(const f32x4*)(p + k * split_stride);
-      for (int k = hh; k < a.ksplit; ++k) hi += *(const f32x4*)(p + k * split_stride);
-      if (a.ksplit > hh) sum += hi;
-    }
-  }
-  f32x4 v;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = sum[e] * a.wscale_inv + b[e];
-  if (a.act == ACT_RELU) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
-  } else if (a.act == ACT_PRELU) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = v[e] >= 0.f ? v[e] : v[e] * sl[e];
-  }
-  bool bad = false;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) bad |= co + e < a.cout && !(__builtin_fabsf(v[e]) < 65504.f);
-  const int y = m / a.W, x = m - y * a.W, Wo = a.W + 2 * a.out_pad;
-  float* oc = a.out + (size_t)n * a.out_fs + (size_t)cc * a.out_chs +
-              (size_t)((y + a.out_pad) * Wo + x + a.out_pad) * 8 + 4 * h;
-  if (co + 3 < a.cout) {
-    *(f32x4*)oc = v;
-  } else {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (co + e < a.cout) oc[e] = v[e];
-  }
-  if (bad) atomicOr(a.range_flag, 1);
+  x3_reduce_item(a, n, cc, m, h);
 }
 
 
@@ -1857,11 +1891,17 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
   if constexpr (!SPLIT && !RANGED && !(VAR & 16) && BPX >= 256) x3_tail_plan(c.n, c.H * c.W, a);
+  a.tile_cnt = nullptr;
+  if constexpr (SPLIT) {
+    // the tiles' counters (ConvLaunch::tile_cnt; bid < nblocks / ksplit indexes them)
+    if (c.tile_cnt && !c.fold_out && a.nblocks / a.ksplit <= c.tile_cnt_n) a.tile_cnt = c.tile_cnt;
+  }
   hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN, VAR, OCC>), dim3(a.nblocks),
                      dim3(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1)), 0, s, a);
   if constexpr (SPLIT) {
-    // fold_out: every consumer sums the partials in its staging (X3Fold), no reduce launch
-    if (!c.fold_out) {
+    // fold_out: every consumer sums the partials in its staging (X3Fold), no reduce launch;
+    // tile_cnt: the last block of each tile reduced it
+    if (!c.fold_out && !a.tile_cnt) {
       const long long nt = (long long)c.n * ((c.cout + 7) / 8) * 2 * c.H * c.W;
       hipLaunchKernelGGL(x3_splitk_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, a);
     }

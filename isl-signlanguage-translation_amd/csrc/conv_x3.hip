@@ -114,7 +114,6 @@ struct X3Args {
   // pixels, blocks [nb_full, nblocks) the frame's rest in tail_tiles tiles of ttpx pixels (0: one
   // tiling of px_tiles tiles)
   int nb_full, full_tiles, tail_tiles, ttpx;
-  int* tile_cnt;                // VAR 2048: the last block of a tile reduces it (ConvLaunch::tile_cnt), or null
 };
 
 // u / d for 0 <= u < 2^20, d >= 1, through the fp32 reciprocal r = 1/d: (u + 0.5) / d sits
@@ -1147,33 +1146,6 @@ __global__ void __launch_bounds__(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1),
         }
       }
     }
-    if (a.tile_cnt) {
-      // No reduce launch: the last of the tile's ksplit blocks to arrive sums the tile's
-      // partials (x3_reduce_item: x3_splitk_reduce's order and epilogue, the same bits).
-      // Release: this block's partials visible at agent scope (the XCDs' L2s are not
-      // coherent) before its arrival is counted; acquire before the last block reads the
-      // others'.  No block waits on another: the grid drains whatever the arrival order.
-      __shared__ int s_last;
-      __threadfence();
-      __syncthreads();
-      if (tid == 0) {
-        int* cnt = a.tile_cnt + bid;   // (bid: the tile, ranges divided out above)
-        const int old = atomicAdd(cnt, 1);
-        s_last = old == a.ksplit - 1;
-        if (s_last) atomicExch(cnt, 0);   // zero again for the next launch
-      }
-      __syncthreads();
-      if (s_last) {
-        __threadfence();
-        const int c8 = (a.cout + 7) / 8, cc0 = co_t * BCO / 8, cc1 = min(c8, cc0 + BCO / 8);
-        const int npx = mlast - m0 + 1, items = (cc1 - cc0) * npx * 2;
-        for (int it = tid; it < items; it += NT) {
-          const int h = it & 1, q = it >> 1;
-          const int px = q % npx, cc = cc0 + q / npx;
-          x3_reduce_item(a, n, cc, m0 + px, h);
-        }
-      }
-    }
     return;
   }
   if constexpr (FUSE67) {
@@ -1891,17 +1863,11 @@ static hipError_t launch_t(const ConvLaunch& c, hipStream_t s) {
   if (nb <= 0 || nb > 0x7fffffff) { set_error("conv_x3: bad grid"); return hipErrorInvalidValue; }
   a.nblocks = (int)nb;
   if constexpr (!SPLIT && !RANGED && !(VAR & 16) && BPX >= 256) x3_tail_plan(c.n, c.H * c.W, a);
-  a.tile_cnt = nullptr;
-  if constexpr (SPLIT) {
-    // the tiles' counters (ConvLaunch::tile_cnt; bid < nblocks / ksplit indexes them)
-    if (c.tile_cnt && !c.fold_out && a.nblocks / a.ksplit <= c.tile_cnt_n) a.tile_cnt = c.tile_cnt;
-  }
   hipLaunchKernelGGL((conv_x3_f16<KS, WAVES_M, WAVES_N, WM, WN, VAR, OCC>), dim3(a.nblocks),
                      dim3(WAVES_M * WAVES_N * 64 * ((VAR & 32) ? 2 : 1)), 0, s, a);
   if constexpr (SPLIT) {
-    // fold_out: every consumer sums the partials in its staging (X3Fold), no reduce launch;
-    // tile_cnt: the last block of each tile reduced it
-    if (!c.fold_out && !a.tile_cnt) {
+    // fold_out: every consumer sums the partials in its staging (X3Fold), no reduce launch
+    if (!c.fold_out) {
       const long long nt = (long long)c.n * ((c.cout + 7) / 8) * 2 * c.H * c.W;
       hipLaunchKernelGGL(x3_splitk_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, a);
     }

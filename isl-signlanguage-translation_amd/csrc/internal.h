@@ -74,12 +74,6 @@ struct ConvLaunch {
   // by folding consumers, so its x3_splitk_reduce launch is skipped (a producer).
   const X3Fold* fold = nullptr;
   int fold_out = 0;
-  // Split-K across blocks without the reduce launch (conv_x3 VAR 2048): per tile a counter
-  // (zero between launches); the last of a tile's ksplit blocks to arrive sums the tile's
-  // partials in x3_splitk_reduce's order and applies its epilogue.  null = the reduce launch;
-  // tile_cnt_n = the counters available.
-  int* tile_cnt = nullptr;
-  int tile_cnt_n = 0;
 
   // The fused 1x1 pair (conv_x3 VAR 16; Mconv6 -> Mconv7 of a stage, model.py:108-109):
   // cout7 > 0 makes this launch the pair.  The fields above describe Mconv6 (wx3 packed for a

@@ -237,9 +237,6 @@ struct isl_net {
     hipEvent_t tab_ev = nullptr;
     float* ks = nullptr;
     size_t ks_floats = 0;
-    // per-tile arrival counters of the split-K launches without a reduce (ConvLaunch::tile_cnt;
-    // zero between launches: each tile's last block clears its own)
-    int* tcnt = nullptr;
     // split-K fold plan for the current batch size (plan_fold): per op, the offset of a
     // producer's partial sums in fold_mem (-1: none) and of a consumer's X3Fold table in
     // fold_tab (-1: none)
@@ -990,7 +987,6 @@ static void drop_arena(isl_net* net, std::map<long long, isl_net::Arena>::iterat
   }
   if (it->second.tab_pin) (void)hipHostFree(it->second.tab_pin);
   if (it->second.ks) (void)hipFree(it->second.ks);
-  if (it->second.tcnt) (void)hipFree(it->second.tcnt);
   if (it->second.fold_mem) (void)hipFree(it->second.fold_mem);
   if (it->second.fold_tab) (void)hipFree(it->second.fold_tab);
   net->plans_bytes -= it->second.bytes;
@@ -1290,23 +1286,6 @@ static int plan_fold(isl_net* net, hipStream_t s) {
   return ISL_OK;
 }
 
-// Split-K launches that finish their tiles in the last block instead of a x3_splitk_reduce
-// launch (37 fewer launches per batch-1 Mode R net, the same bits: 171/171 -m gpu tests).
-// Rejected: batch-1 Mode R 392-395 vs 643-646 frames/s (profiles/r06/fx1/).  The agent-scope
-// release every block needs before its arrival is counted (the XCDs' L2s are not coherent)
-// is a write-back of its XCD's whole L2 (buffer_wbl2 sc1), which costs far more than the
-// reduce launch.  Development build only: ISLPOSE_X3_FIXUP=1 (read per launch, part of the
-// graph run key).
-static bool fixup_enabled() {
-#ifdef ISLPOSE_DEV
-  const char* e = getenv("ISLPOSE_X3_FIXUP");
-  return e && e[0] == '1';
-#else
-  return false;
-#endif
-}
-constexpr int kTileCounters = 4096;   // split-K tiles per launch (small grids: < one block per CU)
-
 static int run_ops_eager(isl_net* net, hipStream_t s) {
   isl_net::TimedRun* tr = nullptr;
   if (net->timing) {
@@ -1530,15 +1509,6 @@ static int run_ops_eager(isl_net* net, hipStream_t s) {
       }
       L.ws = ar.ks;
       L.ws_floats = ar.ks_floats;
-      if (need > 0 && fixup_enabled()) {
-        if (!ar.tcnt) {
-          if (net->capturing) return fail(ISL_E_STATE, "graph capture: tile counter allocation");
-          HIP_OK(hipMalloc(&ar.tcnt, kTileCounters * sizeof(int)));
-          HIP_OK(hipMemsetAsync(ar.tcnt, 0, kTileCounters * sizeof(int), s));   // stream-ordered
-        }
-        L.tile_cnt = ar.tcnt;
-        L.tile_cnt_n = kTileCounters;
-      }
       if (far.fold_ws_off[k] >= 0) {   // a fold producer: its own partial-sum region, no reduce
         L.ws = far.fold_mem + far.fold_ws_off[k];
         L.ws_floats = need;
@@ -1589,7 +1559,7 @@ static const char* const kRunKeySwitches[] = {
     "ISLPOSE_X3_TILES",  "ISLPOSE_X3_UNION", "ISLPOSE_X3_HALF64",  "ISLPOSE_X3_WIDE7",   "ISLPOSE_X3_ACROSS",
     "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67", "ISLPOSE_X3_G2", "ISLPOSE_X3_PX64", "ISLPOSE_X3_HALFSMALL",
     "ISLPOSE_X3_WR",     "ISLPOSE_X3_WR_WN", "ISLPOSE_C12",        "ISLPOSE_X3_TAIL",    "ISLPOSE_X3_SMALL7",
-    "ISLPOSE_X3_W2",     "ISLPOSE_X3_FIXUP",
+    "ISLPOSE_X3_W2",
 #ifdef ISLPOSE_DEV
     "ISLPOSE_X3_HALFCO", "ISLPOSE_X3_PPS2",  "ISLPOSE_X3_M16",     "ISLPOSE_X3_WINO",    "ISLPOSE_X3_ABL",
 #endif
@@ -1843,7 +1813,6 @@ int isl_net_destroy(isl_net* net) {
     if (kv.second.tab_pin) (void)hipHostFree(kv.second.tab_pin);
     if (kv.second.tab) (void)hipFree(kv.second.tab);
     if (kv.second.ks) (void)hipFree(kv.second.ks);
-    if (kv.second.tcnt) (void)hipFree(kv.second.tcnt);
     if (kv.second.fold_mem) (void)hipFree(kv.second.fold_mem);
     if (kv.second.fold_tab) (void)hipFree(kv.second.fold_tab);
   }

@@ -226,10 +226,23 @@ def frame(args):
         codes = [v for _, v in net.op_variants()]
         return sum(1 for v in codes if v not in (-1, -2)) + sum(1 for v in codes if rt.decode_variant(v).get("split"))
     body_launches = launches(body.net)
-    hand_launches = launches(hand.net) if crops else 0   # (the last scale the hand net ran)
+    # the hand net's conv launches over its four scales for one crop of a frame with hands (each
+    # scale run once more, after the timed passes, to read its op variants)
+    hand_launches = 0
+    if widths:
+        from islpose.hand import BOXSIZE
+        f = rgb[0][:, :, ::-1]
+        x = isl._upload(f)
+        w0 = widths[0]
+        crop = [(0, 0, 0, w0, w0)]
+        for s in hand.scale_search:
+            gh, gw = hand.net.preprocess_crops(x, crop, s * BOXSIZE)
+            hand.net.run(torch.empty((1, 22, gh // 8, gw // 8), device=x.device))
+            torch.cuda.synchronize()
+            hand_launches += launches(hand.net)
     return {"config": "FRAME ISLSignPos.call per 1080x1920 frame (extract_features_mp.py:130 pattern)",
             "body_conv_launches_per_frame": body_launches,
-            "hand_conv_launches_last_scale": hand_launches,
+            "hand_conv_launches_per_crop_4_scales": hand_launches,
             "frames": T, "passes": R, "frames_per_s": round(T / dt, 2), "ms_per_frame": round(dt / T * 1e3, 3),
             "body_ms_per_frame": round(db / T * 1e3, 3), "hand_ms_per_frame": round((dt - db) / T * 1e3, 3),
             "hand_crops_per_frame": round(crops / T, 2),

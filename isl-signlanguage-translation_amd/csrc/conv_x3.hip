@@ -1952,6 +1952,19 @@ static bool x3_small7_deep(const ConvLaunch& c) {
   return (long long)c.n * ((c.H * c.W + tpx - 1) / tpx) * 2 * std::max(1, c.ksplit) <= device_cus();
 }
 
+// ... on 96-pixel tiles (6 waves of 32co x 32px, two steps ahead) where the 64-pixel grid takes
+// more than one round of one block per CU and the 96-pixel grid takes one: one crop at the
+// 92^2 (736 px) hand scale, 266 -> 178 blocks (the 64-pixel plain loop left 10 CUs with two
+// blocks, every layer waiting on them).  No K range is split: the same bits.
+// ISLPOSE_X3_S7W96=0 off (A/B; read per launch).
+static bool x3_small7_96(const ConvLaunch& c) {
+  const char* e = getenv("ISLPOSE_X3_S7W96");
+  if ((e && e[0] == '0') || x3_small7_mode() != 2 || c.ksplit > 1) return false;
+  const long long HW = (long long)c.H * c.W, cus = device_cus();
+  const int t64 = tile_pixels(c, 64, x3_segmax(64)), t96 = tile_pixels(c, 96, x3_segmax(96));
+  return c.n * ((HW + t64 - 1) / t64) * 2 > cus && c.n * ((HW + t96 - 1) / t96) * 2 <= cus;
+}
+
 // Small grids (the 128-pixel family) with two K groups per block (VAR 32, 16 waves: the first
 // and second half of the canonical K ranges side by side, one block per CU): every 128-channel
 // 1x1 / 3x3 launch whose K ranges run in one block (Mode R's 23x41 stage layers and conv4_x at
@@ -2265,6 +2278,7 @@ static hipError_t launch_ks(const ConvLaunch& c, hipStream_t s) {
     // slabs; 8 waves measured 2-6 % over 4 waves of 64co x 64px / x 128px)
     if (c.ksplit <= 1 && c.bco == 128) {
       if (x3_small7(c)) {   // 64co x 64px blocks (=2: the steps' operands two steps ahead)
+        if (x3_small7_96(c)) return launch_t<KS, 2, 3, 1, 1, 256 | 128, 1>(c, s);
         if (x3_small7_deep(c)) return launch_t<KS, 2, 2, 1, 1, 256 | 128, 1>(c, s);
         return launch_t<KS, 2, 2, 1, 1, 256, 4>(c, s);
       }

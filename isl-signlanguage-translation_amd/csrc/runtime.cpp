@@ -1559,7 +1559,7 @@ static const char* const kRunKeySwitches[] = {
     "ISLPOSE_X3_TILES",  "ISLPOSE_X3_UNION", "ISLPOSE_X3_HALF64",  "ISLPOSE_X3_WIDE7",   "ISLPOSE_X3_ACROSS",
     "ISLPOSE_X3_S8",     "ISLPOSE_X3_FUSE67", "ISLPOSE_X3_G2", "ISLPOSE_X3_PX64", "ISLPOSE_X3_HALFSMALL",
     "ISLPOSE_X3_WR",     "ISLPOSE_X3_WR_WN", "ISLPOSE_C12",        "ISLPOSE_X3_TAIL",    "ISLPOSE_X3_SMALL7",
-    "ISLPOSE_X3_W2",
+    "ISLPOSE_X3_W2",     "ISLPOSE_X3_S7W96",
 #ifdef ISLPOSE_DEV
     "ISLPOSE_X3_HALFCO", "ISLPOSE_X3_PPS2",  "ISLPOSE_X3_M16",     "ISLPOSE_X3_WINO",    "ISLPOSE_X3_ABL",
 #endif

@@ -175,7 +175,9 @@ def test_small7_half_channel_bit_identical(hest, side, monkeypatch):
     64-pixel tiles with their operands two steps ahead (conv_x3.hip x3_small7, VAR 256 | 128;
     the 23^2 scale with its across-block K ranges) == the same blocks one step ahead
     (ISLPOSE_X3_SMALL7=1) == the 128-pixel blocks (=0) bit for bit, and the crop alone == the
-    crop inside a batch of 8.  (92^2: 266 blocks, past one round: one step ahead.)"""
+    crop inside a batch of 8.  (92^2: 266 64-pixel blocks, past one round: 96-pixel tiles two
+    steps ahead, 178 blocks, x3_small7_96; ISLPOSE_X3_S7W96=0 gives the 64-pixel blocks one
+    step ahead, the same bits.)"""
     from islpose import runtime as rt
     x = torch.from_numpy(np.ascontiguousarray(
         np.transpose(synth.synth_frames(8, side, side, seed=side + 1).astype(np.float32), (0, 3, 1, 2)) / 256 - 0.5)).cuda()
@@ -183,16 +185,20 @@ def test_small7_half_channel_bit_identical(hest, side, monkeypatch):
     h1 = hest.net.forward(x[:1]).clone()
     var = [rt.decode_variant(v) for name, v in hest.net.op_variants()
            if name.startswith("Mconv") and "Mconv6" not in name and "Mconv7" not in name]
-    assert len(var) == 25 and all(d["ks"] == 7 and d["var"] & 256 and d["bpx"] == 64 for d in var), var[:2]
-    # operands two steps ahead where the 64-pixel grid fits one block per CU (x3_small7_deep)
-    assert all(bool(d["var"] & 128) == (side != 736) for d in var), var[:2]
+    want_bpx = 96 if side == 736 else 64
+    assert len(var) == 25 and all(d["ks"] == 7 and d["var"] & 256 and d["bpx"] == want_bpx for d in var), var[:2]
+    # operands two steps ahead where the grid fits one block per CU (x3_small7_deep / _96)
+    assert all(d["var"] & 128 for d in var), var[:2]
     h8 = hest.net.forward(x).clone()
+    monkeypatch.setenv("ISLPOSE_X3_S7W96", "0")
+    h64 = hest.net.forward(x[:1]).clone()
+    monkeypatch.delenv("ISLPOSE_X3_S7W96")
     monkeypatch.setenv("ISLPOSE_X3_SMALL7", "1")
     hs = hest.net.forward(x[:1]).clone()
     monkeypatch.setenv("ISLPOSE_X3_SMALL7", "0")
     h0 = hest.net.forward(x[:1]).clone()
     torch.cuda.synchronize()
-    assert torch.equal(h1, h0) and torch.equal(h1, hs)
+    assert torch.equal(h1, h0) and torch.equal(h1, hs) and torch.equal(h1, h64)
     assert torch.equal(h1[0], h8[0])
 
 

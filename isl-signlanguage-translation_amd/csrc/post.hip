@@ -1548,40 +1548,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) l
     if (MODE == 0) score_range(0, np);
     __shared__ int s_ord[LIMB_MAXP];
     __shared__ unsigned char s_uA[LIMB_MAXPK], s_uB[LIMB_MAXPK];
-    constexpr int PJ = LIMB_MAXP / 256;            // pairs per thread (p = tid + 256 j)
-    const int nj = (np + 255) / 256;
-    double sp[PJ];
-    bool kp[PJ];
-    int rk[PJ];
-#pragma unroll
-    for (int j = 0; j < PJ; ++j) {
-      const int p = tid + 256 * j;
-      kp[j] = j < nj && p < np && pkeep[p];
-      sp[j] = kp[j] ? pscore[p] : 0.0;
-      rk[j] = 0;
+    // The stable descending sort (sorted(..., reverse=True)) as a bitonic sort in LDS on (score,
+    // pair): a before b iff score_a > score_b or (equal and a < b) -- a strict total order, so the
+    // permutation the rank count gave.  Pairs not kept (and the padding to a power of two) sort
+    // last as -inf.  (The rank count, O(np^2 / 256) per thread: limb scoring 215 us per 1080p
+    // frame, profiles/r06/lk1/.)
+    __shared__ double s_key[LIMB_MAXP];
+    int N = 2;
+    while (N < np) N <<= 1;
+    __syncthreads();   // s_nkeep zeroed
+    for (int i = tid; i < N; i += 256) {
+      const bool kept = i < np && pkeep[i];
+      s_key[i] = kept ? pscore[i] : -INFINITY;
+      s_ord[i] = i;
+      if (kept) atomicAdd(&s_nkeep, 1);
     }
-    // kept scores are > 0, so a staged -1 (not kept) is never better than a kept pair
-    for (int q0 = 0; q0 < np; q0 += LIMB_ITEMS) {
-      const int qc = min(LIMB_ITEMS, np - q0);
-      for (int i = tid; i < qc; i += 256) s_item[i] = pkeep[q0 + i] ? pscore[q0 + i] : -1.0;
-      __syncthreads();
-      for (int i = 0; i < qc; ++i) {
-        const double v = s_item[i];
-        const int q = q0 + i;
-#pragma unroll
-        for (int j = 0; j < PJ; ++j)
-          if (j < nj) rk[j] += (v > sp[j] || (v == sp[j] && q < tid + 256 * j)) ? 1 : 0;
+    __syncthreads();
+    for (int size = 2; size <= N; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int t = tid; t < N / 2; t += 256) {
+          const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+          const double ki = s_key[i], kj = s_key[j];
+          const int oi = s_ord[i], oj = s_ord[j];
+          const bool j_first = kj > ki || (kj == ki && oj < oi);
+          if (((i & size) == 0) == j_first) {   // (i & size) == 0: this run sorts first-to-last
+            s_key[i] = kj; s_key[j] = ki;
+            s_ord[i] = oj; s_ord[j] = oi;
+          }
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
-    // the order and the sorted scores (ranks < LIMB_ITEMS) for the greedy
-#pragma unroll
-    for (int j = 0; j < PJ; ++j)
-      if (kp[j]) {
-        s_ord[rk[j]] = tid + 256 * j;
-        if (rk[j] < LIMB_ITEMS) s_item[rk[j]] = sp[j];
-        atomicAdd(&s_nkeep, 1);
-      }
     for (int i = tid; i < nA; i += 256) s_uA[i] = 0;
     for (int j = tid; j < nB; j += 256) s_uB[j] = 0;
     __syncthreads();
@@ -1598,7 +1595,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) l
         double* c = cw + (size_t)m * 5;
         c[0] = (double)(s_offA + i);
         c[1] = (double)(s_offB + j);
-        c[2] = r < LIMB_ITEMS ? s_item[r] : pscore[p];
+        c[2] = s_key[r];   // (the pair's pscore, moved with it)
         c[3] = (double)i;
         c[4] = (double)j;
         ++m;

@@ -1178,51 +1178,59 @@ __global__ void __launch_bounds__(256) compact_kernel(const unsigned long long* 
   const T* src = planes + (size_t)plane * H * W;
   char* rec = result + (size_t)f * lay.record_bytes;
   double* peaks = (double*)(rec + lay.peaks) + (size_t)part * max_peaks * 3;
-  __shared__ int s_scan[256];
+  // Raster order (np.nonzero): each thread owns CW consecutive words of a round, its peaks
+  // go after those of the lower threads (a wave prefix by shuffles, the four wave totals in
+  // LDS), rounds in order.  (The 256-wide Hillis-Steele scan of 1024 words per round was 16
+  // barriers per round: 57 us per 1080p frame of mostly empty rounds, profiles/r06/lk/.)
+  constexpr int CW = 8;
+  __shared__ int s_w[4];
   __shared__ int s_base;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nw = H * words;
   if (tid == 0) s_base = 0;
   __syncthreads();
-  for (int w0 = 0; w0 < nw; w0 += 256 * 4) {
-    // each thread owns 4 consecutive words
-    unsigned long long wv[4];
+  for (int w0 = 0; w0 < nw; w0 += 256 * CW) {
+    unsigned long long wv[CW];
     int cnt = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int wi = w0 + tid * 4 + k;
+    for (int k = 0; k < CW; ++k) {
+      const int wi = w0 + tid * CW + k;
       wv[k] = wi < nw ? mk[wi] : 0ull;
       cnt += __popcll(wv[k]);
     }
-    s_scan[tid] = cnt;
-    __syncthreads();
-    for (int off = 1; off < 256; off <<= 1) {   // inclusive Hillis-Steele scan
-      const int v = tid >= off ? s_scan[tid - off] : 0;
-      __syncthreads();
-      s_scan[tid] += v;
-      __syncthreads();
-    }
-    int pos = s_base + s_scan[tid] - cnt;
+    int inc = cnt;   // inclusive prefix over the wave
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int wi = w0 + tid * 4 + k;
-      unsigned long long w = wv[k];
-      while (w) {
-        const int b = __ffsll((long long)w) - 1;
-        w &= w - 1;
-        const int y = wi / words, x = (wi - y * words) * 64 + b;
-        if (pos < max_peaks) {
-          double* p = peaks + (size_t)pos * 3;
-          p[0] = (double)x;
-          p[1] = (double)y;
-          if constexpr (FUSED) p[2] = (double)sample(m, f, part, y, x);
-          else p[2] = (double)src[(size_t)y * W + x];
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += y;
+    }
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    int pos = s_base + inc - cnt;
+    for (int q = 0; q < wave; ++q) pos += s_w[q];
+    const int round_total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    if (cnt) {
+#pragma unroll
+      for (int k = 0; k < CW; ++k) {
+        const int wi = w0 + tid * CW + k;
+        unsigned long long w = wv[k];
+        while (w) {
+          const int b = __ffsll((long long)w) - 1;
+          w &= w - 1;
+          const int y = wi / words, x = (wi - y * words) * 64 + b;
+          if (pos < max_peaks) {
+            double* p = peaks + (size_t)pos * 3;
+            p[0] = (double)x;
+            p[1] = (double)y;
+            if constexpr (FUSED) p[2] = (double)sample(m, f, part, y, x);
+            else p[2] = (double)src[(size_t)y * W + x];
+          }
+          ++pos;
         }
-        ++pos;
       }
     }
-    __syncthreads();
-    if (tid == 255) s_base += s_scan[255];
+    __syncthreads();   // every thread has read s_base and s_w
+    if (tid == 0) s_base += round_total;
     __syncthreads();
   }
   if (tid == 0) {

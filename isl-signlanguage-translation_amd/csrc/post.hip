@@ -1590,25 +1590,52 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) l
     for (int i = tid; i < nA; i += 256) s_uA[i] = 0;
     for (int j = tid; j < nB; j += 256) s_uB[j] = 0;
     __syncthreads();
-    if (tid == 0) {
+    // The greedy (body.py:166-175) on wave 0, 64 sorted pairs at a time: every lane loads its
+    // pair and drops it if an endpoint is already used; the survivors are then taken in order
+    // by the whole wave (lowest lane first), each re-checked against the pairs accepted before
+    // it in this batch.  The same accepts in the same order as one thread walking the list.
+    if ((tid >> 6) == 0) {
+      const int lane = tid & 63;
+      volatile unsigned char* uA = s_uA;
+      volatile unsigned char* uB = s_uB;
       double* cw = conns + (size_t)k * a.max_conns * 5;
-      const int lim = nA < nB ? nA : nB;
+      const int lim = nA < nB ? nA : nB, nkeep = s_nkeep;
       int m = 0;
-      for (int r = 0; r < s_nkeep && m < lim; ++r) {
-        const int p = s_ord[r];
-        const int i = p / nB, j = p - i * nB;
-        if (s_uA[i] || s_uB[j]) continue;
-        s_uA[i] = s_uB[j] = 1;
-        if (m >= a.max_conns) { atomicExch(status, ISL_E_CAPACITY); break; }
-        double* c = cw + (size_t)m * 5;
-        c[0] = (double)(s_offA + i);
-        c[1] = (double)(s_offB + j);
-        c[2] = s_key[r];   // (the pair's pscore, moved with it)
-        c[3] = (double)i;
-        c[4] = (double)j;
-        ++m;
+      bool full = false;
+      for (int r0 = 0; r0 < nkeep && m < lim && !full; r0 += 64) {
+        const int r = r0 + lane;
+        int i = 0, j = 0;
+        bool cand = false;
+        if (r < nkeep) {
+          const int p = s_ord[r];
+          i = p / nB;
+          j = p - i * nB;
+          cand = !uA[i] && !uB[j];
+        }
+        unsigned long long live = __ballot(cand);
+        while (live && m < lim) {
+          const int l = __builtin_ctzll(live);
+          live &= live - 1;
+          const int il = __shfl(i, l, 64), jl = __shfl(j, l, 64);
+          if (uA[il] || uB[jl]) continue;          // taken by an earlier pair of this batch
+          if (m >= a.max_conns) {
+            if (lane == 0) atomicExch(status, ISL_E_CAPACITY);
+            full = true;
+            break;
+          }
+          if (lane == 0) {
+            uA[il] = 1;
+            uB[jl] = 1;
+          }
+          if (lane < 5) {
+            double* c = cw + (size_t)m * 5;
+            c[lane] = lane == 0 ? (double)(s_offA + il) : lane == 1 ? (double)(s_offB + jl)
+                    : lane == 2 ? s_key[r0 + l] : lane == 3 ? (double)il : (double)jl;
+          }
+          ++m;
+        }
       }
-      n_conns[k] = m;
+      if (lane == 0) n_conns[k] = m;
     }
     return;
   } else if (MODE == 0) {

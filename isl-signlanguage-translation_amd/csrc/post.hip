@@ -3443,10 +3443,12 @@ extern "C" int isl_body_post(isl_net* net, int n, int H, int W, int nscales, con
   // a frame per call: the scoring over Z blocks per limb (MODE 1), then ranks and matches (MODE 2);
   // ISLPOSE_LIMB_SPLIT=0: one block per limb (A/B; read per call)
   const char* lse = getenv("ISLPOSE_LIMB_SPLIT");
-  // ISLPOSE_LIMB_Z=z: z blocks per limb (A/B; read per call)
+  // ISLPOSE_LIMB_Z=z: z blocks per limb (A/B; read per call).  A 1080p frame's scoring: 10 / 32 /
+  // 64 blocks per limb 70.7 / 34.5 / 40.5 us (profiles/r06/lk/lz/); each pair is scored whole
+  // by one block, so the slicing changes no sum
   const char* lzs = getenv("ISLPOSE_LIMB_Z");
   const int lz = (lse && lse[0] == '0') || n * nlimbs >= 128 ? 1
-                 : lzs ? std::max(1, std::min(64, atoi(lzs))) : std::min(16, 256 / (n * nlimbs));
+                 : lzs ? std::max(1, std::min(64, atoi(lzs))) : std::max(1, std::min(32, 1024 / (n * nlimbs)));
   if (lz > 1) {
     hipLaunchKernelGGL(limb_kernel<1>, dim3(nlimbs, n, lz), dim3(256), 0, s, ga);
     hipLaunchKernelGGL(limb_kernel<2>, dim3(nlimbs, n), dim3(256), 0, s, ga);
